@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X lattice decoder (BASELINE.json metric).
+
+One step = one decode of a 64K-sentence synthetic batch (BASELINE.json config
+3: 20 eojeols x 2-5 characters, full-dictionary lattice statistics, 1M-key
+trigram model, RegularizationScore + SimpleTrigramFeatureScore, beam k=1 =
+Viterbi) that is already resident in HBM: decode kernel (incl. backtrace) +
+D2H of the results into pinned host memory + stream sync.  Lattice build and
+packing happen before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--k 1] [--sentences 65536]
+
+N > 1 is launched by torch.distributed.run (one process per GPU); each rank
+decodes its own 64K-sentence shard (weak scaling, no data-path collective),
+ranks are timed between barriers and the max over ranks is reported.
+Rank 0 prints one JSON line.
+"""
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+# Load the HIP library before anything that could pull another HIP runtime in.
+from lattice_based_tagger_amd import _capi, synth  # noqa: E402
+
+METRIC = 'sentences/sec Viterbi decode, 64K-sentence batch; achieved HBM GB/s vs 8 TB/s'
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--k', type=int, default=1, help='beam size (1 = Viterbi headline)')
+    ap.add_argument('--sentences', type=int, default=65536)
+    ap.add_argument('--features', type=int, default=1_000_000)
+    ap.add_argument('--cpu-seconds', type=float, default=10.0,
+                    help='budget of the pure-Python CPU baseline sample')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--seed', type=int, default=0)
+    return ap.parse_args()
+
+
+class Dist:
+    """Rank bookkeeping; gloo process group for barrier / max (host only)."""
+
+    def __init__(self, want):
+        self.rank = int(os.environ.get('RANK', 0))
+        self.world = int(os.environ.get('WORLD_SIZE', 1))
+        self.local = int(os.environ.get('LOCAL_RANK', 0))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist          # after liblt is loaded
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            dist.init_process_group('gloo', rank=self.rank, world_size=self.world)
+            self.pg = dist
+        if want != self.world and self.rank == 0:
+            print('warning: --gpus %d but WORLD_SIZE %d' % (want, self.world), file=sys.stderr)
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, v):
+        if not self.pg:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v):
+        if not self.pg:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+def make_workload(n_sent, seed, n_features):
+    raw = synth.make_lattices(n_sent, seed=seed)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=seed, n_features=n_features)
+    packed, keys, coefs = synth.pack_fast(raw, sm, lay, cols)
+    return raw, lay, sm, packed, keys, coefs
+
+
+def reachable_dict_nodes(raw):
+    """Dictionary candidates on spans <= 8 inside the sentence (all generated ones)."""
+    return int(len(raw.word))
+
+
+def algorithmic_bytes(raw, packed, tuples, length, k):
+    """B = 32*N + 8*(8n+1) + 4*8n + 24*P + 8*T*N + sum_matures (4*(L+1)+8),
+    summed over the batch (N dictionary nodes, n chars, P trigram feature tuples
+    of the reference algorithm, T = 1 node-local term, L words per mature)."""
+    n = packed.sent_n.astype(np.int64)
+    N = reachable_dict_nodes(raw)
+    T = 1
+    out = int(np.sum(4 * (length[length > 0] + 1) + 8)) if k else 0
+    out += int(np.sum(length == 0) * 0)
+    return 32 * N + int(np.sum(8 * (8 * n + 1) + 4 * 8 * n)) + 24 * tuples + 8 * T * N + out
+
+
+def cpu_baseline(raw, sm, budget_s):
+    """Pure-Python restatement of the reference beam_search (oracle/ref_beam.py,
+    1 core) on the first sentences of the same batch, ~budget_s seconds."""
+    from lattice_based_tagger_amd import score_funcs as SF, feature as FE
+    from oracle import ref_beam
+    probe_n = 256
+    sents, dic, coef = synth.to_words(raw, sm, sentences=range(probe_n))
+    funcs = SF.BeamScoreFunctions(SF.RegularizationScore(),
+                                  SF.SimpleTrigramFeatureScore(FE.SimpleTrigramEncoder(dic), coef))
+    done = 0
+    t0 = time.perf_counter()
+    for bindex, chars in sents:
+        ref_beam.beam_search(bindex, chars, funcs, beam_size=1)
+        done += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {'value': done / dt, 'unit': 'sentences/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d sentences (first of the 64K batch, %.1f chars avg), k=1, '
+                      'oracle/ref_beam.py pure-Python restatement of beam.py:5-61, %.1f s'
+                      % (done, float(raw.sent_n[:done].mean()), dt)}
+
+
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def main():
+    a = parse()
+    d = Dist(a.gpus)
+    lib = _capi.load()
+    if lib.lt_device_count() < 1:
+        raise SystemExit('bench.py: no HIP device visible')
+    t_gen = time.perf_counter()
+    raw, lay, sm, packed, keys, coefs = make_workload(a.sentences, a.seed + 1000 * d.rank, a.features)
+    t_gen = time.perf_counter() - t_gen
+    ctx = _capi.Context(d.local)
+    dm = _capi.DeviceModel(ctx, keys, coefs)
+    t_up = time.perf_counter()
+    db = _capi.DeviceBatch(ctx, packed, max_k=a.k)          # H2D, outside the timed region
+    t_up = time.perf_counter() - t_up
+    expansions, tuples, probes = db.count_ops(dm, a.k)
+
+    for _ in range(a.warmup):
+        db.launch(dm, a.k)
+        db.fetch()
+        ctx.sync()
+
+    d.barrier()
+    ctx.sync()
+    kern_ms = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        db.launch(dm, a.k)
+        db.fetch()
+        ctx.sync()
+        kern_ms.append(ctx.kernel_ms())
+    ctx.sync()
+    t1 = time.perf_counter()
+    d.barrier()
+    elapsed = d.max(t1 - t0)
+    total_sent = d.sum(float(a.sentences * a.steps))
+
+    count, length, score, codes = db.results(a.k)
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    B = algorithmic_bytes(raw, packed, tuples, length, a.k)
+    achieved = B / avg_kernel_s / 1e9
+
+    if d.rank == 0:
+        line = {
+            'metric': METRIC,
+            'value': total_sent / elapsed,
+            'unit': 'sentences/s',
+            'n_gpus': d.world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': elapsed / a.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f64',
+            'data': 'synthetic (lattice_based_tagger_amd/synth.py, seed %d + 1000*rank)' % a.seed,
+            'config': {
+                'workload': 'config3: %d synthetic sentences/GPU, 20 eojeols x 2-5 chars, '
+                            'full-dictionary lattice stats, %d-key trigram model, '
+                            'Regularization+SimpleTrigram scorers, beam k=%d, max_len 8'
+                            % (a.sentences, a.features, a.k),
+                'sentences_per_gpu': a.sentences,
+                'beam': a.k,
+                'max_len': 8,
+                'chars_per_sentence': float(packed.sent_n.mean()),
+                'dict_nodes_per_sentence': reachable_dict_nodes(raw) / a.sentences,
+                'parallelism': 'dp%d' % d.world,
+            },
+            'roofline': {
+                'bound': 'hbm',
+                'achieved': achieved,
+                'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s',
+                'frac': achieved / HBM_PEAK_GBS,
+                'traffic': None,
+                'kernel': 'lt_decode_k',
+                'algorithmic_bytes_per_launch': B,
+                'avg_kernel_ms': avg_kernel_s * 1e3,
+            },
+            'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
+                               'table_probes': probes},
+            'kernel_only_sentences_per_s': a.sentences / avg_kernel_s,
+            'host': {'gen_s': t_gen, 'h2d_s': t_up, 'nproc': os.cpu_count(), 'cpu': cpu_model()},
+        }
+        if not a.no_cpu_baseline and d.world == 1:
+            line['cpu_baseline'] = cpu_baseline(raw, sm, a.cpu_seconds)
+        else:
+            line['cpu_baseline'] = None
+        print(json.dumps(line), flush=True)
+    db.close()
+    dm.close()
+    ctx.close()
+    d.close()
+
+
+if __name__ == '__main__':
+    main()

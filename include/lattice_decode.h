@@ -1,0 +1,154 @@
+/*
+ * lattice_decode.h -- C-ABI of the MI355X lattice decoder (liblt.so).
+ *
+ * The reference decoder is the pure-Python `beam_search(bindex, chars,
+ * score_functions, beam_size=5, max_len=8)` (lattice_tagger/beam/beam.py:5-61)
+ * driven by `Tagger.tag` (lattice_tagger/tagger/tagger.py:68-78) and scored by
+ * the plugin composite `BeamScoreFunctions` (lattice_tagger/beam/score_funcs.py:18-54)
+ * over the trigram schema of lattice_tagger/features/feature.py:76-121.
+ * The reference has no FFI; this header is the boundary a ctypes binding of
+ * that Python API binds to.  Every entry point below
+ * cites the reference interface it replaces.
+ *
+ * Conventions: plain pointers + sizes, no C++ or torch types.  All host
+ * buffers passed in are owned by the caller and only read (inputs) or written
+ * (outputs) during the call; the library never frees them.  Device memory is
+ * owned by the handles.  Functions return lt_status (0 = OK, < 0 = error);
+ * lt_last_error() returns a thread-local message for the last failure.
+ * A handle is not re-entrant: use one lt_ctx per host thread.
+ */
+#ifndef LATTICE_DECODE_H
+#define LATTICE_DECODE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LT_ABI_VERSION 1
+#define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
+#define LT_MAX_BEAM 32     /* largest beam_size compiled in */
+
+typedef int32_t lt_status;
+enum {
+  LT_OK = 0,
+  LT_EINVAL = -1,        /* bad argument / malformed batch                  */
+  LT_EHIP = -2,          /* HIP runtime error                               */
+  LT_ENOMEM = -3,        /* host or device allocation failed                */
+  LT_EUNSUPPORTED = -4,  /* configuration not compiled in (k, max_len)      */
+  LT_ERCCL = -5          /* RCCL error                                      */
+};
+
+typedef struct lt_ctx lt_ctx;
+typedef struct lt_model lt_model;
+typedef struct lt_batch lt_batch;
+
+/* ---- library ------------------------------------------------------------ */
+int lt_abi_version(void);
+const char* lt_last_error(void);
+/* Number of visible HIP devices (0 when no GPU). */
+int lt_device_count(void);
+
+/* ---- context: one device + one HIP stream ------------------------------- */
+lt_status lt_ctx_create(int device, lt_ctx** out);
+lt_status lt_ctx_destroy(lt_ctx* ctx);
+lt_status lt_sync(lt_ctx* ctx);
+
+/* ---- model: the lowered scorer composite ---------------------------------
+ * Replaces the per-expansion call `score_functions(immature, expand)`
+ * (beam.py:47 -> score_funcs.py:50-54).  Holds the probed trigram feature
+ * classes 0,1,2,3,7,8 (score_funcs.py:137-144, feature.py:95-119) as an
+ * open-addressing hash table keyed by interned component ids.
+ * keys[4*i .. 4*i+3] = {a, b, c, class}; ids are >= 1, unused components 0.
+ */
+typedef struct {
+  int64_t n_keys;
+  const uint32_t* keys;   /* [n_keys][4] */
+  const double* coefs;    /* [n_keys]  coefficient of each key (float64) */
+} lt_model_desc;
+
+lt_status lt_model_create(lt_ctx* ctx, const lt_model_desc* desc, lt_model** out);
+lt_status lt_model_destroy(lt_model* model);
+/* Hash-table slots allocated on the device (32 B each). */
+int64_t lt_model_slots(const lt_model* model);
+
+/* ---- batch: packed lattices ----------------------------------------------
+ * Replaces the `bindex` / `chars` arguments of beam_search (beam.py:5,
+ * consumed at beam.py:25-38).  Layout: DESIGN.md "Data layout in HBM".
+ *   sentence s owns local nodes [sent_node_off[s], sent_node_off[s+1]) (node 0 = BOS)
+ *   and span entries [sent_span_off[s], sent_span_off[s+1]) (= 8*n_s + 1 entries);
+ *   span_start[sent_span_off[s] + (e-1)*8 + (8-d)] = local index of the first
+ *   candidate of span (e-d, e).
+ */
+typedef struct {
+  int32_t n_sent;
+  int32_t max_len;        /* 1..8 (beam_search max_len, beam.py:5,30) */
+  int32_t n_post;         /* node-local terms that follow the trigram term */
+  int32_t has_trigram;
+  int64_t n_nodes;
+  int64_t n_span;         /* = sent_span_off[n_sent] */
+  const int32_t* sent_n;          /* [n_sent] characters per sentence */
+  const int64_t* sent_node_off;   /* [n_sent+1] */
+  const int64_t* sent_span_off;   /* [n_sent+1] */
+  const int32_t* span_start;      /* [n_span] */
+  const int32_t* node_word;       /* [n_nodes] interned ids (0 = in no key) */
+  const int32_t* node_morph0;
+  const int32_t* node_tag;
+  const uint32_t* node_mask;      /* pre-filter bits 0-15, flags 16-20 */
+  const double* node_pre;         /* node-local terms before the trigram, summed */
+  const double* node_f4;          /* coef of (4, len)                 if flag */
+  const double* node_f5;          /* coef of (5, word, tag0, is_l)    if flag */
+  const double* node_f6;          /* coef of (6, min(8, len))         if flag */
+  const double* node_post;        /* [n_post][n_nodes] or NULL */
+} lt_batch_desc;
+
+/* Copies the batch to the device (H2D) and allocates result buffers for
+ * beams up to max_k.  Blocking. */
+lt_status lt_batch_create(lt_ctx* ctx, const lt_batch_desc* desc, int max_k, lt_batch** out);
+lt_status lt_batch_destroy(lt_batch* batch);
+/* Total path-code slots of the results for beam k: k * sum_s n_s. */
+int64_t lt_batch_code_slots(const lt_batch* batch, int k);
+
+/* ---- decode ---------------------------------------------------------------
+ * Replaces beam_search(bindex, chars, score_functions, beam_size=k, max_len)
+ * (beam.py:5-61) for every sentence of the batch.  Asynchronous on the ctx
+ * stream; results stay on the device until lt_result_fetch.
+ */
+lt_status lt_decode_launch(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k);
+/* Device time of the last decode kernel (HIP events on the ctx stream), ms.
+ * Valid after lt_sync. */
+lt_status lt_last_kernel_ms(lt_ctx* ctx, float* ms);
+
+/* Results of beam_search's `matures` (beam.py:59-61), per sentence s:
+ *   count[s]               number of matures (<= k)
+ *   length[s*k + t]        words in mature t, excluding BOS/EOS
+ *   score[s*k + t]         float64 path score (after the EOS `+ 0`)
+ *   codes[k*off_s + t*n_s + j]  local node index of word j of mature t
+ *                          (off_s = sum_{s'<s} n_{s'})
+ * Matures are ordered best first, ties by expansion order (beam.py:85). */
+typedef struct {
+  int32_t* count;    /* [n_sent] */
+  int32_t* length;   /* [n_sent * k] */
+  double* score;     /* [n_sent * k] */
+  int32_t* codes;    /* [lt_batch_code_slots(batch, k)] */
+} lt_result;
+
+/* D2H of the last decode's results into library-owned pinned buffers
+ * (async on the ctx stream; complete after lt_sync). */
+lt_status lt_result_fetch(lt_ctx* ctx, lt_batch* batch);
+/* Pointers to the pinned result buffers (valid until the next decode). */
+lt_status lt_result_view(lt_batch* batch, lt_result* view);
+/* Blocking convenience: launch + fetch + sync + copy into caller buffers. */
+lt_status lt_decode(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k, lt_result* out);
+
+/* Reference-algorithm operation counts of the batch for beam k (a separate
+ * counting launch, not timed): expansions scored (beam.py:47) and candidate
+ * feature tuples generated by trigram_encoder (feature.py:76-121). */
+lt_status lt_count_ops(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k,
+                       int64_t* expansions, int64_t* feature_tuples, int64_t* probes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LATTICE_DECODE_H */

@@ -1,0 +1,64 @@
+"""Build of the in-tree HIP library ``lattice_based_tagger_amd/_lib/liblt.so``.
+
+``hipcc --offload-arch=gfx950`` cross-compiles without a GPU, so this runs in
+the CPU container and the resulting ``.so`` travels to the GPU box with the
+repository snapshot.  ``-ffp-contract=off`` keeps every float64 add/mul a
+separate IEEE operation, which bit-exact parity with the reference requires.
+"""
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+LIBDIR = os.path.join(HERE, '_lib')
+LIB = os.path.join(LIBDIR, 'liblt.so')
+ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
+HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
+ARCH = 'gfx950'
+
+SOURCES = ['lt_decode.hip', 'lt_capi.cpp']
+HEADERS = ['lt_common.h', 'lt_internal.h', os.path.join('..', '..', 'include', 'lattice_decode.h')]
+
+COMMON_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
+                '-Wall', '-Wno-unused-result', '-I' + os.path.join(HERE, '..', 'include')]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(dp) > t for dp in deps)
+
+
+def build(force=False, verbose=True):
+    """Compile liblt.so if any source is newer than it.  Returns its path."""
+    os.makedirs(LIBDIR, exist_ok=True)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [__file__]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + '.o')
+        cmd = [HIPCC, '--offload-arch=' + ARCH] + COMMON_FLAGS + ['-c', os.path.join(CSRC, src), '-o', obj]
+        if src.endswith('.cpp'):
+            cmd = [HIPCC] + COMMON_FLAGS + ['-D__HIP_PLATFORM_AMD__', '-c', os.path.join(CSRC, src), '-o', obj]
+        if verbose:
+            print(' '.join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + '.tmp'
+    cmd = [HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', tmp] + objs + [
+        '-Wl,-rpath,' + os.path.join(ROCM, 'lib'), '-Wl,--no-undefined']
+    if verbose:
+        print(' '.join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == '__main__':
+    build(force='--force' in sys.argv)

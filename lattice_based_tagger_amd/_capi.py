@@ -1,0 +1,233 @@
+"""ctypes binding of ``liblt.so`` (include/lattice_decode.h).
+
+The library is the product path: if it is missing or no GPU is visible the
+calls raise -- there is no CPU fallback decoder.
+"""
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+from ._build import LIB
+
+LT_OK = 0
+LT_MAX_BEAM = 32
+_STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED', -5: 'LT_ERCCL'}
+
+EXPORTED_SYMBOLS = (
+    'lt_abi_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
+    'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
+    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms',
+    'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
+)
+
+
+class LTError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__('%s (%d): %s' % (_STATUS.get(status, 'LT_ERROR'), status, msg))
+        self.status = status
+
+
+class ModelDesc(C.Structure):
+    _fields_ = [('n_keys', C.c_int64), ('keys', C.c_void_p), ('coefs', C.c_void_p)]
+
+
+class BatchDesc(C.Structure):
+    _fields_ = [('n_sent', C.c_int32), ('max_len', C.c_int32), ('n_post', C.c_int32),
+                ('has_trigram', C.c_int32), ('n_nodes', C.c_int64), ('n_span', C.c_int64),
+                ('sent_n', C.c_void_p), ('sent_node_off', C.c_void_p),
+                ('sent_span_off', C.c_void_p), ('span_start', C.c_void_p),
+                ('node_word', C.c_void_p), ('node_morph0', C.c_void_p), ('node_tag', C.c_void_p),
+                ('node_mask', C.c_void_p), ('node_pre', C.c_void_p), ('node_f4', C.c_void_p),
+                ('node_f5', C.c_void_p), ('node_f6', C.c_void_p), ('node_post', C.c_void_p)]
+
+
+class Result(C.Structure):
+    _fields_ = [('count', C.POINTER(C.c_int32)), ('length', C.POINTER(C.c_int32)),
+                ('score', C.POINTER(C.c_double)), ('codes', C.POINTER(C.c_int32))]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path=None):
+    """Load liblt.so (built in-tree by ``_build.build``).  Raises if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = path or LIB
+        if not os.path.exists(path):
+            raise RuntimeError('liblt.so not built (%s); run __graft_entry__.build()' % path)
+        lib = C.CDLL(path)
+        vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+        sig = {
+            'lt_abi_version': (C.c_int, []),
+            'lt_last_error': (C.c_char_p, []),
+            'lt_device_count': (C.c_int, []),
+            'lt_ctx_create': (i32, [C.c_int, C.POINTER(vp)]),
+            'lt_ctx_destroy': (i32, [vp]),
+            'lt_sync': (i32, [vp]),
+            'lt_model_create': (i32, [vp, C.POINTER(ModelDesc), C.POINTER(vp)]),
+            'lt_model_destroy': (i32, [vp]),
+            'lt_model_slots': (i64, [vp]),
+            'lt_batch_create': (i32, [vp, C.POINTER(BatchDesc), C.c_int, C.POINTER(vp)]),
+            'lt_batch_destroy': (i32, [vp]),
+            'lt_batch_code_slots': (i64, [vp, C.c_int]),
+            'lt_decode_launch': (i32, [vp, vp, vp, C.c_int]),
+            'lt_last_kernel_ms': (i32, [vp, C.POINTER(C.c_float)]),
+            'lt_result_fetch': (i32, [vp, vp]),
+            'lt_result_view': (i32, [vp, C.POINTER(Result)]),
+            'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),
+            'lt_count_ops': (i32, [vp, vp, vp, C.c_int, C.POINTER(i64), C.POINTER(i64),
+                                   C.POINTER(i64)]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(status):
+    if status != LT_OK:
+        msg = load().lt_last_error().decode('utf-8', 'replace')
+        raise LTError(status, msg)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class Context:
+    """One device + one HIP stream (lt_ctx)."""
+
+    def __init__(self, device=0):
+        lib = load()
+        h = C.c_void_p()
+        check(lib.lt_ctx_create(int(device), C.byref(h)))
+        self.handle = h
+        self.device = device
+        self._lib = lib
+
+    def sync(self):
+        check(self._lib.lt_sync(self.handle))
+
+    def kernel_ms(self):
+        v = C.c_float()
+        check(self._lib.lt_last_kernel_ms(self.handle, C.byref(v)))
+        return float(v.value)
+
+    def close(self):
+        if self.handle:
+            self._lib.lt_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceModel:
+    """Hash table of the probed feature classes on one device (lt_model)."""
+
+    def __init__(self, ctx, keys, coefs):
+        keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 4)
+        coefs = np.ascontiguousarray(coefs, dtype=np.float64)
+        desc = ModelDesc(keys.shape[0], _ptr(keys), _ptr(coefs))
+        h = C.c_void_p()
+        check(ctx._lib.lt_model_create(ctx.handle, C.byref(desc), C.byref(h)))
+        self.handle = h
+        self.ctx = ctx
+        self.slots = ctx._lib.lt_model_slots(h)
+
+    def close(self):
+        if self.handle:
+            self.ctx._lib.lt_model_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceBatch:
+    """A packed batch resident on the device (lt_batch)."""
+
+    FIELDS = ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start', 'node_word',
+              'node_morph0', 'node_tag', 'node_mask', 'node_pre', 'node_f4', 'node_f5',
+              'node_f6')
+    DTYPES = {'sent_n': np.int32, 'sent_node_off': np.int64, 'sent_span_off': np.int64,
+              'span_start': np.int32, 'node_word': np.int32, 'node_morph0': np.int32,
+              'node_tag': np.int32, 'node_mask': np.uint32, 'node_pre': np.float64,
+              'node_f4': np.float64, 'node_f5': np.float64, 'node_f6': np.float64}
+
+    def __init__(self, ctx, packed, max_k):
+        arr = {f: np.ascontiguousarray(getattr(packed, f), dtype=self.DTYPES[f])
+               for f in self.FIELDS}
+        n_post = int(packed.n_post)
+        post = np.ascontiguousarray(packed.node_post, dtype=np.float64) if n_post else None
+        self.n_sent = int(arr['sent_n'].shape[0])
+        self.sent_n = arr['sent_n']
+        self.cum_n = np.zeros(self.n_sent + 1, dtype=np.int64)
+        np.cumsum(self.sent_n, out=self.cum_n[1:])
+        desc = BatchDesc(
+            self.n_sent, int(packed.max_len), n_post, int(packed.has_trigram),
+            int(arr['node_word'].shape[0]), int(arr['span_start'].shape[0]),
+            *[_ptr(arr[f]) for f in self.FIELDS], _ptr(post))
+        h = C.c_void_p()
+        check(ctx._lib.lt_batch_create(ctx.handle, C.byref(desc), int(max_k), C.byref(h)))
+        self.handle = h
+        self.ctx = ctx
+        self.max_k = int(max_k)
+
+    def launch(self, model, k):
+        check(self.ctx._lib.lt_decode_launch(self.ctx.handle, model.handle, self.handle, int(k)))
+
+    def fetch(self):
+        check(self.ctx._lib.lt_result_fetch(self.ctx.handle, self.handle))
+
+    def results(self, k):
+        """numpy copies of (count, length, score, codes) after fetch + sync."""
+        v = Result()
+        check(self.ctx._lib.lt_result_view(self.handle, C.byref(v)))
+        S = self.n_sent
+        nc = int(self.cum_n[-1]) * k
+
+        def arr(p, n, dt):
+            if n == 0:
+                return np.zeros(0, dtype=dt)
+            return np.ctypeslib.as_array(p, shape=(n,)).copy()
+        return (arr(v.count, S, np.int32), arr(v.length, S * k, np.int32).reshape(S, k),
+                arr(v.score, S * k, np.float64).reshape(S, k), arr(v.codes, nc, np.int32))
+
+    def decode(self, model, k):
+        self.launch(model, k)
+        self.fetch()
+        self.ctx.sync()
+        return self.results(k)
+
+    def count_ops(self, model, k):
+        x, p, q = C.c_int64(), C.c_int64(), C.c_int64()
+        check(self.ctx._lib.lt_count_ops(self.ctx.handle, model.handle, self.handle, int(k),
+                                         C.byref(x), C.byref(p), C.byref(q)))
+        return x.value, p.value, q.value
+
+    def close(self):
+        if self.handle:
+            self.ctx._lib.lt_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

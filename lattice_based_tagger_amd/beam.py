@@ -1,0 +1,182 @@
+"""Drop-in ``beam_search`` backed by the MI355X decoder.
+
+Same signature and result type as the reference decoder
+``beam_search(bindex, chars, score_functions, beam_size=5, max_len=8,
+debug=False)`` (`lattice_tagger/beam/beam.py:5-61`): a list of at most
+``beam_size`` ``Sequence`` objects (best first, each ending in EOS).  The
+work is done by ``liblt.so``: the scorer composite is lowered once
+(``lowering.py``), the lattice is packed (``packer.py``) and decoded on the
+GPU by the HIP kernel (``csrc/lt_decode.hip``).
+
+``beam_search_batch`` decodes many sentences in one launch -- the intended
+high-throughput entry point.
+"""
+
+import weakref
+
+import numpy as np
+
+from . import _capi
+from .lowering import LoweredModel
+from .packer import pack
+from .word import bos_word, eos_word
+
+__all__ = ['beam_search', 'beam_search_batch', 'Beam', 'Sequence', 'Decoder']
+
+
+class Sequence:
+    """A hypothesis: node path, score and trailing-unknown count
+    (`beam.py:88-116`)."""
+
+    def __init__(self, sequences, score, num_unk=0):
+        self.sequences = sequences
+        self.score = score
+        self.num_unk = num_unk
+
+    def add(self, node, score_increment):
+        num_unk = self.num_unk + 1 if node.tag0 == 'Unknown' else 0
+        return Sequence(list(self.sequences) + [node], self.score + score_increment, num_unk)
+
+    def __repr__(self):
+        body = '\n    '.join(str(w) for w in self.sequences)
+        return 'Sequences(\n  words : [\n    {}\n  ]\n  score : {}\n  num unks in tails : {}\n)'.format(
+            body, self.score, self.num_unk)
+
+    __str__ = __repr__
+
+
+class Beam:
+    """Per-end-position hypothesis lists (`beam.py:64-86`).  Kept for API
+    compatibility; the GPU decoder keeps its beams on the device."""
+
+    def __init__(self, beam=None, k=5):
+        self.k = k
+        self.beam = beam if beam is not None else []
+
+    def __getitem__(self, index):
+        return self.beam[index]
+
+    def append(self, candidates):
+        self.beam.append(sorted(candidates, key=lambda x: -x.score)[:self.k])
+
+
+# ---------------------------------------------------------------------------
+# lowered-model cache: one LoweredModel per scorer composite
+# ---------------------------------------------------------------------------
+_model_cache = weakref.WeakKeyDictionary()
+
+
+def _fingerprint(score_functions):
+    parts = []
+    for f in getattr(score_functions, 'funcs', []):
+        parts.append(id(f))
+        if type(f).__name__ == 'SimpleTrigramFeatureScore':
+            enc = f.encoder
+            dic = getattr(enc, 'feature_dic', None)
+            coef = f.coefficients
+            parts += [id(enc), id(dic), len(dic) if dic is not None else -1, id(coef),
+                      coef.ctypes.data if isinstance(coef, np.ndarray) else 0]
+    return tuple(parts)
+
+
+def lowered_model(score_functions):
+    """LoweredModel of a composite, cached while the composite is unchanged
+    (same plugin objects, same feature_dic object and size, same
+    coefficient array).  Call ``invalidate_model_cache`` after mutating a
+    feature_dic or coefficients in place."""
+    fp = _fingerprint(score_functions)
+    try:
+        hit = _model_cache.get(score_functions)
+    except TypeError:
+        hit = None
+    if hit is not None and hit[0] == fp:
+        return hit[1]
+    model = LoweredModel(score_functions)
+    try:
+        _model_cache[score_functions] = (fp, model)
+    except TypeError:
+        pass
+    return model
+
+
+def invalidate_model_cache():
+    _model_cache.clear()
+
+
+class Decoder:
+    """A device context plus the device-resident models it has seen."""
+
+    _instances = {}
+
+    def __init__(self, device=0):
+        self.ctx = _capi.Context(device)
+        self.device = device
+
+    @classmethod
+    def get(cls, device=0):
+        dec = cls._instances.get(device)
+        if dec is None:
+            dec = cls._instances[device] = cls(device)
+        return dec
+
+    def device_model(self, model):
+        dm = model._device_models.get(self.device)
+        if dm is None:
+            dm = model._device_models[self.device] = _capi.DeviceModel(
+                self.ctx, model.keys, model.coefs)
+        return dm
+
+    def decode_packed(self, model, packed, k):
+        """Decode a PackedBatch; returns (count, length, score, codes, cum_n)."""
+        dm = self.device_model(model)
+        db = _capi.DeviceBatch(self.ctx, packed, max_k=k)
+        try:
+            count, length, score, codes = db.decode(dm, k)
+            return count, length, score, codes, db.cum_n
+        finally:
+            db.close()
+
+
+def _check_beam(beam_size):
+    k = int(beam_size)
+    if k < 0:
+        raise NotImplementedError('negative beam_size is not supported')
+    if k > _capi.LT_MAX_BEAM:
+        raise NotImplementedError('beam_size > %d is not compiled in' % _capi.LT_MAX_BEAM)
+    return k
+
+
+def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device=0):
+    """Decode ``sentences`` = list of ``(bindex, chars)``; returns one list of
+    matures per sentence, each as ``beam_search`` returns it."""
+    sentences = list(sentences)
+    k = _check_beam(beam_size)
+    model = lowered_model(score_functions)
+    packed, objs = pack(sentences, model, max_len)
+    if k == 0:
+        # beam_size=0 keeps no hypothesis past BOS (beam.py:85 slices to [])
+        return [[Sequence([bos_word(), eos_word(0)], 0)] if len(ch) == 0 else []
+                for _, ch in sentences]
+    count, length, score, codes, cum_n = Decoder.get(device).decode_packed(model, packed, k)
+    out = []
+    for s, (_, chars) in enumerate(sentences):
+        n = len(chars)
+        nodes = objs[s]
+        base = k * int(cum_n[s])
+        matures = []
+        for t in range(int(count[s])):
+            L = int(length[s, t])
+            off = base + t * n
+            path = [nodes[0]] + [nodes[c] for c in codes[off:off + L]] + [eos_word(n)]
+            sc = float(score[s, t]) if n > 0 else 0
+            matures.append(Sequence(path, sc, 0))
+        out.append(matures)
+    return out
+
+
+def beam_search(bindex, chars, score_functions, beam_size=5, max_len=8, debug=False):
+    """Drop-in for the reference ``beam_search`` (`beam.py:5-61`)."""
+    if debug:
+        raise NotImplementedError('debug=True (per-position hypothesis dump) is not available '
+                                  'from the device decoder')
+    return beam_search_batch([(bindex, chars)], score_functions, beam_size, max_len)[0]

@@ -1,0 +1,488 @@
+// lt_capi.cpp -- host side of liblt.so: the C-ABI declared in
+// include/lattice_decode.h (contexts, the model hash table, batch upload and
+// validation, decode launch, result download).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdarg>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/lattice_decode.h"
+#include "lt_common.h"
+#include "lt_internal.h"
+
+using namespace lt;
+
+namespace {
+
+thread_local std::string g_err;
+
+lt_status fail(lt_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+#define HIP_TRY(expr)                                                          \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess)                                                      \
+      return fail(LT_EHIP, "%s failed: %s", #expr, hipGetErrorString(_e));   \
+  } while (0)
+
+template <class T>
+hipError_t dalloc_copy(T** dst, const T* src, size_t count, hipStream_t st) {
+  *dst = nullptr;
+  if (count == 0) return hipSuccess;
+  hipError_t e = hipMalloc((void**)dst, count * sizeof(T));
+  if (e != hipSuccess) return e;
+  if (src) return hipMemcpyAsync(*dst, src, count * sizeof(T), hipMemcpyHostToDevice, st);
+  return hipSuccess;
+}
+
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+}  // namespace
+
+struct lt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  unsigned long long* d_counters = nullptr;
+};
+
+struct lt_model {
+  lt_ctx* ctx = nullptr;
+  Slot* d_table = nullptr;
+  int64_t slots = 0;
+};
+
+struct lt_batch {
+  lt_ctx* ctx = nullptr;
+  int32_t n_sent = 0, max_len = 8, n_post = 0, has_tri = 0, max_k = 1;
+  int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
+  int last_k = 0;
+  // device inputs
+  int32_t *d_order = nullptr, *d_sent_n = nullptr, *d_span_start = nullptr;
+  int64_t *d_node_off = nullptr, *d_span_off = nullptr, *d_bp_off = nullptr, *d_cum_n = nullptr;
+  int32_t *d_word = nullptr, *d_morph = nullptr, *d_tag = nullptr;
+  uint32_t* d_mask = nullptr;
+  double *d_pre = nullptr, *d_f4 = nullptr, *d_f5 = nullptr, *d_f6 = nullptr, *d_post = nullptr;
+  // scratch + device results (sized for max_k)
+  uint32_t* d_bp = nullptr;
+  int32_t *d_count = nullptr, *d_len = nullptr, *d_codes = nullptr;
+  double* d_score = nullptr;
+  // pinned host results
+  int32_t *h_count = nullptr, *h_len = nullptr, *h_codes = nullptr;
+  double* h_score = nullptr;
+};
+
+extern "C" {
+
+int lt_abi_version(void) { return LT_ABI_VERSION; }
+
+const char* lt_last_error(void) { return g_err.c_str(); }
+
+int lt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+lt_status lt_ctx_create(int device, lt_ctx** out) {
+  if (!out) return fail(LT_EINVAL, "lt_ctx_create: out is NULL");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return fail(LT_EHIP, "lt_ctx_create: no HIP device visible");
+  if (device < 0 || device >= n) return fail(LT_EINVAL, "lt_ctx_create: device %d of %d", device, n);
+  HIP_TRY(hipSetDevice(device));
+  lt_ctx* c = new (std::nothrow) lt_ctx;
+  if (!c) return fail(LT_ENOMEM, "lt_ctx_create: out of host memory");
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    lt_ctx_destroy(c);
+    return fail(LT_EHIP, "lt_ctx_create: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return LT_OK;
+}
+
+lt_status lt_ctx_destroy(lt_ctx* c) {
+  if (!c) return LT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  dfree(c->d_counters);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return LT_OK;
+}
+
+lt_status lt_sync(lt_ctx* c) {
+  if (!c) return fail(LT_EINVAL, "lt_sync: ctx is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return LT_OK;
+}
+
+// ---------------------------------------------------------------- model --
+lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
+  if (!c || !d || !out) return fail(LT_EINVAL, "lt_model_create: NULL argument");
+  *out = nullptr;
+  if (d->n_keys < 0 || (d->n_keys > 0 && (!d->keys || !d->coefs)))
+    return fail(LT_EINVAL, "lt_model_create: bad key arrays");
+  if (d->n_keys > ((int64_t)1 << 29)) return fail(LT_EUNSUPPORTED, "lt_model_create: too many keys");
+  int64_t slots = 64;
+  while (slots < 2 * d->n_keys) slots <<= 1;
+  std::vector<Slot> tab;
+  try {
+    tab.assign((size_t)slots, Slot{0u, 0u, 0u, EMPTY, 0.0, 0ull});
+  } catch (...) {
+    return fail(LT_ENOMEM, "lt_model_create: cannot allocate %lld slots", (long long)slots);
+  }
+  const uint32_t mask = (uint32_t)(slots - 1);
+  for (int64_t i = 0; i < d->n_keys; ++i) {
+    const uint32_t a = d->keys[4 * i], b = d->keys[4 * i + 1], cc = d->keys[4 * i + 2],
+                   cls = d->keys[4 * i + 3];
+    if (!(cls <= 3 || cls == 7 || cls == 8))
+      return fail(LT_EINVAL, "lt_model_create: key %lld has class %u (only 0,1,2,3,7,8 are probed)",
+                  (long long)i, cls);
+    const bool two = (cls == 1 || cls == 3 || cls == 8);
+    if (a == 0 || b == 0 || (two ? cc != 0 : cc == 0))
+      return fail(LT_EINVAL, "lt_model_create: key %lld has a bad component id", (long long)i);
+    if (!std::isfinite(d->coefs[i]))
+      return fail(LT_EUNSUPPORTED, "lt_model_create: non-finite coefficient at key %lld", (long long)i);
+    uint32_t h = key_hash(a, b, cc, cls) & mask;
+    for (;;) {
+      Slot& s = tab[h];
+      if (s.cls1 == EMPTY) {
+        s.a = a; s.b = b; s.c = cc; s.cls1 = cls + 1; s.coef = d->coefs[i];
+        break;
+      }
+      if (s.cls1 == cls + 1 && s.a == a && s.b == b && s.c == cc)
+        return fail(LT_EINVAL, "lt_model_create: duplicate key %lld", (long long)i);
+      h = (h + 1) & mask;
+    }
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  lt_model* m = new (std::nothrow) lt_model;
+  if (!m) return fail(LT_ENOMEM, "lt_model_create: out of host memory");
+  m->ctx = c;
+  m->slots = slots;
+  hipError_t e = dalloc_copy(&m->d_table, tab.data(), tab.size(), c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    dfree(m->d_table);
+    delete m;
+    return fail(LT_EHIP, "lt_model_create: %s", hipGetErrorString(e));
+  }
+  *out = m;
+  return LT_OK;
+}
+
+lt_status lt_model_destroy(lt_model* m) {
+  if (!m) return LT_OK;
+  (void)hipSetDevice(m->ctx->device);
+  dfree(m->d_table);
+  delete m;
+  return LT_OK;
+}
+
+int64_t lt_model_slots(const lt_model* m) { return m ? m->slots : 0; }
+
+// ---------------------------------------------------------------- batch --
+static lt_status validate(const lt_batch_desc* d) {
+  if (d->n_sent < 0 || d->n_nodes < 0 || d->n_span < 0 || d->n_post < 0)
+    return fail(LT_EINVAL, "batch: negative size");
+  if (d->max_len < 1 || d->max_len > LT_MAX_SPAN)
+    return fail(LT_EUNSUPPORTED, "batch: max_len %d not in 1..%d", d->max_len, LT_MAX_SPAN);
+  if (!d->sent_n || !d->sent_node_off || !d->sent_span_off)
+    return fail(LT_EINVAL, "batch: NULL sentence arrays");
+  if (d->n_nodes > 0 && (!d->node_word || !d->node_morph0 || !d->node_tag || !d->node_mask ||
+                         !d->node_pre || !d->node_f4 || !d->node_f5 || !d->node_f6))
+    return fail(LT_EINVAL, "batch: NULL node arrays");
+  if (d->n_post > 0 && !d->node_post) return fail(LT_EINVAL, "batch: NULL node_post");
+  if (d->n_span > 0 && !d->span_start) return fail(LT_EINVAL, "batch: NULL span_start");
+  if (d->sent_node_off[0] != 0 || d->sent_span_off[0] != 0)
+    return fail(LT_EINVAL, "batch: offsets must start at 0");
+  if (d->sent_node_off[d->n_sent] != d->n_nodes || d->sent_span_off[d->n_sent] != d->n_span)
+    return fail(LT_EINVAL, "batch: offsets do not end at n_nodes / n_span");
+  for (int32_t s = 0; s < d->n_sent; ++s) {
+    const int64_t n = d->sent_n[s];
+    const int64_t nodes = d->sent_node_off[s + 1] - d->sent_node_off[s];
+    const int64_t spans = d->sent_span_off[s + 1] - d->sent_span_off[s];
+    if (n < 0 || spans != LT_MAX_SPAN * n + 1)
+      return fail(LT_EINVAL, "batch: sentence %d has %lld span entries for %lld chars", s,
+                  (long long)spans, (long long)n);
+    if (nodes < 1 || nodes >= MAX_LOCAL_NODES)
+      return fail(LT_EINVAL, "batch: sentence %d has %lld nodes", s, (long long)nodes);
+    const int32_t* ss = d->span_start + d->sent_span_off[s];
+    if (ss[0] != 1 || ss[spans - 1] != nodes)
+      return fail(LT_EINVAL, "batch: sentence %d span table does not cover its nodes", s);
+    for (int64_t e = 1; e <= n; ++e) {
+      const int64_t dmax = std::min<int64_t>(e, d->max_len);
+      for (int j = 0; j < LT_MAX_SPAN; ++j) {
+        const int64_t idx = (e - 1) * LT_MAX_SPAN + j;
+        const int32_t cnt = ss[idx + 1] - ss[idx];
+        const int dd = LT_MAX_SPAN - j;
+        if (cnt < 0) return fail(LT_EINVAL, "batch: sentence %d span table not monotone", s);
+        if (dd <= dmax && cnt == 0)
+          return fail(LT_EINVAL, "batch: sentence %d span (e=%lld,d=%d) has no candidate", s,
+                      (long long)e, dd);
+        if (dd > dmax && cnt != 0)
+          return fail(LT_EINVAL, "batch: sentence %d span (e=%lld,d=%d) is out of range", s,
+                      (long long)e, dd);
+      }
+    }
+  }
+  for (int64_t i = 0; i < d->n_nodes; ++i) {
+    if (d->node_word[i] < 0 || d->node_morph0[i] < 0 || d->node_tag[i] < 0)
+      return fail(LT_EINVAL, "batch: node %lld has a negative id", (long long)i);
+    if (!std::isfinite(d->node_pre[i]) || !std::isfinite(d->node_f4[i]) ||
+        !std::isfinite(d->node_f5[i]) || !std::isfinite(d->node_f6[i]))
+      return fail(LT_EUNSUPPORTED, "batch: node %lld has a non-finite score term", (long long)i);
+  }
+  for (int64_t i = 0; i < (int64_t)d->n_post * d->n_nodes; ++i)
+    if (!std::isfinite(d->node_post[i]))
+      return fail(LT_EUNSUPPORTED, "batch: non-finite post term %lld", (long long)i);
+  return LT_OK;
+}
+
+static void batch_free(lt_batch* b) {
+  if (!b) return;
+  void* dev[] = {b->d_order, b->d_sent_n, b->d_span_start, b->d_node_off, b->d_span_off,
+                 b->d_bp_off, b->d_cum_n, b->d_word, b->d_morph, b->d_tag, b->d_mask,
+                 b->d_pre, b->d_f4, b->d_f5, b->d_f6, b->d_post, b->d_bp, b->d_count,
+                 b->d_len, b->d_codes, b->d_score};
+  for (void* p : dev) dfree(p);
+  void* host[] = {b->h_count, b->h_len, b->h_codes, b->h_score};
+  for (void* p : host)
+    if (p) (void)hipHostFree(p);
+  delete b;
+}
+
+lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch** out) {
+  if (!c || !d || !out) return fail(LT_EINVAL, "lt_batch_create: NULL argument");
+  *out = nullptr;
+  if (max_k < 1 || max_k > LT_MAX_BEAM)
+    return fail(LT_EUNSUPPORTED, "lt_batch_create: max_k %d not in 1..%d", max_k, LT_MAX_BEAM);
+  lt_status st = validate(d);
+  if (st != LT_OK) return st;
+  HIP_TRY(hipSetDevice(c->device));
+  lt_batch* b = new (std::nothrow) lt_batch;
+  if (!b) return fail(LT_ENOMEM, "lt_batch_create: out of host memory");
+  b->ctx = c;
+  b->n_sent = d->n_sent;
+  b->max_len = d->max_len;
+  b->n_post = d->n_post;
+  b->has_tri = d->has_trigram ? 1 : 0;
+  b->max_k = max_k;
+  b->n_nodes = d->n_nodes;
+  b->n_span = d->n_span;
+
+  const int32_t S = d->n_sent;
+  std::vector<int32_t> order(S);
+  std::vector<int64_t> bp_off(S + 1), cum_n(S + 1);
+  for (int32_t s = 0; s < S; ++s) order[s] = s;
+  // longest sentences first: the grid drains evenly
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int32_t x, int32_t y) { return d->sent_n[x] > d->sent_n[y]; });
+  bp_off[0] = 0;
+  cum_n[0] = 0;
+  for (int32_t s = 0; s < S; ++s) {
+    bp_off[s + 1] = bp_off[s] + (int64_t)(d->sent_n[s] + 1) * max_k;
+    cum_n[s + 1] = cum_n[s] + d->sent_n[s];
+  }
+  b->total_chars = cum_n[S];
+  b->bp_entries = bp_off[S];
+
+  hipStream_t stm = c->stream;
+  hipError_t e = hipSuccess;
+  auto up = [&](auto** dst, const auto* src, size_t count) {
+    if (e == hipSuccess) e = dalloc_copy(dst, src, count, stm);
+  };
+  up(&b->d_order, order.data(), (size_t)S);
+  up(&b->d_sent_n, d->sent_n, (size_t)S);
+  up(&b->d_node_off, d->sent_node_off, (size_t)S + 1);
+  up(&b->d_span_off, d->sent_span_off, (size_t)S + 1);
+  up(&b->d_bp_off, bp_off.data(), (size_t)S + 1);
+  up(&b->d_cum_n, cum_n.data(), (size_t)S + 1);
+  up(&b->d_span_start, d->span_start, (size_t)d->n_span);
+  up(&b->d_word, d->node_word, (size_t)d->n_nodes);
+  up(&b->d_morph, d->node_morph0, (size_t)d->n_nodes);
+  up(&b->d_tag, d->node_tag, (size_t)d->n_nodes);
+  up(&b->d_mask, d->node_mask, (size_t)d->n_nodes);
+  up(&b->d_pre, d->node_pre, (size_t)d->n_nodes);
+  up(&b->d_f4, d->node_f4, (size_t)d->n_nodes);
+  up(&b->d_f5, d->node_f5, (size_t)d->n_nodes);
+  up(&b->d_f6, d->node_f6, (size_t)d->n_nodes);
+  up(&b->d_post, d->node_post, (size_t)d->n_post * (size_t)d->n_nodes);
+  const size_t nres = (size_t)S * max_k;
+  const size_t ncodes = (size_t)b->total_chars * max_k;
+  up(&b->d_bp, (const uint32_t*)nullptr, (size_t)b->bp_entries);
+  up(&b->d_count, (const int32_t*)nullptr, (size_t)S);
+  up(&b->d_len, (const int32_t*)nullptr, nres);
+  up(&b->d_score, (const double*)nullptr, nres);
+  up(&b->d_codes, (const int32_t*)nullptr, ncodes);
+  if (e == hipSuccess && S) e = hipHostMalloc((void**)&b->h_count, (size_t)S * 4, hipHostMallocDefault);
+  if (e == hipSuccess && nres) e = hipHostMalloc((void**)&b->h_len, nres * 4, hipHostMallocDefault);
+  if (e == hipSuccess && nres) e = hipHostMalloc((void**)&b->h_score, nres * 8, hipHostMallocDefault);
+  if (e == hipSuccess && ncodes) e = hipHostMalloc((void**)&b->h_codes, ncodes * 4, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipStreamSynchronize(stm);
+  if (e != hipSuccess) {
+    batch_free(b);
+    return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "lt_batch_create: %s",
+                hipGetErrorString(e));
+  }
+  *out = b;
+  return LT_OK;
+}
+
+lt_status lt_batch_destroy(lt_batch* b) {
+  if (!b) return LT_OK;
+  (void)hipSetDevice(b->ctx->device);
+  (void)hipStreamSynchronize(b->ctx->stream);
+  batch_free(b);
+  return LT_OK;
+}
+
+int64_t lt_batch_code_slots(const lt_batch* b, int k) { return b ? b->total_chars * (int64_t)k : 0; }
+
+// --------------------------------------------------------------- decode --
+static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, DecodeParams& p) {
+  if (!c || !m || !b) return fail(LT_EINVAL, "decode: NULL argument");
+  if (m->ctx != c || b->ctx != c) return fail(LT_EINVAL, "decode: handles from another context");
+  if (k < 1 || k > b->max_k)
+    return fail(LT_EUNSUPPORTED, "decode: beam %d not in 1..%d (batch max_k)", k, b->max_k);
+  if (beam_template_for(k) < 0) return fail(LT_EUNSUPPORTED, "decode: beam %d not compiled", k);
+  p = DecodeParams{};
+  p.table = m->d_table;
+  p.tmask = (uint32_t)(m->slots - 1);
+  p.has_tri = b->has_tri;
+  p.n_sent = b->n_sent;
+  p.max_len = b->max_len;
+  p.n_post = b->n_post;
+  p.k = k;
+  p.bp_stride = b->max_k;
+  p.n_nodes = b->n_nodes;
+  p.order = b->d_order;
+  p.sent_n = b->d_sent_n;
+  p.node_off = b->d_node_off;
+  p.span_off = b->d_span_off;
+  p.span_start = b->d_span_start;
+  p.nword = b->d_word;
+  p.nmorph = b->d_morph;
+  p.ntag = b->d_tag;
+  p.nmask = b->d_mask;
+  p.npre = b->d_pre;
+  p.nf4 = b->d_f4;
+  p.nf5 = b->d_f5;
+  p.nf6 = b->d_f6;
+  p.npost = b->d_post;
+  p.bp = b->d_bp;
+  p.bp_off = b->d_bp_off;
+  p.cum_n = b->d_cum_n;
+  p.out_count = b->d_count;
+  p.out_len = b->d_len;
+  p.out_score = b->d_score;
+  p.out_codes = b->d_codes;
+  p.counters = c->d_counters;
+  return LT_OK;
+}
+
+lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
+  DecodeParams p;
+  lt_status st = fill_params(c, m, b, k, p);
+  if (st != LT_OK) return st;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  HIP_TRY(launch_decode(p, c->stream, false));
+  HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  b->last_k = k;
+  return LT_OK;
+}
+
+lt_status lt_last_kernel_ms(lt_ctx* c, float* ms) {
+  if (!c || !ms) return fail(LT_EINVAL, "lt_last_kernel_ms: NULL argument");
+  HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return LT_OK;
+}
+
+lt_status lt_result_fetch(lt_ctx* c, lt_batch* b) {
+  if (!c || !b) return fail(LT_EINVAL, "lt_result_fetch: NULL argument");
+  if (b->last_k < 1) return fail(LT_EINVAL, "lt_result_fetch: no decode launched");
+  const int k = b->last_k;
+  const size_t S = (size_t)b->n_sent;
+  HIP_TRY(hipSetDevice(c->device));
+  if (S) {
+    HIP_TRY(hipMemcpyAsync(b->h_count, b->d_count, S * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(b->h_len, b->d_len, S * k * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(b->h_score, b->d_score, S * k * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  const size_t nc = (size_t)b->total_chars * k;
+  if (nc) HIP_TRY(hipMemcpyAsync(b->h_codes, b->d_codes, nc * 4, hipMemcpyDeviceToHost, c->stream));
+  return LT_OK;
+}
+
+lt_status lt_result_view(lt_batch* b, lt_result* v) {
+  if (!b || !v) return fail(LT_EINVAL, "lt_result_view: NULL argument");
+  v->count = b->h_count;
+  v->length = b->h_len;
+  v->score = b->h_score;
+  v->codes = b->h_codes;
+  return LT_OK;
+}
+
+lt_status lt_decode(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_result* out) {
+  if (!out) return fail(LT_EINVAL, "lt_decode: out is NULL");
+  lt_status st = lt_decode_launch(c, m, b, k);
+  if (st != LT_OK) return st;
+  if ((st = lt_result_fetch(c, b)) != LT_OK) return st;
+  if ((st = lt_sync(c)) != LT_OK) return st;
+  const size_t S = (size_t)b->n_sent;
+  if (S) {
+    if (out->count) memcpy(out->count, b->h_count, S * 4);
+    if (out->length) memcpy(out->length, b->h_len, S * k * 4);
+    if (out->score) memcpy(out->score, b->h_score, S * k * 8);
+  }
+  const size_t nc = (size_t)b->total_chars * k;
+  if (nc && out->codes) memcpy(out->codes, b->h_codes, nc * 4);
+  return LT_OK;
+}
+
+lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t* expansions,
+                       int64_t* feature_tuples, int64_t* probes) {
+  DecodeParams p;
+  lt_status st = fill_params(c, m, b, k, p);
+  if (st != LT_OK) return st;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+  HIP_TRY(launch_decode(p, c->stream, true));
+  unsigned long long h[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  b->last_k = k;
+  if (expansions) *expansions = (int64_t)h[0];
+  if (feature_tuples) *feature_tuples = (int64_t)h[1];
+  if (probes) *probes = (int64_t)h[2];
+  return LT_OK;
+}
+
+}  // extern "C"

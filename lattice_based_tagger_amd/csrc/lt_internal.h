@@ -1,0 +1,49 @@
+// lt_internal.h -- kernel launch interface between lt_capi.cpp and lt_decode.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "lt_common.h"
+
+namespace lt {
+
+struct DecodeParams {
+  // model
+  const Slot* table;
+  uint32_t tmask;
+  int32_t has_tri;
+  // batch (device pointers)
+  int32_t n_sent;
+  int32_t max_len;
+  int32_t n_post;
+  int32_t k;
+  int32_t bp_stride;            // backpointer entries per end position (batch max_k)
+  int64_t n_nodes;
+  const int32_t* order;         // processing order of sentences
+  const int32_t* sent_n;
+  const int64_t* node_off;
+  const int64_t* span_off;
+  const int32_t* span_start;
+  const int32_t* nword;
+  const int32_t* nmorph;
+  const int32_t* ntag;
+  const uint32_t* nmask;
+  const double* npre;
+  const double* nf4;
+  const double* nf5;
+  const double* nf6;
+  const double* npost;
+  // scratch + results
+  uint32_t* bp;
+  const int64_t* bp_off;
+  const int64_t* cum_n;         // sum_{s2<s} n_s2 (codes of s start at k*cum_n[s])
+  int32_t* out_count;
+  int32_t* out_len;
+  double* out_score;
+  int32_t* out_codes;
+  unsigned long long* counters; // [3] expansions, feature tuples, probes
+};
+
+int beam_template_for(int k);
+hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count);
+
+}  // namespace lt

@@ -1,0 +1,209 @@
+"""Lowering of a ``BeamScoreFunctions`` composite to the device model.
+
+The reference scores every expansion by calling each plugin in order
+(`lattice_tagger/beam/score_funcs.py:50-54`).  The build splits the
+composite into
+
+* node-local terms -- ``RegularizationScore`` (`:65-73`),
+  ``MorphemePreferenceScore`` (`:84-88`) and ``WordPreferenceScore``
+  (`:99-100`) depend on the appended node only.  They are evaluated once per
+  lattice node while packing.  Terms in front of the trigram scorer are
+  pre-summed in constructor order into ``pre`` (exact: the same left-to-right
+  additions); terms after it stay separate (``post``) because f64 addition is
+  not associative.
+* the trigram term -- ``SimpleTrigramFeatureScore`` (`:137-144`).  Feature
+  classes 0-3, 7 and 8 depend on the hypothesis and are probed per expansion
+  in a device hash table; classes 4-6 depend on one node and are resolved per
+  node by the packer.
+
+Feature tuples are matched exactly as Python tuple membership does
+(`features/feature.py:28-29`): every component value that occurs in a key of
+``feature_dic`` is interned into one id space through a Python dict, so two
+values receive the same id iff they compare (and hash) equal.  Id 0 means "occurs
+in no key", which makes every feature containing it absent.
+
+Unsupported composites (a plugin of any other class, two trigram scorers,
+non-float64 coefficients) raise ``NotImplementedError``: there is no CPU
+fallback decoder.
+"""
+
+import numpy as np
+
+from .feature import FEATURE_ARITY, EXPANSION_CLASSES
+
+# ---------------------------------------------------------------------------
+# Node mask bits (shared with csrc/lt_decode.hip and oracle/lt_oracle.c).
+# Bits 0-15: "this node's component occurs at key slot X" (exact pre-filter).
+# ---------------------------------------------------------------------------
+K0B, K0C, K1B, K2B, K2C, K3B, K7C, K8B = (1 << i for i in range(8))
+J0A, J1A, J2A, J3A, J7B, J8A = (1 << i for i in range(8, 14))
+I7A, I8A = 1 << 14, 1 << 15
+F_UNK = 1 << 16      # tag0 == 'Unknown'
+F_CTX = 1 << 17      # tag0 in {Noun, Adverb, Adjective, Verb}
+F_HAS4 = 1 << 18     # (4, len) in feature_dic
+F_HAS5 = 1 << 19     # (5, word, tag0, is_l) in feature_dic
+F_HAS6 = 1 << 20     # tag0 == Unk and (6, min(8, len)) in feature_dic
+
+# Key slots: (class, component position) -> bit in the vocabulary mask.
+SLOT_BITS = {
+    (0, 0): 0, (0, 1): 1, (0, 2): 2,
+    (1, 0): 3, (1, 1): 4,
+    (2, 0): 5, (2, 1): 6, (2, 2): 7,
+    (3, 0): 8, (3, 1): 9,
+    (7, 0): 10, (7, 1): 11, (7, 2): 12,
+    (8, 0): 13, (8, 1): 14,
+}
+
+
+def node_mask_from_vocab(vm_word, vm_morph, vm_tag):
+    """Node pre-filter bits from the vocabulary slot masks of the node's word,
+    morph0 and tag0 ids.  Works on ints and on numpy uint32 arrays."""
+    def has(vm, cls, pos):
+        return (vm >> SLOT_BITS[(cls, pos)]) & 1
+    m = (has(vm_word, 0, 1) * K0B | has(vm_tag, 0, 2) * K0C |
+         has(vm_tag, 1, 1) * K1B | has(vm_word, 2, 1) * K2B |
+         has(vm_tag, 2, 2) * K2C | has(vm_tag, 3, 1) * K3B |
+         has(vm_word, 7, 2) * K7C | has(vm_morph, 8, 1) * K8B |
+         has(vm_word, 0, 0) * J0A | has(vm_word, 1, 0) * J1A |
+         has(vm_tag, 2, 0) * J2A | has(vm_tag, 3, 0) * J3A |
+         has(vm_word, 7, 1) * J7B | has(vm_morph, 8, 0) * J8A |
+         has(vm_word, 7, 0) * I7A | has(vm_morph, 8, 0) * I8A)
+    return m
+
+
+NODE_LOCAL_SCORERS = ('RegularizationScore', 'MorphemePreferenceScore',
+                      'WordPreferenceScore')
+TRIGRAM_SCORER = 'SimpleTrigramFeatureScore'
+ENCODER_CLASSES = ('SimpleTrigramEncoder',)
+
+
+class _ClassIndex:
+    """Python-equality lookup of a feature class id (True == 1 etc.)."""
+    table = {c: c for c in range(9)}
+
+
+class LoweredModel:
+    """Host-side description of one scorer composite.
+
+    Attributes
+    ----------
+    pre_funcs, post_funcs : node-local plugins before / after the trigram
+    trigram : the SimpleTrigramFeatureScore or None
+    vocab : dict value -> id (1-based) over every key component
+    vmask : uint32[len(vocab)+1] key-slot bits per id
+    keys : uint32[F, 4] (a, b, c, class) of the probed classes
+    coefs : float64[F]
+    feature_dic, coefficients : the trigram's tables (node-local classes)
+    """
+
+    def __init__(self, score_functions):
+        funcs = list(getattr(score_functions, 'funcs', None) or [])
+        if not hasattr(score_functions, 'funcs'):
+            raise NotImplementedError(
+                'beam_search expects a BeamScoreFunctions composite')
+        self.pre_funcs, self.post_funcs = [], []
+        self.trigram = None
+        for f in funcs:
+            name = type(f).__name__
+            if name == TRIGRAM_SCORER:
+                if self.trigram is not None:
+                    raise NotImplementedError('at most one SimpleTrigramFeatureScore is supported')
+                self.trigram = f
+            elif name in NODE_LOCAL_SCORERS:
+                (self.post_funcs if self.trigram is not None else self.pre_funcs).append(f)
+            else:
+                raise NotImplementedError(
+                    'scorer %s has no device lowering (supported: %s, %s)'
+                    % (name, ', '.join(NODE_LOCAL_SCORERS), TRIGRAM_SCORER))
+        self.vocab = {}
+        self.vmask = np.zeros(1, dtype=np.uint32)
+        self.keys = np.zeros((0, 4), dtype=np.uint32)
+        self.coefs = np.zeros(0, dtype=np.float64)
+        self.feature_dic = None
+        self.coefficients = None
+        if self.trigram is not None:
+            self._lower_trigram(self.trigram)
+        self._device_models = {}
+
+    @property
+    def n_post(self):
+        return len(self.post_funcs)
+
+    @property
+    def has_trigram(self):
+        return self.trigram is not None
+
+    def _lower_trigram(self, tri):
+        enc = tri.encoder
+        if enc is None:
+            raise AttributeError("'NoneType' object has no attribute 'encode_word'")
+        if type(enc).__name__ not in ENCODER_CLASSES:
+            raise NotImplementedError('encoder %s has no device lowering' % type(enc).__name__)
+        coef = tri.coefficients
+        if not isinstance(coef, np.ndarray) or coef.dtype != np.float64 or coef.ndim != 1:
+            raise NotImplementedError('coefficients must be a 1-D float64 numpy array')
+        dic = enc.feature_dic
+        self.feature_dic = dic
+        self.coefficients = coef
+        vocab = self.vocab
+        keys, coefs, slot_pairs = [], [], []
+        cls_of = _ClassIndex.table
+        n_coef = coef.shape[0]
+        for key, idx in dic.items():
+            if not isinstance(key, tuple) or not key:
+                continue
+            try:
+                cls = cls_of.get(key[0])
+            except TypeError:
+                cls = None
+            if cls is None or cls not in EXPANSION_CLASSES:
+                continue
+            if len(key) != FEATURE_ARITY[cls] + 1:
+                continue        # can never equal a generated feature
+            ids = []
+            for pos, comp in enumerate(key[1:]):
+                vid = vocab.get(comp)
+                if vid is None:
+                    vid = len(vocab) + 1
+                    vocab[comp] = vid
+                ids.append(vid)
+                slot_pairs.append((vid, SLOT_BITS[(cls, pos)]))
+            ids += [0] * (3 - len(ids))
+            i = int(idx)
+            if not -n_coef <= i < n_coef:
+                raise IndexError('feature index %d out of range for %d coefficients' % (i, n_coef))
+            keys.append((ids[0], ids[1], ids[2], cls))
+            coefs.append(coef[i])
+        vmask = np.zeros(len(vocab) + 1, dtype=np.uint32)
+        if slot_pairs:
+            sp = np.asarray(slot_pairs, dtype=np.int64)
+            np.bitwise_or.at(vmask, sp[:, 0], (np.uint32(1) << sp[:, 1].astype(np.uint32)))
+        self.vmask = vmask
+        self.keys = np.asarray(keys, dtype=np.uint32).reshape(-1, 4)
+        self.coefs = np.asarray(coefs, dtype=np.float64)
+
+    # -- node-local helpers (used by the packer) ---------------------------
+    def node_terms(self, w):
+        """(pre, [post...]) for appending node ``w``: the node-local plugins'
+        values summed as ``BeamScoreFunctions.score`` does."""
+        pre = 0
+        for f in self.pre_funcs:
+            pre = pre + f.score(None, w)
+        return pre, [f.score(None, w) for f in self.post_funcs]
+
+    def node_local_features(self, w, is_unk):
+        """Coefficients (or None) of feature classes 4, 5 and 6 for node w."""
+        dic = self.feature_dic
+        if dic is None:
+            return None, None, None
+        coef = self.coefficients
+        i4 = dic.get((4, w.len))
+        i5 = dic.get((5, w.word, w.tag0, w.is_l))
+        i6 = dic.get((6, min(8, w.len))) if is_unk else None
+        return (None if i4 is None else float(coef[i4]),
+                None if i5 is None else float(coef[i5]),
+                None if i6 is None else float(coef[i6]))
+
+
+def lower_scorers(score_functions):
+    return LoweredModel(score_functions)

@@ -1,0 +1,147 @@
+"""Lattice packer: ``bindex`` lists of ``Word`` nodes -> packed CSR batch.
+
+Input is exactly what the reference decoder consumes
+(`lattice_tagger/beam/beam.py:5`): per sentence ``bindex`` (a list indexed by
+begin character of lists of nodes, as produced by
+`dictionary/lookup.py:344-369`) and ``chars``.  Output is the device batch
+layout described in DESIGN.md §Data layout:
+
+* nodes of one sentence are stored in *expansion generation order*: local
+  node 0 is BOS, then for every end position ``e`` and every begin
+  ``b = e-d`` in ascending order (d = max_len..1) the span's candidates in
+  ``bindex[b]`` order filtered by ``w.e == e`` (`beam.py:31-33`), or the
+  synthesised Unknown node when that filter is empty (`beam.py:36-38`).
+* ``span_start[(e-1)*8 + (8-d)]`` is the local index of the first node of
+  span (e-d, e); entry ``8n`` closes the sentence.
+* per node: interned ``word``/``morph0``/``tag0`` ids, the 21-bit
+  mask/flag word (``lowering.py``), the node-local score terms and the
+  coefficients of the node-local feature classes 4, 5 and 6.
+
+The packer never reorders candidates: duplicates, ``len != e-b`` nodes and
+nodes filed under a begin slot other than their ``b`` field are kept exactly
+as the reference would see them.
+"""
+
+import numpy as np
+
+from . import lowering as L
+from .tagset import BOS, CONTEXTUAL_TAGS, Unk
+from .word import Word, bos_word
+
+MAX_SPAN = 8            # span slots per end position in the packed layout
+
+
+class PackedBatch:
+    """Host arrays of one packed batch (field names follow lt_batch_desc)."""
+
+    def __init__(self, **arrays):
+        self.__dict__.update(arrays)
+
+    @property
+    def n_sent(self):
+        return int(self.sent_n.shape[0])
+
+    @property
+    def n_nodes(self):
+        return int(self.node_word.shape[0])
+
+
+def _span_candidates(bindex_b, b, n, max_len):
+    """Dict e -> candidates of bindex[b] ending at e, in bindex order."""
+    groups = {}
+    for w in bindex_b:
+        groups.setdefault(w.e, []).append(w)
+    return groups
+
+
+def pack(sentences, model, max_len=8):
+    """Pack ``sentences`` = iterable of ``(bindex, chars)``.
+
+    Returns ``(PackedBatch, node_objects)`` where ``node_objects[s][i]`` is the
+    Python node behind local node ``i`` of sentence ``s`` (the original
+    object for dictionary nodes).  Raises ``IndexError`` for a sentence whose
+    ``bindex`` is shorter than its character count, as the reference does
+    (`beam.py:32`).
+    """
+    if not 1 <= max_len <= MAX_SPAN:
+        raise NotImplementedError('max_len must be in 1..%d' % MAX_SPAN)
+    vocab = model.vocab
+    vmask = model.vmask
+    n_post = model.n_post
+
+    sent_n, node_off, span_off = [], [0], [0]
+    span_start = []
+    words, morphs, tags, masks = [], [], [], []
+    pre, f4, f5, f6 = [], [], [], []
+    post = [[] for _ in range(n_post)]
+    node_objects = []
+
+    def add_node(w):
+        is_unk = w.tag0 == Unk
+        wid = vocab.get(w.word, 0)
+        mid = vocab.get(w.morph0, 0)
+        tid = vocab.get(w.tag0, 0)
+        m = L.node_mask_from_vocab(int(vmask[wid]), int(vmask[mid]), int(vmask[tid]))
+        if is_unk:
+            m |= L.F_UNK
+        if w.tag0 in CONTEXTUAL_TAGS:
+            m |= L.F_CTX
+        c4, c5, c6 = model.node_local_features(w, is_unk)
+        if c4 is not None:
+            m |= L.F_HAS4
+        if c5 is not None:
+            m |= L.F_HAS5
+        if c6 is not None:
+            m |= L.F_HAS6
+        p, q = model.node_terms(w)
+        words.append(wid)
+        morphs.append(mid)
+        tags.append(tid)
+        masks.append(m)
+        pre.append(float(p))
+        f4.append(0.0 if c4 is None else c4)
+        f5.append(0.0 if c5 is None else c5)
+        f6.append(0.0 if c6 is None else c6)
+        for j in range(n_post):
+            post[j].append(float(q[j]))
+
+    for bindex, chars in sentences:
+        n = len(chars)
+        if len(bindex) < n:
+            raise IndexError('list index out of range')
+        objs = [bos_word()]
+        base = len(words)
+        add_node(objs[0])
+        groups = [_span_candidates(bindex[b], b, n, max_len) for b in range(n)]
+        for e in range(1, n + 1):
+            for d in range(MAX_SPAN, 0, -1):
+                span_start.append(len(objs))
+                b = e - d
+                if d > max_len or b < 0:
+                    continue
+                cands = groups[b].get(e)
+                if not cands:
+                    cands = [Word(chars[b:e], chars[b:e], None, Unk, None, d, b, e, False)]
+                for w in cands:
+                    objs.append(w)
+                    add_node(w)
+        span_start.append(len(objs))
+        sent_n.append(n)
+        node_off.append(base + len(objs))
+        span_off.append(len(span_start))
+        node_objects.append(objs)
+
+    u32 = lambda a: np.asarray(a, dtype=np.uint32)
+    i32 = lambda a: np.asarray(a, dtype=np.int32)
+    f64 = lambda a: np.asarray(a, dtype=np.float64)
+    batch = PackedBatch(
+        max_len=max_len, n_post=n_post, has_trigram=int(model.has_trigram),
+        sent_n=i32(sent_n), sent_node_off=np.asarray(node_off, dtype=np.int64),
+        sent_span_off=np.asarray(span_off, dtype=np.int64),
+        span_start=i32(span_start),
+        node_word=i32(words), node_morph0=i32(morphs), node_tag=i32(tags),
+        node_mask=u32(masks), node_pre=f64(pre), node_f4=f64(f4),
+        node_f5=f64(f5), node_f6=f64(f6),
+        node_post=f64(post).reshape(n_post, -1) if n_post else np.zeros((0, len(words))),
+    )
+    return batch, node_objects

@@ -1,0 +1,52 @@
+"""liblt.so builds, loads and exports every entry point include/lattice_decode.h
+declares (no compute without a GPU)."""
+
+import os
+import re
+import subprocess
+
+import pytest
+
+from lattice_based_tagger_amd import _build, _capi
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      'include', 'lattice_decode.h')
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(lt_[a-z_]+)\s*\(', text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _build.build(verbose=False)
+    out = subprocess.run(['nm', '-D', '--defined-only', lib], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r'\bT (lt_\w+)', out))
+    declared = declared_symbols()
+    assert declared, 'no declarations parsed'
+    missing = [s for s in declared if s not in exported]
+    assert not missing, missing
+    assert set(declared) == set(_capi.EXPORTED_SYMBOLS)
+
+
+def test_library_loads_and_reports_abi():
+    lib = _capi.load()
+    assert lib.lt_abi_version() == 1
+    assert lib.lt_device_count() >= 0
+
+
+def test_kernels_are_gfx950_code_objects():
+    lib = _build.build(verbose=False)
+    blob = open(lib, 'rb').read()
+    assert b'amdgcn-amd-amdhsa--gfx950' in blob
+    assert b'lt_decode_k' in blob
+
+
+def test_context_without_gpu_fails_loudly():
+    lib = _capi.load()
+    if lib.lt_device_count() > 0:
+        pytest.skip('GPU present')
+    with pytest.raises(_capi.LTError):
+        _capi.Context(0)

@@ -1,0 +1,138 @@
+"""Parity of the HIP decoder (through the C-ABI) with the reference.
+
+* golden vectors of the reference itself (tests/golden) through the drop-in
+  ``beam_search_batch`` / ``beam_search`` API: bit-exact paths (node identity)
+  and float64 scores compared as float.hex() -- 0 ULP;
+* the C restatement (oracle/lt_oracle.c) on synthetic batches of the bench
+  shape, bit-exact, up to the full 64K-sentence config;
+* size-independent properties at full size (determinism, path validity,
+  sorted matures).
+"""
+
+import numpy as np
+import pytest
+
+from golden_io import SETS, load, path_matches
+from lattice_based_tagger_amd import _capi, beam_search, beam_search_batch, synth
+from oracle import lt_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('name', SETS)
+def test_golden_vectors_on_gpu(gpu_decoder, name):
+    cases = load(name)
+    groups = {}
+    for c in cases:
+        groups.setdefault((id(c.funcs), c.max_len), []).append(c)
+    checked = 0
+    for group in groups.values():
+        ok = [c for c in group if not any('error' in e for e in c.expected.values())]
+        for c in group:
+            if c not in ok:
+                with pytest.raises(IndexError):
+                    beam_search(c.bindex, c.chars, c.funcs, beam_size=1, max_len=c.max_len)
+        if not ok:
+            continue
+        for k in (1, 5, 16):
+            got = beam_search_batch([(c.bindex, c.chars) for c in ok], ok[0].funcs,
+                                    beam_size=k, max_len=ok[0].max_len)
+            for c, matures in zip(ok, got):
+                exp = c.expected[str(k)]['matures']
+                assert len(matures) == len(exp), (c.tag, k)
+                for m, (codes, shex, _) in zip(matures, exp):
+                    assert float(m.score).hex() == shex, (c.tag, k)
+                    assert path_matches(c, codes, m.sequences[1:-1]), (c.tag, k)
+                    checked += 1
+    assert checked > 0
+
+
+def test_single_sentence_drop_in(gpu_decoder):
+    case = load('base')[0]          # config 1: one 10-eojeol sentence
+    m = beam_search(case.bindex, case.chars, case.funcs, beam_size=5)
+    exp = case.expected['5']['matures']
+    assert [float(x.score).hex() for x in m] == [e[1] for e in exp]
+
+
+def _synthetic(n_sent, seed, n_features):
+    raw = synth.make_lattices(n_sent, seed=seed)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=seed, n_features=n_features)
+    return synth.pack_fast(raw, sm, lay, cols)
+
+
+def _gpu_decode(ctx, packed, keys, coefs, k):
+    dm = _capi.DeviceModel(ctx, keys, coefs)
+    db = _capi.DeviceBatch(ctx, packed, max_k=k)
+    try:
+        return db.decode(dm, k), db.count_ops(dm, k)
+    finally:
+        db.close()
+        dm.close()
+
+
+@pytest.mark.parametrize('k,n_sent', [(1, 65536), (5, 8192), (16, 4096), (2, 2048), (32, 512)])
+def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
+    packed, keys, coefs = _synthetic(n_sent, seed=100 + k, n_features=1_000_000)
+    (count, length, score, codes), (ex, tu, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
+    o_count, o_len, o_score, o_codes, o_ex, o_tu = lt_oracle.decode(packed, keys, coefs, k,
+                                                                    nthreads=16)
+    assert np.array_equal(count, o_count)
+    assert np.array_equal(length, o_len)
+    assert np.array_equal(score.view(np.uint64), o_score.view(np.uint64))   # 0 ULP
+    assert np.array_equal(codes, o_codes)
+    assert (ex, tu) == (o_ex, o_tu)
+
+
+def test_full_size_properties(gpu_decoder):
+    """64K sentences, k=16: deterministic, sorted, and every path is a chain of
+    spans from 0 to n made of the sentence's own nodes."""
+    raw = synth.make_lattices(65536, seed=7)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=7)
+    packed, keys, coefs = synth.pack_fast(raw, sm, lay, cols)
+    k = 16
+    dm = _capi.DeviceModel(gpu_decoder.ctx, keys, coefs)
+    db = _capi.DeviceBatch(gpu_decoder.ctx, packed, max_k=k)
+    r1 = db.decode(dm, k)
+    r2 = db.decode(dm, k)
+    for a, b in zip(r1, r2):
+        assert np.array_equal(a, b)
+    count, length, score, codes = r1
+    assert np.all(count == k)
+    assert np.all(np.diff(score, axis=1) <= 0)
+    # span chain check on a sample
+    node_b = lay.node_b
+    span_of = lambda g: (node_b[g], node_b[g] + 0)
+    n = packed.sent_n.astype(np.int64)
+    cum = np.r_[0, np.cumsum(n)]
+    rng = np.random.default_rng(0)
+    for s in rng.choice(len(n), size=200, replace=False):
+        for t in range(k):
+            L = length[s, t]
+            off = k * cum[s] + t * n[s]
+            local = codes[off:off + L].astype(np.int64)
+            g = packed.sent_node_off[s] + local
+            b = node_b[g]
+            # e of each node = b of the next one; first starts at 0
+            assert b[0] == 0
+            ends = np.r_[b[1:], n[s]]
+            assert np.all(ends > b) and np.all(ends - b <= 8)
+    db.close()
+    dm.close()
+
+
+def test_ragged_and_empty_batch(gpu_decoder):
+    from golden_io import load as gl
+    cases = [c for c in gl('edge') if c.model == 'edge_tri' and c.max_len == 8
+             and not any('error' in e for e in c.expected.values())]
+    # interleave empty and long sentences; results must not depend on batching
+    lats = [(c.bindex, c.chars) for c in cases]
+    funcs = cases[0].funcs
+    together = beam_search_batch(lats, funcs, beam_size=5)
+    for (b, ch), m in zip(lats, together):
+        alone = beam_search_batch([(b, ch)], funcs, beam_size=5)[0]
+        assert [float(x.score).hex() for x in m] == [float(x.score).hex() for x in alone]
+    assert beam_search_batch([], funcs, beam_size=3) == []

@@ -1,0 +1,107 @@
+"""Host packing (packer.py, lowering.py) + the C restatement (oracle/lt_oracle.c)
+reproduce the reference's golden vectors, and the vectorised synthetic packer
+(synth.pack_fast) builds the same batch as packer.pack on the Word rendering."""
+
+import numpy as np
+import pytest
+
+from golden_io import SETS, load, path_matches
+from lattice_based_tagger_amd import lowering, packer, synth
+from lattice_based_tagger_amd import score_funcs as SF, feature as FE
+from oracle import lt_oracle, ref_beam
+
+
+def _groups(cases):
+    out = {}
+    for c in cases:
+        out.setdefault((id(c.funcs), c.max_len), []).append(c)
+    return out.values()
+
+
+@pytest.mark.parametrize('name', SETS)
+def test_c_oracle_on_packed_golden(name):
+    for group in _groups(load(name)):
+        model = lowering.LoweredModel(group[0].funcs)
+        ok_cases = []
+        for c in group:
+            try:
+                packer.pack([(c.bindex, c.chars)], model, c.max_len)
+                ok_cases.append(c)
+            except IndexError:
+                assert all(e.get('error') == 'IndexError' for e in c.expected.values())
+        if not ok_cases:
+            continue
+        pk, objs = packer.pack([(c.bindex, c.chars) for c in ok_cases], model, ok_cases[0].max_len)
+        cum = np.r_[0, np.cumsum(pk.sent_n)]
+        for k in (1, 5, 16):
+            count, length, score, codes, _, _ = lt_oracle.decode(pk, model.keys, model.coefs, k)
+            for s, c in enumerate(ok_cases):
+                exp = c.expected[str(k)]['matures']
+                assert count[s] == len(exp), (c.tag, k)
+                n = len(c.chars)
+                for t, (ecodes, shex, _) in enumerate(exp):
+                    L = int(length[s, t])
+                    off = k * cum[s] + t * n
+                    words = [objs[s][x] for x in codes[off:off + L]]
+                    assert float(score[s, t]).hex() == shex, (c.tag, k, t)
+                    assert path_matches(c, ecodes, words), (c.tag, k, t)
+
+
+def test_pack_fast_equals_word_packer():
+    raw = synth.make_lattices(30, seed=5, eojeols=7)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=5, n_features=5000)
+    sents, dic, coef = synth.to_words(raw, sm)
+    funcs = SF.BeamScoreFunctions(SF.RegularizationScore(),
+                                  SF.SimpleTrigramFeatureScore(FE.SimpleTrigramEncoder(dic), coef))
+    lm = lowering.LoweredModel(funcs)
+    pk, _ = packer.pack(sents, lm)
+    fb, fkeys, fcoefs = synth.pack_fast(raw, sm, lay, cols)
+    # identical structure
+    for f in ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start'):
+        assert np.array_equal(getattr(pk, f), getattr(fb, f)), f
+    for f in ('node_pre', 'node_f4', 'node_f5', 'node_f6'):
+        assert np.array_equal(getattr(pk, f), getattr(fb, f)), f
+    flag_bits = np.uint32(0x1F0000)
+    assert np.array_equal(pk.node_mask & flag_bits, fb.node_mask & flag_bits)
+    # identical decode (ids differ by renaming only)
+    for k in (1, 4, 16):
+        a = lt_oracle.decode(pk, lm.keys, lm.coefs, k)
+        b = lt_oracle.decode(fb, fkeys, fcoefs, k)
+        for x, y in zip(a[:4], b[:4]):
+            assert np.array_equal(x, y)
+        assert a[4:] == b[4:]
+
+
+def test_c_oracle_counts_match_python_oracle():
+    raw = synth.make_lattices(12, seed=8, eojeols=5)
+    sm = synth.make_model(raw, seed=8, n_features=2000)
+    sents, dic, coef = synth.to_words(raw, sm)
+    funcs = SF.BeamScoreFunctions(SF.RegularizationScore(),
+                                  SF.SimpleTrigramFeatureScore(FE.SimpleTrigramEncoder(dic), coef))
+    lm = lowering.LoweredModel(funcs)
+    pk, _ = packer.pack(sents, lm)
+    for k in (1, 5):
+        ex = tu = 0
+        for b, c in sents:
+            x, p = ref_beam.count_ops(b, c, funcs, k)
+            ex += x
+            tu += p
+        res = lt_oracle.decode(pk, lm.keys, lm.coefs, k)
+        assert (res[4], res[5]) == (ex, tu)
+
+
+def test_packer_rejects_short_bindex():
+    funcs = SF.BeamScoreFunctions(SF.RegularizationScore())
+    lm = lowering.LoweredModel(funcs)
+    with pytest.raises(IndexError):
+        packer.pack([([], 'abc')], lm)
+
+
+def test_unsupported_scorer_raises():
+    class Custom(SF.BeamScoreFunction):
+        def score(self, seq, w):
+            return 1.0
+    with pytest.raises(NotImplementedError):
+        lowering.LoweredModel(SF.BeamScoreFunctions(Custom()))
