@@ -125,7 +125,7 @@ lt_status lt_last_kernel_ms(lt_ctx* ctx, float* ms);
  *   length[s*k + t]        words in mature t, excluding BOS/EOS
  *   score[s*k + t]         float64 path score (after the EOS `+ 0`)
  *   codes[k*off_s + t*n_s + j]  local node index of word j of mature t
- *                          (off_s = sum_{s'<s} n_{s'})
+ *                          (off_s = sum_{s'<s} n_{s'}); slots j >= length are -1
  * Matures are ordered best first, ties by expansion order (beam.py:85). */
 typedef struct {
   int32_t* count;    /* [n_sent] */

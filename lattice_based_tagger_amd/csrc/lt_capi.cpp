@@ -412,6 +412,9 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
+  // code slots past a path's length read as -1 (deterministic output)
+  const size_t ncodes = (size_t)b->total_chars * k;
+  if (ncodes) HIP_TRY(hipMemsetAsync(b->d_codes, 0xFF, ncodes * 4, c->stream));
   HIP_TRY(hipEventRecord(c->ev0, c->stream));
   HIP_TRY(launch_decode(p, c->stream, false));
   HIP_TRY(hipEventRecord(c->ev1, c->stream));

@@ -355,6 +355,10 @@ lt_decode_k(DecodeParams p) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const int nm = cnt[grp][n % RING];
   if (gl == 0) p.out_count[s] = nm;
+  if (gl >= nm && gl < k) {                  // unused mature slots read as empty
+    p.out_score[(int64_t)s * k + gl] = 0.0;
+    p.out_len[(int64_t)s * k + gl] = 0;
+  }
   if (gl < nm) {
     const Entry& f = R[n % RING][gl];
     const int64_t o = (int64_t)s * k + gl;
