@@ -224,7 +224,7 @@ def main():
                 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS,
                 'traffic': None,
-                'kernel': 'lt_decode_k',
+                'kernel': 'lt_viterbi_k' if a.k == 1 else 'lt_beam_k',
                 'algorithmic_bytes_per_launch': B,
                 'avg_kernel_ms': avg_kernel_s * 1e3,
             },

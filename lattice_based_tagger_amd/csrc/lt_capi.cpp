@@ -64,9 +64,79 @@ struct lt_ctx {
 
 struct lt_model {
   lt_ctx* ctx = nullptr;
-  Slot* d_table = nullptr;
+  void* d_table = nullptr;
   int64_t slots = 0;
+  uint32_t seed = 0;
+  int narrow = 0;          // 16 B SlotN (all ids < 2^20) or 32 B SlotW
 };
+
+namespace {
+
+struct KeyRec {
+  uint32_t a, b, c, cls;
+  double coef;
+};
+
+// Cuckoo table build (two choices, one slot per bucket).  Returns false when
+// the random walk fails; the caller reseeds / grows and retries.
+template <class SlotT>
+bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed,
+                  std::vector<SlotT>& tab, int64_t* dup) {
+  tab.assign(slots, SlotT{});
+  std::vector<int32_t> who(slots, -1);          // key index held by each slot
+  uint64_t rng = 0x9E3779B97F4A7C15ull ^ seed;
+  const int max_kicks = 2000;
+  for (int32_t i = 0; i < (int32_t)keys.size(); ++i) {
+    int32_t cur = i;
+    uint32_t i1, i2;
+    {
+      const KeyRec& k = keys[(size_t)i];
+      cuckoo_slots(key_base(k.a, k.b, k.c, k.cls), seed, slots, i1, i2);
+      for (uint32_t x : {i1, i2}) {
+        const int32_t w = who[x];
+        if (w >= 0 && keys[(size_t)w].a == k.a && keys[(size_t)w].b == k.b &&
+            keys[(size_t)w].c == k.c && keys[(size_t)w].cls == k.cls) {
+          *dup = i;
+          return false;
+        }
+      }
+    }
+    uint32_t pos = 0;
+    bool placed = false;
+    for (int kick = 0; kick < max_kicks; ++kick) {
+      const KeyRec& k = keys[(size_t)cur];
+      cuckoo_slots(key_base(k.a, k.b, k.c, k.cls), seed, slots, i1, i2);
+      uint32_t target;
+      if (who[i1] < 0) target = i1;
+      else if (who[i2] < 0) target = i2;
+      else {
+        rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+        target = (kick == 0) ? ((rng & 1) ? i1 : i2) : (pos == i1 ? i2 : i1);
+        if (i1 == i2) target = i1;
+      }
+      const int32_t evicted = who[target];
+      who[target] = cur;
+      if (evicted < 0) { placed = true; break; }
+      cur = evicted;
+      pos = target;                              // the evicted key must leave this slot
+    }
+    if (!placed) return false;
+  }
+  for (uint32_t x = 0; x < slots; ++x) {
+    if (who[x] < 0) continue;
+    const KeyRec& k = keys[(size_t)who[x]];
+    SlotT& sl = tab[x];
+    if constexpr (sizeof(SlotT) == sizeof(SlotN)) {
+      sl.key = narrow_key(k.a, k.b, k.c, k.cls);
+      sl.coef = k.coef;
+    } else {
+      sl.a = k.a; sl.b = k.b; sl.c = k.c; sl.cls1 = k.cls + 1; sl.coef = k.coef;
+    }
+  }
+  return true;
+}
+
+}  // namespace
 
 struct lt_batch {
   lt_ctx* ctx = nullptr;
@@ -76,9 +146,8 @@ struct lt_batch {
   // device inputs
   int32_t *d_order = nullptr, *d_sent_n = nullptr, *d_span_start = nullptr;
   int64_t *d_node_off = nullptr, *d_span_off = nullptr, *d_bp_off = nullptr, *d_cum_n = nullptr;
-  int32_t *d_word = nullptr, *d_morph = nullptr, *d_tag = nullptr;
-  uint32_t* d_mask = nullptr;
-  double *d_pre = nullptr, *d_f4 = nullptr, *d_f5 = nullptr, *d_f6 = nullptr, *d_post = nullptr;
+  NodeRec* d_nodes = nullptr;
+  double* d_post = nullptr;
   // scratch + device results (sized for max_k)
   uint32_t* d_bp = nullptr;
   int32_t *d_count = nullptr, *d_len = nullptr, *d_codes = nullptr;
@@ -149,15 +218,13 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
   if (d->n_keys < 0 || (d->n_keys > 0 && (!d->keys || !d->coefs)))
     return fail(LT_EINVAL, "lt_model_create: bad key arrays");
   if (d->n_keys > ((int64_t)1 << 29)) return fail(LT_EUNSUPPORTED, "lt_model_create: too many keys");
-  int64_t slots = 64;
-  while (slots < 2 * d->n_keys) slots <<= 1;
-  std::vector<Slot> tab;
+  std::vector<KeyRec> keys;
+  uint32_t max_id = 0;
   try {
-    tab.assign((size_t)slots, Slot{0u, 0u, 0u, EMPTY, 0.0, 0ull});
+    keys.resize((size_t)d->n_keys);
   } catch (...) {
-    return fail(LT_ENOMEM, "lt_model_create: cannot allocate %lld slots", (long long)slots);
+    return fail(LT_ENOMEM, "lt_model_create: out of host memory");
   }
-  const uint32_t mask = (uint32_t)(slots - 1);
   for (int64_t i = 0; i < d->n_keys; ++i) {
     const uint32_t a = d->keys[4 * i], b = d->keys[4 * i + 1], cc = d->keys[4 * i + 2],
                    cls = d->keys[4 * i + 3];
@@ -169,24 +236,45 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
       return fail(LT_EINVAL, "lt_model_create: key %lld has a bad component id", (long long)i);
     if (!std::isfinite(d->coefs[i]))
       return fail(LT_EUNSUPPORTED, "lt_model_create: non-finite coefficient at key %lld", (long long)i);
-    uint32_t h = key_hash(a, b, cc, cls) & mask;
-    for (;;) {
-      Slot& s = tab[h];
-      if (s.cls1 == EMPTY) {
-        s.a = a; s.b = b; s.c = cc; s.cls1 = cls + 1; s.coef = d->coefs[i];
-        break;
-      }
-      if (s.cls1 == cls + 1 && s.a == a && s.b == b && s.c == cc)
-        return fail(LT_EINVAL, "lt_model_create: duplicate key %lld", (long long)i);
-      h = (h + 1) & mask;
+    keys[(size_t)i] = KeyRec{a, b, cc, cls, d->coefs[i]};
+    max_id = std::max(max_id, std::max(a, std::max(b, cc)));
+  }
+  const bool narrow = max_id < (1u << NARROW_ID_BITS);
+  const int64_t slot_bytes = narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
+  int64_t slots = std::max<int64_t>(64, (int64_t)(d->n_keys / 0.45) + 1);   // load factor <= 0.45
+  std::vector<SlotN> tn;
+  std::vector<SlotW> tw;
+  uint32_t seed = 0x2545F491u;
+  bool ok = false;
+  for (int attempt = 0; attempt < 24 && !ok; ++attempt) {
+    if (slots * slot_bytes >= ((int64_t)1 << 31))
+      return fail(LT_EUNSUPPORTED, "lt_model_create: table of %lld slots exceeds 2 GiB",
+                  (long long)slots);
+    int64_t dup = -1;
+    try {
+      ok = narrow ? cuckoo_build(keys, (uint32_t)slots, seed, tn, &dup)
+                  : cuckoo_build(keys, (uint32_t)slots, seed, tw, &dup);
+    } catch (...) {
+      return fail(LT_ENOMEM, "lt_model_create: cannot allocate %lld slots", (long long)slots);
+    }
+    if (dup >= 0) return fail(LT_EINVAL, "lt_model_create: duplicate key %lld", (long long)dup);
+    if (!ok) {
+      seed = seed * 0x9E3779B1u + 0x7F4A7C15u;
+      if (attempt % 3 == 2) slots = slots + slots / 8;
     }
   }
+  if (!ok) return fail(LT_EINVAL, "lt_model_create: cuckoo table build failed");
   HIP_TRY(hipSetDevice(c->device));
   lt_model* m = new (std::nothrow) lt_model;
   if (!m) return fail(LT_ENOMEM, "lt_model_create: out of host memory");
   m->ctx = c;
   m->slots = slots;
-  hipError_t e = dalloc_copy(&m->d_table, tab.data(), tab.size(), c->stream);
+  m->seed = seed;
+  m->narrow = narrow ? 1 : 0;
+  hipError_t e = hipMalloc(&m->d_table, (size_t)(slots * slot_bytes));
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(m->d_table, narrow ? (const void*)tn.data() : (const void*)tw.data(),
+                       (size_t)(slots * slot_bytes), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     dfree(m->d_table);
@@ -219,6 +307,9 @@ static lt_status validate(const lt_batch_desc* d) {
                          !d->node_pre || !d->node_f4 || !d->node_f5 || !d->node_f6))
     return fail(LT_EINVAL, "batch: NULL node arrays");
   if (d->n_post > 0 && !d->node_post) return fail(LT_EINVAL, "batch: NULL node_post");
+  if (d->n_nodes * (int64_t)sizeof(NodeRec) >= ((int64_t)1 << 31))
+    return fail(LT_EUNSUPPORTED, "batch: %lld nodes exceed one launch (2^31 B of node records); split the batch",
+                (long long)d->n_nodes);
   if (d->n_span > 0 && !d->span_start) return fail(LT_EINVAL, "batch: NULL span_start");
   if (d->sent_node_off[0] != 0 || d->sent_span_off[0] != 0)
     return fail(LT_EINVAL, "batch: offsets must start at 0");
@@ -268,8 +359,7 @@ static lt_status validate(const lt_batch_desc* d) {
 static void batch_free(lt_batch* b) {
   if (!b) return;
   void* dev[] = {b->d_order, b->d_sent_n, b->d_span_start, b->d_node_off, b->d_span_off,
-                 b->d_bp_off, b->d_cum_n, b->d_word, b->d_morph, b->d_tag, b->d_mask,
-                 b->d_pre, b->d_f4, b->d_f5, b->d_f6, b->d_post, b->d_bp, b->d_count,
+                 b->d_bp_off, b->d_cum_n, b->d_nodes, b->d_post, b->d_bp, b->d_count,
                  b->d_len, b->d_codes, b->d_score};
   for (void* p : dev) dfree(p);
   void* host[] = {b->h_count, b->h_len, b->h_codes, b->h_score};
@@ -325,14 +415,28 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   up(&b->d_bp_off, bp_off.data(), (size_t)S + 1);
   up(&b->d_cum_n, cum_n.data(), (size_t)S + 1);
   up(&b->d_span_start, d->span_start, (size_t)d->n_span);
-  up(&b->d_word, d->node_word, (size_t)d->n_nodes);
-  up(&b->d_morph, d->node_morph0, (size_t)d->n_nodes);
-  up(&b->d_tag, d->node_tag, (size_t)d->n_nodes);
-  up(&b->d_mask, d->node_mask, (size_t)d->n_nodes);
-  up(&b->d_pre, d->node_pre, (size_t)d->n_nodes);
-  up(&b->d_f4, d->node_f4, (size_t)d->n_nodes);
-  up(&b->d_f5, d->node_f5, (size_t)d->n_nodes);
-  up(&b->d_f6, d->node_f6, (size_t)d->n_nodes);
+  // device node records: AoS, mask + each node's span length d-1 (bits 24-26)
+  std::vector<NodeRec> recs((size_t)d->n_nodes);
+  for (int64_t i = 0; i < d->n_nodes; ++i) {
+    NodeRec& r = recs[(size_t)i];
+    r.word = (uint32_t)d->node_word[i];
+    r.morph = (uint32_t)d->node_morph0[i];
+    r.tag = (uint32_t)d->node_tag[i];
+    r.mask = d->node_mask[i] & ~(D_MASK | F_WI);
+    r.pre = d->node_pre[i];
+    r.f4 = d->node_f4[i];
+    r.f5 = d->node_f5[i];
+    r.f6 = d->node_f6[i];
+  }
+  for (int32_t s = 0; s < S; ++s) {
+    const int32_t* ss = d->span_start + d->sent_span_off[s];
+    const int64_t base = d->sent_node_off[s];
+    for (int64_t x = 0; x < (int64_t)LT_MAX_SPAN * d->sent_n[s]; ++x) {
+      const uint32_t dd = (uint32_t)(LT_MAX_SPAN - (x % LT_MAX_SPAN));
+      for (int32_t v = ss[x]; v < ss[x + 1]; ++v) recs[(size_t)(base + v)].mask |= (dd - 1u) << D_SHIFT;
+    }
+  }
+  up(&b->d_nodes, recs.data(), recs.size());
   up(&b->d_post, d->node_post, (size_t)d->n_post * (size_t)d->n_nodes);
   const size_t nres = (size_t)S * max_k;
   const size_t ncodes = (size_t)b->total_chars * max_k;
@@ -374,7 +478,9 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   if (beam_template_for(k) < 0) return fail(LT_EUNSUPPORTED, "decode: beam %d not compiled", k);
   p = DecodeParams{};
   p.table = m->d_table;
-  p.tmask = (uint32_t)(m->slots - 1);
+  p.slots = (uint32_t)m->slots;
+  p.seed = m->seed;
+  p.narrow = m->narrow;
   p.has_tri = b->has_tri;
   p.n_sent = b->n_sent;
   p.max_len = b->max_len;
@@ -387,14 +493,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.node_off = b->d_node_off;
   p.span_off = b->d_span_off;
   p.span_start = b->d_span_start;
-  p.nword = b->d_word;
-  p.nmorph = b->d_morph;
-  p.ntag = b->d_tag;
-  p.nmask = b->d_mask;
-  p.npre = b->d_pre;
-  p.nf4 = b->d_f4;
-  p.nf5 = b->d_f5;
-  p.nf6 = b->d_f6;
+  p.nodes = b->d_nodes;
   p.npost = b->d_post;
   p.bp = b->d_bp;
   p.bp_off = b->d_bp_off;

@@ -27,37 +27,63 @@ constexpr uint32_t F_CTX = 1u << 17;   // tag0 in {Noun, Adverb, Adjective, Verb
 constexpr uint32_t F_HAS4 = 1u << 18;
 constexpr uint32_t F_HAS5 = 1u << 19;
 constexpr uint32_t F_HAS6 = 1u << 20;
-constexpr uint32_t F_WI = 1u << 31;    // (hypothesis entry only) wi exists
 constexpr uint32_t FLAG_BITS = 0x1F0000u;
+// set by the library on its device copy of the mask: span length d-1 of the
+// node (bits 24-26); bit 31 marks "wi exists" in hypothesis entries.
+constexpr int D_SHIFT = 24;
+constexpr uint32_t D_MASK = 7u << D_SHIFT;
+constexpr uint32_t F_WI = 1u << 31;
 
 constexpr int MAX_SPAN = 8;
 constexpr int RING = MAX_SPAN + 1;     // frontier positions e-8 .. e
-constexpr uint32_t EMPTY = 0u;         // slot.cls1 of an empty slot
 
-// One hash-table slot: key {a, b, c, class+1} + coefficient.  32 B, so a
-// slot never straddles a 64 B line.
-struct alignas(32) Slot {
+// -- feature hash table ----------------------------------------------------
+// Narrow slot (16 B): exact 64-bit key cls<<60 | a<<40 | b<<20 | c, valid
+// when every interned id is < 2^20.  key 0 = empty (ids are >= 1).
+constexpr int NARROW_ID_BITS = 20;
+struct alignas(16) SlotN {
+  uint64_t key;
+  double coef;
+};
+// Wide slot (32 B): {a, b, c, class+1}; cls1 0 = empty.
+struct alignas(32) SlotW {
   uint32_t a, b, c, cls1;
   double coef;
   uint64_t pad;
 };
 
-// 32-bit mix of the interned key.  Identical on host (table build) and
-// device (probe).
-LT_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-LT_HD uint32_t key_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
-  uint32_t h = cls * 0x27D4EB2Fu + 0x165667B1u;
-  h ^= a * 0x9E3779B1u;
-  h = rotl32(h, 13) * 0x85EBCA77u;
-  h ^= b * 0xC2B2AE3Du;
-  h = rotl32(h, 17) * 0x9E3779B1u;
-  h ^= c * 0x85EBCA77u;
-  // fmix32
-  h ^= h >> 16; h *= 0x85EBCA6Bu;
-  h ^= h >> 13; h *= 0xC2B2AE35u;
+LT_HD uint64_t narrow_key(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+  return ((uint64_t)cls << 60) | ((uint64_t)a << 40) | ((uint64_t)b << 20) | (uint64_t)c;
+}
+
+// Cuckoo hashing: every key lives in one of its two candidate slots
+// i1 = mulhi(h1, slots), i2 = mulhi(h2, slots), so a lookup is exactly two
+// independent loads (no probe chains).  Identical on host and device.
+LT_HD uint32_t key_base(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+  return (a * 0x9E3779B1u) ^ (b * 0x85EBCA77u) ^ (c * 0xC2B2AE3Du) ^ (cls * 0x27D4EB2Fu);
+}
+LT_HD uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
   h ^= h >> 16;
   return h;
 }
+LT_HD uint32_t slot_of(uint32_t h, uint32_t slots) {
+  return (uint32_t)(((uint64_t)h * slots) >> 32);
+}
+LT_HD void cuckoo_slots(uint32_t base, uint32_t seed, uint32_t slots, uint32_t& i1, uint32_t& i2) {
+  i1 = slot_of(fmix32(base ^ seed), slots);
+  i2 = slot_of(fmix32(base ^ seed ^ 0x5BD1E995u), slots);
+}
+
+// Device node record (AoS, 48 B = 3 x 16 B loads), built by the library from
+// the SoA arrays of lt_batch_desc.
+struct alignas(16) NodeRec {
+  uint32_t word, morph, tag, mask;
+  double pre, f4, f5, f6;
+};
 
 // Backpointer word: local node index (24 b) | span d-1 (3 b) | parent rank (5 b)
 LT_HD uint32_t bp_pack(uint32_t node, uint32_t d, uint32_t r) {

@@ -9,25 +9,26 @@
 //   SimpleTrigramFeatureScore.score  score_funcs.py:137-144
 //   trigram_encoder        features/feature.py:76-121
 //
-// Execution model:
-//  * a group of G lanes (G = 16/32/64, inside one wave64) owns one sentence;
-//    256-thread blocks hold 256/G sentences; no block-level barriers.
-//  * the frontier -- beams of the last 9 end positions -- lives in LDS as a
-//    ring; each hypothesis entry caches the fields of its last two nodes, so
-//    scoring an expansion reads the candidate node from HBM and the
-//    hypothesis from LDS only.
-//  * expansions of end position e are enumerated in the reference's
-//    generation order g (begin ascending, hypothesis rank, candidate order);
-//    lane l takes g = l, l+G, ...; ties are broken by lower g exactly as
-//    Python's stable sort does.
-//  * trigram features: classes 4/5/6 arrive pre-resolved per node; classes
-//    0,1,2,3,7,8 are probed in an open-addressing table (32 B slots), all
-//    probes of an expansion issued before any is resolved.  The present
-//    coefficients are summed in numpy's pairwise order (H7).
-//  * top-k: every lane keeps its own top-k of the expansions it scored
-//    (registers), then k rounds of group argmax merge them.
-//  * backpointers (4 B per beam entry) go to HBM; the final backtrace walks
-//    them per mature.
+// Two kernels:
+//  * lt_viterbi_k  -- beam_size 1.  A 16-lane group owns one sentence; the
+//    candidates of end position e are the contiguous node range
+//    [A_e, A_{e+1}) of the packed layout, lane l scores node A_e + l.  The
+//    next position's span start and candidate node fields are loaded while
+//    the current position is scored (software prefetch), so the only
+//    dependent memory round trip per position is the hash probe.  The
+//    winner lane writes the new frontier entry from its registers.
+//  * lt_beam_k<KT,G> -- beam_size 2..32.  Expansions enumerated in the
+//    reference's generation order (begin ascending, hypothesis rank,
+//    candidate order), each lane keeps its own top-k, k rounds of group
+//    argmax merge them.
+// Both: the frontier (beams of the last 9 end positions) lives in LDS as a
+// ring whose entries cache the fields of the hypothesis' last two nodes;
+// trigram classes 4/5/6 arrive pre-resolved per node, classes 0,1,2,3,7,8 are
+// probed in an open-addressing table -- all probes of an expansion issued
+// together as buffer loads, an unneeded probe gets an out-of-range offset
+// (returns 0, touches no memory) instead of a branch.  Present coefficients
+// are summed in numpy's pairwise order; ties go to the lower
+// generation index (Python's stable sort).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include "lt_common.h"
@@ -38,19 +39,72 @@ using namespace lt;
 namespace {
 
 constexpr uint32_t INV = 0xFFFFFFFFu;
+constexpr uint32_t OOB = 0x80000000u;   // >= every buffer's num_records (host-checked)
 
-struct alignas(16) Entry {
-  double score;     // path score
-  double f6;        // coefficient of (6, min(8, wj.len)) when wj has F_HAS6
-  int32_t node;     // local node index of wj (the last node)
-  int32_t jword, jmorph, jtag;
-  uint32_t jmask;   // wj mask + flags
-  int32_t iword, imorph;
-  uint32_t imask;   // wi mask + flags, F_WI when wi exists
-  int32_t depth;    // words on the path, BOS excluded
-  int32_t pad[3];
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* ptr, uint64_t bytes) {
+  const uint32_t nr = bytes >= 0x80000000ull ? 0x7FFFFFFFu : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, (int)nr, 0x00020000);
+}
+__device__ __forceinline__ u32x4 ld128(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+
+struct Bufs {
+  rsrc_t node, tab;
 };
-static_assert(sizeof(Entry) == 64, "Entry must be 64 B");
+
+__device__ __forceinline__ Bufs make_bufs(const DecodeParams& p) {
+  Bufs B;
+  B.node = make_rsrc(p.nodes, (uint64_t)p.n_nodes * sizeof(NodeRec));
+  const uint64_t slot_bytes = p.narrow ? sizeof(SlotN) : sizeof(SlotW);
+  B.tab = make_rsrc(p.table, (uint64_t)p.slots * slot_bytes);
+  return B;
+}
+
+// Candidate node fields (gn = global node index; INV -> zeros, no access).
+struct Cand {
+  uint32_t word, morph, tag, mask;
+  double pre, f4, f5, f6;
+};
+
+__device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) {
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ Cand load_cand(const Bufs& B, uint32_t gn) {
+  const uint32_t o = gn == INV ? OOB : gn * (uint32_t)sizeof(NodeRec);
+  const u32x4 a = ld128(B.node, o);
+  const u32x4 b = ld128(B.node, o == OOB ? OOB : o + 16u);
+  const u32x4 c4 = ld128(B.node, o == OOB ? OOB : o + 32u);
+  Cand c;
+  c.word = a.x; c.morph = a.y; c.tag = a.z; c.mask = a.w;
+  c.pre = dbl(b.x, b.y); c.f4 = dbl(b.z, b.w);
+  c.f5 = dbl(c4.x, c4.y); c.f6 = dbl(c4.z, c4.w);
+  return c;
+}
+
+// Pin prefetched values in registers: the empty asm makes them opaque, so the
+// compiler cannot re-issue ("rematerialise") the loads at their later use.
+__device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(double& x) {
+  uint64_t b = __builtin_bit_cast(uint64_t, x);
+  asm volatile("" : "+v"(b));
+  x = __builtin_bit_cast(double, b);
+}
+__device__ __forceinline__ void pin(Cand& c) {
+  pin(c.word); pin(c.morph); pin(c.tag); pin(c.mask);
+  pin(c.pre); pin(c.f4); pin(c.f5); pin(c.f6);
+}
+
+// Hypothesis fields the scorer needs (from the LDS frontier).
+struct Hyp {
+  double score, f6;
+  uint32_t jword, jmorph, jtag, jmask, iword, imorph, imask, depth;
+};
 
 __device__ __forceinline__ bool better(double s1, uint32_t g1, double s2, uint32_t g2) {
   // (score desc, generation index asc); INV never wins.
@@ -63,10 +117,31 @@ template <int G>
 __device__ __forceinline__ void group_argmax(double& s, uint32_t& g) {
 #pragma unroll
   for (int off = G / 2; off >= 1; off >>= 1) {
-    double os = __shfl_xor(s, off, G);
-    uint32_t og = __shfl_xor(g, off, G);
+    const double os = __shfl_xor(s, off, G);
+    const uint32_t og = __shfl_xor(g, off, G);
     if (better(os, og, s, g)) { s = os; g = og; }
   }
+}
+
+// Argmax over one 16-lane DPP row (the k=1 lane group): quad xor-1, quad
+// xor-2, half-row mirror, row mirror -- register-to-register, no LDS trip.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ void dpp_step(double& s, uint32_t& g) {
+  const uint64_t bits = __builtin_bit_cast(uint64_t, s);
+  const uint32_t lo = dpp_u32<CTRL>((uint32_t)bits), hi = dpp_u32<CTRL>((uint32_t)(bits >> 32));
+  const double os = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+  const uint32_t og = dpp_u32<CTRL>(g);
+  if (better(os, og, s, g)) { s = os; g = og; }
+}
+__device__ __forceinline__ void row16_argmax(double& s, uint32_t& g) {
+  dpp_step<0xB1>(s, g);    // quad_perm [1,0,3,2]
+  dpp_step<0x4E>(s, g);    // quad_perm [2,3,0,1]
+  dpp_step<0x141>(s, g);   // row_half_mirror
+  dpp_step<0x140>(s, g);   // row_mirror
 }
 
 template <int G>
@@ -74,31 +149,6 @@ __device__ __forceinline__ unsigned long long group_sum(unsigned long long v) {
 #pragma unroll
   for (int off = G / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off, G);
   return v;
-}
-
-// Probe the table for key (a,b,c,cls); returns true and the coefficient if
-// present.  `first` is the already-loaded slot at the home index.
-__device__ __forceinline__ bool resolve(const Slot* __restrict__ tab, uint32_t tmask,
-                                        uint32_t h, Slot first, uint32_t a, uint32_t b,
-                                        uint32_t c, uint32_t cls1, double& coef) {
-  Slot sl = first;
-  for (;;) {
-    if (sl.cls1 == cls1 && sl.a == a && sl.b == b && sl.c == c) { coef = sl.coef; return true; }
-    if (sl.cls1 == EMPTY) return false;
-    h = (h + 1u) & tmask;
-    sl = tab[h];
-  }
-}
-
-__device__ __forceinline__ Slot load_slot(const Slot* __restrict__ tab, uint32_t h) {
-  const uint4* p = reinterpret_cast<const uint4*>(tab + h);
-  uint4 k = p[0];
-  uint4 v = p[1];
-  Slot s;
-  s.a = k.x; s.b = k.y; s.c = k.z; s.cls1 = k.w;
-  s.coef = __hiloint2double((int)v.y, (int)v.x);
-  s.pad = 0;
-  return s;
 }
 
 // Sum of the present features in numpy's pairwise order
@@ -126,46 +176,381 @@ __device__ __forceinline__ double numpy_sum9(const double (&v)[9], const bool (&
   return s;
 }
 
-template <int KT, int G, bool COUNT>
+// Slot access per table format.
+template <bool NARROW>
+struct Tab;
+
+template <>
+struct Tab<true> {
+  static constexpr uint32_t SZ = sizeof(SlotN);
+  struct S { uint64_t key; double coef; };
+  __device__ static S load(rsrc_t t, uint32_t off) {
+    const u32x4 v = ld128(t, off);
+    S s;
+    s.key = ((uint64_t)v.y << 32) | v.x;
+    s.coef = __builtin_bit_cast(double, (u32x2){v.z, v.w});
+    return s;
+  }
+  // 0 = empty, 1 = hit, 2 = other key (continue)
+  __device__ static int test(const S& s, uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+    if (s.key == narrow_key(a, b, c, cls)) return 1;
+    return s.key == 0 ? 0 : 2;
+  }
+};
+
+template <>
+struct Tab<false> {
+  static constexpr uint32_t SZ = sizeof(SlotW);
+  struct S { uint32_t a, b, c, cls1; double coef; };
+  __device__ static S load(rsrc_t t, uint32_t off) {
+    const u32x4 k = ld128(t, off);
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(t, off == OOB ? OOB : off + 16u, 0, 0);
+    S s;
+    s.a = k.x; s.b = k.y; s.c = k.z; s.cls1 = k.w;
+    s.coef = __builtin_bit_cast(double, v);
+    return s;
+  }
+  __device__ static int test(const S& s, uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+    if (s.cls1 == cls + 1 && s.a == a && s.b == b && s.c == c) return 1;
+    return s.cls1 == 0 ? 0 : 2;
+  }
+};
+
+struct Counts {
+  unsigned long long exp = 0, tup = 0, probe = 0;
+};
+
+// Trigram score of appending candidate c after hypothesis h
+// (score_funcs.py:137-144 over feature.py:76-121), in two phases so that
+// other loads can be issued while the probes are in flight:
+//   probe_issue   -- keys, hashes, one buffer load per needed probe
+//   probe_finish  -- match / collision chains, numpy-order sum
+template <bool NARROW>
+struct Probe {
+  typename Tab<NARROW>::S s1[6], s2[6];   // the two cuckoo candidates
+  uint32_t need;                           // bit q: probe q is needed
+};
+
+// Key components of probe q for (h, c); recomputed where needed instead of
+// being kept live across the memory wait.
+struct Keys {
+  uint32_t a[6], b[6], c[6];
+};
+__device__ __forceinline__ Keys make_keys(const Hyp& h, const Cand& c, bool use_j8) {
+  Keys K;
+  // class 0 (wj.word, wk.word, tk) .. class 3 (tj, tk), class 7 (wi, wj, wk)
+  K.a[0] = h.jword; K.b[0] = c.word; K.c[0] = c.tag;
+  K.a[1] = h.jword; K.b[1] = c.tag;  K.c[1] = 0;
+  K.a[2] = h.jtag;  K.b[2] = c.word; K.c[2] = c.tag;
+  K.a[3] = h.jtag;  K.b[3] = c.tag;  K.c[3] = 0;
+  K.a[4] = h.iword; K.b[4] = h.jword; K.c[4] = c.word;
+  // class 8: (wj.morph0 | wi.morph0, wk.morph0) (feature.py:113-119)
+  K.a[5] = use_j8 ? h.jmorph : h.imorph; K.b[5] = c.morph; K.c[5] = 0;
+  return K;
+}
+
+constexpr uint32_t PCLS[6] = {0, 1, 2, 3, 7, 8};
+
+__device__ __forceinline__ bool use_j8_of(const Hyp& h, const Cand& c) {
+  return (c.mask & F_CTX) && (h.jmask & F_CTX);
+}
+
+// Which of the six probed classes can be present (exact pre-filter on the
+// component-slot bits; an absent class issues no load).
+__device__ __forceinline__ uint32_t probe_need(const Hyp& h, const Cand& c) {
+  const uint32_t jm = h.jmask, km = c.mask, im = h.imask;
+  const bool has_i = (im & F_WI) != 0;
+  const bool k_ctx = (km & F_CTX) != 0, j_ctx = (jm & F_CTX) != 0;
+  const bool use_j8 = k_ctx && j_ctx;
+  const bool use_i8 = k_ctx && !j_ctx && has_i && (im & F_CTX);
+  uint32_t need = 0;
+  need |= ((jm & J0A) && (km & K0B) && (km & K0C)) ? 1u : 0u;
+  need |= ((jm & J1A) && (km & K1B)) ? 2u : 0u;
+  need |= ((jm & J2A) && (km & K2B) && (km & K2C)) ? 4u : 0u;
+  need |= ((jm & J3A) && (km & K3B)) ? 8u : 0u;
+  need |= (has_i && (im & I7A) && (jm & J7B) && (km & K7C)) ? 16u : 0u;
+  need |= (use_j8 ? ((jm & J8A) && (km & K8B)) : (use_i8 && (im & I8A) && (km & K8B))) ? 32u : 0u;
+  return need;
+}
+
+template <bool NARROW>
+__device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uint32_t slots,
+                                            uint32_t seed, const Hyp& h, const Cand& c,
+                                            uint32_t need) {
+  using T = Tab<NARROW>;
+  P.need = need;
+  const Keys K = make_keys(h, c, use_j8_of(h, c));
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    uint32_t i1, i2;
+    cuckoo_slots(key_base(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
+    const bool nq = (need >> q) & 1u;
+    P.s1[q] = T::load(B.tab, nq ? i1 * T::SZ : OOB);
+    P.s2[q] = T::load(B.tab, nq ? i2 * T::SZ : OOB);
+  }
+}
+
+template <bool NARROW, bool COUNT>
+__device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp& h,
+                                               const Cand& c, Counts& cnt) {
+  using T = Tab<NARROW>;
+  const uint32_t jm = h.jmask, km = c.mask, im = h.imask;
+  const bool use_j8 = use_j8_of(h, c);
+  const Keys K = make_keys(h, c, use_j8);
+  bool pr6[6];
+  double cf[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const bool m1 = T::test(P.s1[q], K.a[q], K.b[q], K.c[q], PCLS[q]) == 1;
+    const bool m2 = T::test(P.s2[q], K.a[q], K.b[q], K.c[q], PCLS[q]) == 1;
+    pr6[q] = ((P.need >> q) & 1u) && (m1 || m2);
+    cf[q] = m1 ? P.s1[q].coef : P.s2[q].coef;
+  }
+  double v[9];
+  bool pr[9];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { v[q] = cf[q]; pr[q] = pr6[q]; }
+  v[4] = c.f4; pr[4] = (km & F_HAS4) != 0;
+  v[5] = c.f5; pr[5] = (km & F_HAS5) != 0;
+  v[6] = h.f6; pr[6] = (jm & F_HAS6) != 0;
+  v[7] = cf[4]; pr[7] = pr6[4];
+  v[8] = cf[5]; pr[8] = pr6[5];
+  if (COUNT) {
+    const bool has_i = (im & F_WI) != 0;
+    const bool use_i8 = (km & F_CTX) && !(jm & F_CTX) && has_i && (im & F_CTX);
+    cnt.tup += 6 + ((jm & F_UNK) ? 1 : 0) + (has_i ? 1 : 0) + ((use_j8 || use_i8) ? 1 : 0);
+    cnt.probe += __builtin_popcount(P.need);
+  }
+  return numpy_sum9(v, pr);
+}
+
+template <bool NARROW, bool COUNT>
+__device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_t seed,
+                                          const Hyp& h, const Cand& c, Counts& cnt) {
+  Probe<NARROW> P;
+  probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c));
+  return probe_finish<NARROW, COUNT>(P, h, c, cnt);
+}
+
+// inc = ((0 + pre...) + tri) + post...   (score_funcs.py:50-54)
+__device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c, double tri,
+                                            uint32_t gn) {
+  double inc = c.pre + tri;
+  for (int t = 0; t < p.n_post; ++t) inc += p.npost[(int64_t)t * p.n_nodes + gn];
+  return inc;
+}
+
+// ===========================================================================
+// beam_size = 1
+// ===========================================================================
+constexpr int V_G = 16;                 // lanes per sentence
+constexpr int V_SPB = 256 / V_G;        // sentences per block
+constexpr int V_BP_LDS = 256;           // end positions whose backpointer stays in LDS
+
+struct alignas(16) VEntry {
+  double score, f6;
+  uint32_t jword, jmorph, jtag, jmask;
+  uint32_t iword, imorph, imask, depth;
+};
+
+__device__ __forceinline__ Hyp read_hyp(const VEntry& e) {
+  Hyp h;
+  h.score = e.score; h.f6 = e.f6;
+  h.jword = e.jword; h.jmorph = e.jmorph; h.jtag = e.jtag; h.jmask = e.jmask;
+  h.iword = e.iword; h.imorph = e.imorph; h.imask = e.imask; h.depth = e.depth;
+  return h;
+}
+
+template <bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(256)
-lt_decode_k(DecodeParams p) {
+lt_viterbi_k(DecodeParams p) {
+  __shared__ VEntry ring[V_SPB][RING];
+  __shared__ uint32_t bpl[V_SPB][V_BP_LDS];
+
+  const int grp = threadIdx.x / V_G;
+  const int gl = threadIdx.x % V_G;
+  const int slot = blockIdx.x * V_SPB + grp;
+  if (slot >= p.n_sent) return;
+  const Bufs B = make_bufs(p);
+  const int s = p.order[slot];
+  const int n = p.sent_n[s];
+  const uint32_t nbase = (uint32_t)p.node_off[s];
+  const int32_t* __restrict__ ssp = p.span_start + p.span_off[s];
+  uint32_t* __restrict__ bpg = p.bp + p.bp_off[s];
+  const bool bp_in_lds = n < V_BP_LDS;
+  const int bstride = p.bp_stride;
+  const uint32_t slots = p.slots, seed = p.seed;
+  const int has_tri = p.has_tri;
+  VEntry (&R)[RING] = ring[grp];
+  Counts cnt;
+
+  if (gl == 0) {                                   // beam[0] = [BOS] (beam.py:21-23)
+    const Cand b0 = load_cand(B, nbase);
+    VEntry e0;
+    e0.score = 0.0; e0.f6 = b0.f6;
+    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
+    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+    R[0] = e0;
+  }
+  __builtin_amdgcn_wave_barrier();
+
+  // A_e = first node of end position e = ssp[(e-1)*8]; A_{n+1} = node count
+  int A0 = ssp[0];
+  int A1 = ssp[n >= 1 ? 8 : 0];
+  Cand cur = load_cand(B, (n >= 1 && gl < A1 - A0) ? nbase + (uint32_t)(A0 + gl) : INV);
+  int em9 = 0;
+  for (int e = 1; e <= n; ++e) {
+    // everything still outstanding was issued a full position ago (prefetch,
+    // backpointer store): settle it here, before this position issues loads,
+    // so the compiler's own waits below only count this position's loads.
+    __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
+    em9 = em9 == RING - 1 ? 0 : em9 + 1;
+    const int dmax = min(e, p.max_len);
+    const int X = A1 - A0;
+
+    double best_s = -INFINITY;
+    uint32_t best_g = INV;
+
+    // candidate gl: hypothesis from the LDS ring, probes issued
+    const bool act = gl < X;
+    const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
+    int bm0 = em9 - d0;
+    bm0 += bm0 < 0 ? RING : 0;
+    const Hyp h0 = read_hyp(R[act ? bm0 : 0]);
+    const bool skip0 = !act || ((h0.jmask & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));
+
+    // next position: span start and candidate fields (software prefetch; a
+    // node past the batch end reads as zeros).  Issued ahead of the probes:
+    // both round trips overlap.
+    int A2 = ssp[min(e + 1, n) * 8];
+    Cand nxt = load_cand(B, e < n ? nbase + (uint32_t)(A1 + gl) : INV);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // probes of candidate gl (unneeded ones read nothing)
+    Probe<NARROW> P;
+    probe_issue<NARROW>(P, B, slots, seed, h0, cur,
+                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u);
+    if (!skip0) {
+      const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h0, cur, cnt) : 0.0;
+      if (COUNT) ++cnt.exp;
+      best_s = h0.score + increment(p, cur, tri, nbase + (uint32_t)(A0 + gl));  // beam.py:115
+      best_g = (uint32_t)gl;
+    }
+    // more than 16 candidates ending at e (rare): serial extra rounds
+    for (int g = gl + V_G; g < X; g += V_G) {
+      const Cand c = load_cand(B, nbase + (uint32_t)(A0 + g));
+      const int d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
+      int bm = em9 - d;
+      bm += bm < 0 ? RING : 0;
+      const Hyp h = read_hyp(R[bm]);
+      if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;   // beam.py:43-45
+      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt) : 0.0;
+      if (COUNT) ++cnt.exp;
+      const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)(A0 + g));
+      if (better(sc, (uint32_t)g, best_s, best_g)) { best_s = sc; best_g = (uint32_t)g; }
+    }
+
+    double ws = best_s;
+    uint32_t wg = best_g;
+    row16_argmax(ws, wg);
+    __builtin_amdgcn_wave_barrier();
+    if (wg != INV && best_g == wg) {                 // the winner writes beam[e] (beam.py:112-116)
+      Cand c = cur;
+      Hyp h = h0;
+      int d = d0;
+      if (wg != (uint32_t)gl) {                      // won in an extra round: reload
+        c = load_cand(B, nbase + (uint32_t)(A0 + (int)wg));
+        d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
+        int bm = em9 - d;
+        bm += bm < 0 ? RING : 0;
+        h = read_hyp(R[bm]);
+      }
+      VEntry ne;
+      ne.score = ws; ne.f6 = c.f6;
+      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
+      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
+      ne.depth = h.depth + 1;
+      R[em9] = ne;
+      const uint32_t bpv = bp_pack((uint32_t)(A0 + (int)wg), (uint32_t)d, 0u);
+      if (bp_in_lds) bpl[grp][e] = bpv;
+      else bpg[(int64_t)e * bstride] = bpv;
+    }
+    __builtin_amdgcn_wave_barrier();
+    pin(nxt);
+    pin(A2);
+    cur = nxt;
+    A0 = A1;
+    A1 = A2;
+  }
+
+  // matures = beam[n] + EOS (beam.py:59-61); backtrace
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  if (gl == 0) {
+    const VEntry& f = R[n % RING];
+    p.out_count[s] = 1;
+    p.out_score[s] = f.score + 0.0;
+    p.out_len[s] = (int32_t)f.depth;
+    int32_t* codes = p.out_codes + p.cum_n[s];
+    int pos = n;
+    for (int step = (int)f.depth - 1; step >= 0; --step) {
+      const uint32_t v = bp_in_lds ? bpl[grp][pos] : bpg[(int64_t)pos * bstride];
+      codes[step] = (int32_t)bp_node(v);
+      pos -= (int)bp_d(v);
+    }
+  }
+  if (COUNT) {
+    const unsigned long long ex = group_sum<V_G>(cnt.exp), tu = group_sum<V_G>(cnt.tup),
+                             pb = group_sum<V_G>(cnt.probe);
+    if (gl == 0) {
+      atomicAdd(p.counters + 0, ex);
+      atomicAdd(p.counters + 1, tu);
+      atomicAdd(p.counters + 2, pb);
+    }
+  }
+}
+
+// ===========================================================================
+// beam_size 2..32
+// ===========================================================================
+struct alignas(16) Entry {
+  double score, f6;
+  uint32_t jword, jmorph, jtag, jmask;
+  uint32_t iword, imorph, imask, depth;
+};
+
+template <int KT, int G, bool NARROW, bool COUNT>
+__global__ void __launch_bounds__(256)
+lt_beam_k(DecodeParams p) {
   constexpr int SPB = 256 / G;               // sentences per block
   static_assert(KT <= G, "beam width must not exceed the lane group");
   __shared__ Entry ring[SPB][RING][KT];
-  __shared__ int32_t cnt[SPB][RING];
+  __shared__ int32_t cntl[SPB][RING];
 
   const int grp = threadIdx.x / G;
   const int gl = threadIdx.x % G;
   const int slot = blockIdx.x * SPB + grp;
   if (slot >= p.n_sent) return;
+  const Bufs B = make_bufs(p);
   const int s = p.order[slot];
   const int n = p.sent_n[s];
-  const int64_t nbase = p.node_off[s];
+  const uint32_t nbase = (uint32_t)p.node_off[s];
   const int32_t* __restrict__ ssp = p.span_start + p.span_off[s];
   uint32_t* __restrict__ bp = p.bp + p.bp_off[s];
   const int k = p.k;
   const int bstride = p.bp_stride;
-  const Slot* __restrict__ tab = p.table;
-  const uint32_t tmask = p.tmask;
+  const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
-
   Entry (&R)[RING][KT] = ring[grp];
-  unsigned long long n_exp = 0, n_tup = 0, n_probe = 0;
+  Counts cnt;
 
   if (gl == 0) {                             // beam[0] = [BOS] (beam.py:21-23)
+    const Cand b0 = load_cand(B, nbase);
     Entry e0;
-    e0.score = 0.0;
-    e0.f6 = p.nf6[nbase];
-    e0.node = 0;
-    e0.jword = p.nword[nbase];
-    e0.jmorph = p.nmorph[nbase];
-    e0.jtag = p.ntag[nbase];
-    e0.jmask = p.nmask[nbase];
-    e0.iword = 0; e0.imorph = 0; e0.imask = 0;
-    e0.depth = 0;
-    e0.pad[0] = e0.pad[1] = e0.pad[2] = 0;
+    e0.score = 0.0; e0.f6 = b0.f6;
+    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
+    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
     R[0][0] = e0;
-    cnt[grp][0] = 1;
+    cntl[grp][0] = 1;
   }
   __builtin_amdgcn_wave_barrier();
 
@@ -181,7 +566,7 @@ lt_decode_k(DecodeParams p) {
 #pragma unroll
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
-      const int c = (d <= dmax) ? cnt[grp][(e - d) % RING] : 0;
+      const int c = (d <= dmax) ? cntl[grp][(e - d) % RING] : 0;
       pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
     }
     const int X = pre[MAX_SPAN];
@@ -201,84 +586,18 @@ lt_decode_k(DecodeParams p) {
       const int r = local / m;
       const int i = local - r * m;
       const int d = MAX_SPAN - j;
-      const Entry& h = R[(e - d) % RING][r];
-      const int64_t gn = nbase + ss[j] + i;
-      const uint32_t km = p.nmask[gn];
-      const uint32_t jm = h.jmask;
+      const Entry& he = R[(e - d) % RING][r];
+      const uint32_t gn = nbase + (uint32_t)(ss[j] + i);
+      const Cand c = load_cand(B, gn);
+      Hyp h;
+      h.score = he.score; h.f6 = he.f6;
+      h.jword = he.jword; h.jmorph = he.jmorph; h.jtag = he.jtag; h.jmask = he.jmask;
+      h.iword = he.iword; h.imorph = he.imorph; h.imask = he.imask; h.depth = he.depth;
       // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
-      if ((jm & F_UNK) && (km & F_UNK) && (d < dmax)) continue;
-
-      double tri = 0.0;
-      if (has_tri) {
-        const uint32_t kw = (uint32_t)p.nword[gn], kmo = (uint32_t)p.nmorph[gn],
-                       kt = (uint32_t)p.ntag[gn];
-        const uint32_t jw = (uint32_t)h.jword, jmo = (uint32_t)h.jmorph, jt = (uint32_t)h.jtag;
-        const uint32_t im = h.imask;
-        const bool has_i = (im & F_WI) != 0;
-        // keys of the probed classes, in feature order 0,1,2,3,7,8
-        uint32_t ka[6], kb[6], kc[6], kcls[6];
-        bool need[6];
-        ka[0] = jw;  kb[0] = kw; kc[0] = kt; kcls[0] = 1;
-        need[0] = (jm & J0A) && (km & K0B) && (km & K0C);
-        ka[1] = jw;  kb[1] = kt; kc[1] = 0;  kcls[1] = 2;
-        need[1] = (jm & J1A) && (km & K1B);
-        ka[2] = jt;  kb[2] = kw; kc[2] = kt; kcls[2] = 3;
-        need[2] = (jm & J2A) && (km & K2B) && (km & K2C);
-        ka[3] = jt;  kb[3] = kt; kc[3] = 0;  kcls[3] = 4;
-        need[3] = (jm & J3A) && (km & K3B);
-        ka[4] = (uint32_t)h.iword; kb[4] = jw; kc[4] = kw; kcls[4] = 8;
-        need[4] = has_i && (im & I7A) && (jm & J7B) && (km & K7C);
-        // class 8: (wj.morph0 | wi.morph0, wk.morph0) (feature.py:113-119)
-        bool emit8 = false;
-        kb[5] = kmo; kc[5] = 0; kcls[5] = 9; ka[5] = 0; need[5] = false;
-        if (km & F_CTX) {
-          if (jm & F_CTX) {
-            emit8 = true; ka[5] = jmo; need[5] = (jm & J8A) && (km & K8B);
-          } else if (has_i && (im & F_CTX)) {
-            emit8 = true; ka[5] = (uint32_t)h.imorph; need[5] = (im & I8A) && (km & K8B);
-          }
-        }
-        uint32_t hh[6];
-        Slot first[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          hh[q] = key_hash(ka[q], kb[q], kc[q], kcls[q] - 1u) & tmask;
-          first[q].a = first[q].b = first[q].c = first[q].cls1 = 0u;
-          first[q].coef = 0.0;
-          if (need[q]) first[q] = load_slot(tab, hh[q]);
-        }
-        double v[9];
-        bool pr[9];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          double cf = 0.0;
-          pr[q] = need[q] && resolve(tab, tmask, hh[q], first[q], ka[q], kb[q], kc[q], kcls[q], cf);
-          v[q] = cf;
-        }
-        pr[4] = (km & F_HAS4) != 0; v[4] = p.nf4[gn];
-        pr[5] = (km & F_HAS5) != 0; v[5] = p.nf5[gn];
-        pr[6] = (jm & F_HAS6) != 0; v[6] = h.f6;
-        {
-          double cf = 0.0;
-          pr[7] = need[4] && resolve(tab, tmask, hh[4], first[4], ka[4], kb[4], kc[4], kcls[4], cf);
-          v[7] = cf;
-          cf = 0.0;
-          pr[8] = need[5] && resolve(tab, tmask, hh[5], first[5], ka[5], kb[5], kc[5], kcls[5], cf);
-          v[8] = cf;
-        }
-        tri = numpy_sum9(v, pr);
-        if (COUNT) {
-          n_tup += 6 + ((jm & F_UNK) ? 1 : 0) + (has_i ? 1 : 0) + (emit8 ? 1 : 0);
-#pragma unroll
-          for (int q = 0; q < 6; ++q) n_probe += need[q] ? 1 : 0;
-        }
-      }
-      // inc = ((0 + pre...) + tri) + post...   (score_funcs.py:50-54)
-      double inc = p.npre[gn] + tri;
-      for (int t = 0; t < p.n_post; ++t) inc += p.npost[(int64_t)t * p.n_nodes + gn];
-      const double sc = h.score + inc;       // Sequence.add (beam.py:115)
-      if (COUNT) ++n_exp;
-
+      if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;
+      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt) : 0.0;
+      const double sc = h.score + increment(p, c, tri, gn);     // beam.py:115
+      if (COUNT) ++cnt.exp;
       // insert (sc, g) into the lane-local sorted list; g grows per lane, so
       // an equal score lands after the earlier expansion (stable).
       if (better(sc, (uint32_t)g, ls[KT - 1], lg[KT - 1])) {
@@ -286,8 +605,8 @@ lt_decode_k(DecodeParams p) {
 #pragma unroll
         for (int q = KT - 1; q > 0; --q) {
           if (better(ls[q], lg[q], ls[q - 1], lg[q - 1])) {
-            double ts = ls[q]; ls[q] = ls[q - 1]; ls[q - 1] = ts;
-            uint32_t tg = lg[q]; lg[q] = lg[q - 1]; lg[q - 1] = tg;
+            const double ts = ls[q]; ls[q] = ls[q - 1]; ls[q - 1] = ts;
+            const uint32_t tg = lg[q]; lg[q] = lg[q - 1]; lg[q - 1] = tg;
           }
         }
       }
@@ -327,19 +646,11 @@ lt_decode_k(DecodeParams p) {
       const int d = MAX_SPAN - j;
       const Entry& h = R[(e - d) % RING][r];
       const int node = ss[j] + i;
-      const int64_t gn = nbase + node;
-      ne.score = sel_s;
-      ne.f6 = p.nf6[gn];
-      ne.node = node;
-      ne.jword = p.nword[gn];
-      ne.jmorph = p.nmorph[gn];
-      ne.jtag = p.ntag[gn];
-      ne.jmask = p.nmask[gn];
-      ne.iword = h.jword;
-      ne.imorph = h.jmorph;
-      ne.imask = h.jmask | F_WI;
+      const Cand c = load_cand(B, nbase + (uint32_t)node);
+      ne.score = sel_s; ne.f6 = c.f6;
+      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
+      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
       ne.depth = h.depth + 1;
-      ne.pad[0] = ne.pad[1] = ne.pad[2] = 0;
       bpv = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
     }
     __builtin_amdgcn_wave_barrier();
@@ -347,13 +658,13 @@ lt_decode_k(DecodeParams p) {
       R[e % RING][gl] = ne;
       bp[(int64_t)e * bstride + gl] = bpv;
     }
-    if (gl == 0) cnt[grp][e % RING] = nsel;
+    if (gl == 0) cntl[grp][e % RING] = nsel;
     __builtin_amdgcn_wave_barrier();
   }
 
   // matures = beam[n] + EOS (beam.py:59-61); backtrace per mature rank
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const int nm = cnt[grp][n % RING];
+  const int nm = cntl[grp][n % RING];
   if (gl == 0) p.out_count[s] = nm;
   if (gl >= nm && gl < k) {                  // unused mature slots read as empty
     p.out_score[(int64_t)s * k + gl] = 0.0;
@@ -363,10 +674,10 @@ lt_decode_k(DecodeParams p) {
     const Entry& f = R[n % RING][gl];
     const int64_t o = (int64_t)s * k + gl;
     p.out_score[o] = f.score + 0.0;
-    p.out_len[o] = f.depth;
+    p.out_len[o] = (int32_t)f.depth;
     int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)gl * n;
     int pos = n, rank = gl;
-    for (int step = f.depth - 1; step >= 0; --step) {
+    for (int step = (int)f.depth - 1; step >= 0; --step) {
       const uint32_t v = bp[(int64_t)pos * bstride + rank];
       codes[step] = (int32_t)bp_node(v);
       pos -= (int)bp_d(v);
@@ -374,35 +685,42 @@ lt_decode_k(DecodeParams p) {
     }
   }
   if (COUNT) {
-    n_exp = group_sum<G>(n_exp);
-    n_tup = group_sum<G>(n_tup);
-    n_probe = group_sum<G>(n_probe);
+    const unsigned long long ex = group_sum<G>(cnt.exp), tu = group_sum<G>(cnt.tup),
+                             pb = group_sum<G>(cnt.probe);
     if (gl == 0) {
-      atomicAdd(p.counters + 0, n_exp);
-      atomicAdd(p.counters + 1, n_tup);
-      atomicAdd(p.counters + 2, n_probe);
+      atomicAdd(p.counters + 0, ex);
+      atomicAdd(p.counters + 1, tu);
+      atomicAdd(p.counters + 2, pb);
     }
   }
 }
 
-template <int KT, int G, bool COUNT>
-hipError_t launch_t(const DecodeParams& p, hipStream_t st) {
-  constexpr int SPB = 256 / G;
-  const int blocks = (p.n_sent + SPB - 1) / SPB;
+template <bool NARROW, bool COUNT>
+hipError_t launch_v(const DecodeParams& p, hipStream_t st) {
+  const int blocks = (p.n_sent + V_SPB - 1) / V_SPB;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_decode_k<KT, G, COUNT>), dim3(blocks), dim3(256), 0, st, p);
+  hipLaunchKernelGGL((lt_viterbi_k<NARROW, COUNT>), dim3(blocks), dim3(256), 0, st, p);
   return hipGetLastError();
 }
 
-template <bool COUNT>
+template <int KT, int G, bool NARROW, bool COUNT>
+hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
+  constexpr int SPB = 256 / G;
+  const int blocks = (p.n_sent + SPB - 1) / SPB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((lt_beam_k<KT, G, NARROW, COUNT>), dim3(blocks), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
   switch (kt) {
-    case 1: return launch_t<1, 16, COUNT>(p, st);
-    case 2: return launch_t<2, 32, COUNT>(p, st);
-    case 4: return launch_t<4, 32, COUNT>(p, st);
-    case 8: return launch_t<8, 64, COUNT>(p, st);
-    case 16: return launch_t<16, 64, COUNT>(p, st);
-    case 32: return launch_t<32, 64, COUNT>(p, st);
+    case 1: return launch_v<NARROW, COUNT>(p, st);
+    case 2: return launch_b<2, 32, NARROW, COUNT>(p, st);
+    case 4: return launch_b<4, 32, NARROW, COUNT>(p, st);
+    case 8: return launch_b<8, 64, NARROW, COUNT>(p, st);
+    case 16: return launch_b<16, 64, NARROW, COUNT>(p, st);
+    case 32: return launch_b<32, 64, NARROW, COUNT>(p, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -423,7 +741,9 @@ int beam_template_for(int k) {
 
 hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count) {
   const int kt = beam_template_for(p.k);
-  return count ? launch_k<true>(p, kt, st) : launch_k<false>(p, kt, st);
+  if (p.narrow)
+    return count ? launch_k<true, true>(p, kt, st) : launch_k<true, false>(p, kt, st);
+  return count ? launch_k<false, true>(p, kt, st) : launch_k<false, false>(p, kt, st);
 }
 
 }  // namespace lt

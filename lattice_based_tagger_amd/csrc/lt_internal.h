@@ -8,8 +8,10 @@ namespace lt {
 
 struct DecodeParams {
   // model
-  const Slot* table;
-  uint32_t tmask;
+  const void* table;            // SlotN[] or SlotW[] (cuckoo, two choices)
+  uint32_t slots;
+  uint32_t seed;
+  int32_t narrow;               // 1: SlotN, 0: SlotW
   int32_t has_tri;
   // batch (device pointers)
   int32_t n_sent;
@@ -23,14 +25,7 @@ struct DecodeParams {
   const int64_t* node_off;
   const int64_t* span_off;
   const int32_t* span_start;
-  const int32_t* nword;
-  const int32_t* nmorph;
-  const int32_t* ntag;
-  const uint32_t* nmask;
-  const double* npre;
-  const double* nf4;
-  const double* nf5;
-  const double* nf6;
+  const NodeRec* nodes;         // AoS node records; mask + span length bits (D_SHIFT)
   const double* npost;
   // scratch + results
   uint32_t* bp;

@@ -41,7 +41,7 @@ def test_kernels_are_gfx950_code_objects():
     lib = _build.build(verbose=False)
     blob = open(lib, 'rb').read()
     assert b'amdgcn-amd-amdhsa--gfx950' in blob
-    assert b'lt_decode_k' in blob
+    assert b'lt_viterbi_k' in blob and b'lt_beam_k' in blob
 
 
 def test_context_without_gpu_fails_loudly():
