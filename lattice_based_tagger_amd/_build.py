@@ -42,8 +42,6 @@ def build(force=False, verbose=True):
     for src in SOURCES:
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + '.o')
         cmd = [HIPCC, '--offload-arch=' + ARCH] + COMMON_FLAGS + ['-c', os.path.join(CSRC, src), '-o', obj]
-        if src.endswith('.cpp'):
-            cmd = [HIPCC] + COMMON_FLAGS + ['-D__HIP_PLATFORM_AMD__', '-c', os.path.join(CSRC, src), '-o', obj]
         if verbose:
             print(' '.join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

@@ -80,6 +80,11 @@ struct KeyRec {
 // Cuckoo table build (two choices, one slot per bucket).  Returns false when
 // the random walk fails; the caller reseeds / grows and retries.
 template <class SlotT>
+KeyBase base_of(const KeyRec& k) {
+  return key_base<sizeof(SlotT) == sizeof(SlotN)>(k.a, k.b, k.c, k.cls);
+}
+
+template <class SlotT>
 bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed,
                   std::vector<SlotT>& tab, int64_t* dup) {
   tab.assign(slots, SlotT{});
@@ -91,7 +96,7 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
     uint32_t i1, i2;
     {
       const KeyRec& k = keys[(size_t)i];
-      cuckoo_slots(key_base(k.a, k.b, k.c, k.cls), seed, slots, i1, i2);
+      cuckoo_slots(base_of<SlotT>(k), seed, slots, i1, i2);
       for (uint32_t x : {i1, i2}) {
         const int32_t w = who[x];
         if (w >= 0 && keys[(size_t)w].a == k.a && keys[(size_t)w].b == k.b &&
@@ -105,7 +110,7 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
     bool placed = false;
     for (int kick = 0; kick < max_kicks; ++kick) {
       const KeyRec& k = keys[(size_t)cur];
-      cuckoo_slots(key_base(k.a, k.b, k.c, k.cls), seed, slots, i1, i2);
+      cuckoo_slots(base_of<SlotT>(k), seed, slots, i1, i2);
       uint32_t target;
       if (who[i1] < 0) target = i1;
       else if (who[i2] < 0) target = i2;

@@ -56,26 +56,49 @@ LT_HD uint64_t narrow_key(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
   return ((uint64_t)cls << 60) | ((uint64_t)a << 40) | ((uint64_t)b << 20) | (uint64_t)c;
 }
 
-// Cuckoo hashing: every key lives in one of its two candidate slots
-// i1 = mulhi(h1, slots), i2 = mulhi(h2, slots), so a lookup is exactly two
-// independent loads (no probe chains).  Identical on host and device.
-LT_HD uint32_t key_base(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
-  return (a * 0x9E3779B1u) ^ (b * 0x85EBCA77u) ^ (c * 0xC2B2AE3Du) ^ (cls * 0x27D4EB2Fu);
+// Cuckoo hashing: every key lives in one of its two candidate slots, so a
+// lookup is exactly two independent loads (no probe chains).  Identical on
+// host and device.
+//
+// Two independent key mixes (base1, base2), each avalanched with its own
+// seed, give the two candidate slots; a key set can only defeat the build by
+// a triple collision of the full 64-bit (base1, base2) pair.  Narrow tables
+// (ids < 2^20) mix with full-rate 24-bit multiplies (v_mul_u32_u24); wide
+// tables with 32-bit multiplies.
+LT_HD uint32_t mul24(uint32_t x, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(x, k);                         // v_mul_u32_u24: full rate
+#else
+  return (x & 0xFFFFFFu) * (k & 0xFFFFFFu);
+#endif
 }
-LT_HD uint32_t fmix32(uint32_t h) {
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return h;
+struct KeyBase {
+  uint32_t b1, b2;
+};
+template <bool NARROW>
+LT_HD KeyBase key_base(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+  KeyBase k;
+  if (NARROW) {
+    k.b1 = mul24(a, 0x9E3779u) ^ mul24(b, 0x85EBCBu) ^ mul24(c, 0xC2B2AFu) ^ (cls * 0x27D4EB2Fu);
+    k.b2 = mul24(a, 0x7FEB35u) ^ mul24(b, 0x846CA7u) ^ mul24(c, 0xD35A2Du) ^ (cls * 0x165667B1u);
+  } else {
+    k.b1 = (a * 0x9E3779B1u) ^ (b * 0x85EBCA77u) ^ (c * 0xC2B2AE3Du) ^ (cls * 0x27D4EB2Fu);
+    k.b2 = (a * 0x7FEB352Du) ^ (b * 0x846CA68Bu) ^ (c * 0xD35A2D97u) ^ (cls * 0x165667B1u);
+  }
+  return k;
 }
 LT_HD uint32_t slot_of(uint32_t h, uint32_t slots) {
   return (uint32_t)(((uint64_t)h * slots) >> 32);
 }
-LT_HD void cuckoo_slots(uint32_t base, uint32_t seed, uint32_t slots, uint32_t& i1, uint32_t& i2) {
-  i1 = slot_of(fmix32(base ^ seed), slots);
-  i2 = slot_of(fmix32(base ^ seed ^ 0x5BD1E995u), slots);
+LT_HD uint32_t mix1(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  return h;
+}
+LT_HD void cuckoo_slots(KeyBase kb, uint32_t seed, uint32_t slots, uint32_t& i1, uint32_t& i2) {
+  i1 = slot_of(mix1(kb.b1 ^ seed), slots);
+  i2 = slot_of(mix1(kb.b2 ^ (seed * 0x9E3779B1u + 0x632BE5ABu)), slots);
 }
 
 // Device node record (AoS, 48 B = 3 x 16 B loads), built by the library from

@@ -86,6 +86,27 @@ __device__ __forceinline__ Cand load_cand(const Bufs& B, uint32_t gn) {
   return c;
 }
 
+// Buffer -> LDS DMA of one node record per lane (three 16 B planes; lane l's
+// bytes land at plane + 16*l).  `planes` points at this wave's 3 x 64 x 16 B
+// region; no VGPR holds the data.
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void dma_cand(const Bufs& B, uint32_t gn, uint4* planes) {
+  const uint32_t o = gn == INV ? OOB : gn * (uint32_t)sizeof(NodeRec);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(planes), 16, o, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(planes + 64), 16,
+                                           o == OOB ? OOB : o + 16u, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(planes + 128), 16,
+                                           o == OOB ? OOB : o + 32u, 0, 0, 0);
+}
+__device__ __forceinline__ Cand read_staged(const uint4* planes, int lane) {
+  const uint4 a = planes[lane], b = planes[64 + lane], c4 = planes[128 + lane];
+  Cand c;
+  c.word = a.x; c.morph = a.y; c.tag = a.z; c.mask = a.w;
+  c.pre = dbl(b.x, b.y); c.f4 = dbl(b.z, b.w);
+  c.f5 = dbl(c4.x, c4.y); c.f6 = dbl(c4.z, c4.w);
+  return c;
+}
+
 // Pin prefetched values in registers: the empty asm makes them opaque, so the
 // compiler cannot re-issue ("rematerialise") the loads at their later use.
 __device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)); }
@@ -184,6 +205,11 @@ template <>
 struct Tab<true> {
   static constexpr uint32_t SZ = sizeof(SlotN);
   struct S { uint64_t key; double coef; };
+  typedef uint64_t Key;
+  __device__ static Key key(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+    return narrow_key(a, b, c, cls);
+  }
+  __device__ static bool hit(const S& s, Key k) { return s.key == k; }
   __device__ static S load(rsrc_t t, uint32_t off) {
     const u32x4 v = ld128(t, off);
     S s;
@@ -202,6 +228,13 @@ template <>
 struct Tab<false> {
   static constexpr uint32_t SZ = sizeof(SlotW);
   struct S { uint32_t a, b, c, cls1; double coef; };
+  struct Key { uint32_t a, b, c, cls1; };
+  __device__ static Key key(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+    return Key{a, b, c, cls + 1};
+  }
+  __device__ static bool hit(const S& s, Key k) {
+    return s.cls1 == k.cls1 && s.a == k.a && s.b == k.b && s.c == k.c;
+  }
   __device__ static S load(rsrc_t t, uint32_t off) {
     const u32x4 k = ld128(t, off);
     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(t, off == OOB ? OOB : off + 16u, 0, 0);
@@ -228,6 +261,7 @@ struct Counts {
 template <bool NARROW>
 struct Probe {
   typename Tab<NARROW>::S s1[6], s2[6];   // the two cuckoo candidates
+  typename Tab<NARROW>::Key key[6];       // expected key of probe q
   uint32_t need;                           // bit q: probe q is needed
 };
 
@@ -283,7 +317,8 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uin
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     uint32_t i1, i2;
-    cuckoo_slots(key_base(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
+    cuckoo_slots(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
+    P.key[q] = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
     const bool nq = (need >> q) & 1u;
     P.s1[q] = T::load(B.tab, nq ? i1 * T::SZ : OOB);
     P.s2[q] = T::load(B.tab, nq ? i2 * T::SZ : OOB);
@@ -295,14 +330,12 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
                                                const Cand& c, Counts& cnt) {
   using T = Tab<NARROW>;
   const uint32_t jm = h.jmask, km = c.mask, im = h.imask;
-  const bool use_j8 = use_j8_of(h, c);
-  const Keys K = make_keys(h, c, use_j8);
   bool pr6[6];
   double cf[6];
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
-    const bool m1 = T::test(P.s1[q], K.a[q], K.b[q], K.c[q], PCLS[q]) == 1;
-    const bool m2 = T::test(P.s2[q], K.a[q], K.b[q], K.c[q], PCLS[q]) == 1;
+    const bool m1 = T::hit(P.s1[q], P.key[q]);
+    const bool m2 = T::hit(P.s2[q], P.key[q]);
     pr6[q] = ((P.need >> q) & 1u) && (m1 || m2);
     cf[q] = m1 ? P.s1[q].coef : P.s2[q].coef;
   }
@@ -316,6 +349,7 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
   v[7] = cf[4]; pr[7] = pr6[4];
   v[8] = cf[5]; pr[8] = pr6[5];
   if (COUNT) {
+    const bool use_j8 = use_j8_of(h, c);
     const bool has_i = (im & F_WI) != 0;
     const bool use_i8 = (km & F_CTX) && !(jm & F_CTX) && has_i && (im & F_CTX);
     cnt.tup += 6 + ((jm & F_UNK) ? 1 : 0) + (has_i ? 1 : 0) + ((use_j8 || use_i8) ? 1 : 0);
@@ -366,6 +400,7 @@ __global__ void __launch_bounds__(256)
 lt_viterbi_k(DecodeParams p) {
   __shared__ VEntry ring[V_SPB][RING];
   __shared__ uint32_t bpl[V_SPB][V_BP_LDS];
+  __shared__ uint4 stg[4][3 * 64];             // per wave: 3 planes x 64 lanes x 16 B
 
   const int grp = threadIdx.x / V_G;
   const int gl = threadIdx.x % V_G;
@@ -397,7 +432,10 @@ lt_viterbi_k(DecodeParams p) {
   // A_e = first node of end position e = ssp[(e-1)*8]; A_{n+1} = node count
   int A0 = ssp[0];
   int A1 = ssp[n >= 1 ? 8 : 0];
-  Cand cur = load_cand(B, (n >= 1 && gl < A1 - A0) ? nbase + (uint32_t)(A0 + gl) : INV);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint4* const wst = stg[wv];
+  const int lane = (int)(threadIdx.x & 63);
+  dma_cand(B, (n >= 1 && gl < A1 - A0) ? nbase + (uint32_t)(A0 + gl) : INV, wst);
   int em9 = 0;
   for (int e = 1; e <= n; ++e) {
     // everything still outstanding was issued a full position ago (prefetch,
@@ -407,6 +445,7 @@ lt_viterbi_k(DecodeParams p) {
     em9 = em9 == RING - 1 ? 0 : em9 + 1;
     const int dmax = min(e, p.max_len);
     const int X = A1 - A0;
+    const Cand cur = read_staged(wst, lane);   // this position's candidate (staged by DMA)
 
     double best_s = -INFINITY;
     uint32_t best_g = INV;
@@ -419,11 +458,12 @@ lt_viterbi_k(DecodeParams p) {
     const Hyp h0 = read_hyp(R[act ? bm0 : 0]);
     const bool skip0 = !act || ((h0.jmask & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));
 
-    // next position: span start and candidate fields (software prefetch; a
-    // node past the batch end reads as zeros).  Issued ahead of the probes:
-    // both round trips overlap.
+    // next position: span start and candidate record (software prefetch; the
+    // record goes straight to LDS by DMA once `cur` has been read out of it; a
+    // node past the batch end reads as zeros).  Issued ahead of the probes.
     int A2 = ssp[min(e + 1, n) * 8];
-    Cand nxt = load_cand(B, e < n ? nbase + (uint32_t)(A1 + gl) : INV);
+    __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): cur is out of the staging area
+    dma_cand(B, e < n ? nbase + (uint32_t)(A1 + gl) : INV, wst);
     __builtin_amdgcn_sched_barrier(0);
 
     // probes of candidate gl (unneeded ones read nothing)
@@ -476,9 +516,7 @@ lt_viterbi_k(DecodeParams p) {
       else bpg[(int64_t)e * bstride] = bpv;
     }
     __builtin_amdgcn_wave_barrier();
-    pin(nxt);
     pin(A2);
-    cur = nxt;
     A0 = A1;
     A1 = A2;
   }
@@ -518,13 +556,87 @@ struct alignas(16) Entry {
   uint32_t iword, imorph, imask, depth;
 };
 
+__device__ __forceinline__ Hyp read_entry(const Entry& e) {
+  Hyp h;
+  h.score = e.score; h.f6 = e.f6;
+  h.jword = e.jword; h.jmorph = e.jmorph; h.jtag = e.jtag; h.jmask = e.jmask;
+  h.iword = e.iword; h.imorph = e.imorph; h.imask = e.imask; h.depth = e.depth;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ double rdlane(double v, int lane) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  return dbl(rdlane((uint32_t)b, lane), rdlane((uint32_t)(b >> 32), lane));
+}
+
+// Argmax over a G-lane group (G = 32 or 64): DPP within 16-lane rows, then the
+// row leaders are read with v_readlane (group-uniform control flow only).
+template <int G>
+__device__ __forceinline__ void group_argmax_fast(double& s, uint32_t& g) {
+  row16_argmax(s, g);
+  const double s0 = rdlane(s, 0), s1 = rdlane(s, 16), s2 = rdlane(s, 32), s3 = rdlane(s, 48);
+  const uint32_t g0 = rdlane(g, 0), g1 = rdlane(g, 16), g2 = rdlane(g, 32), g3 = rdlane(g, 48);
+  double a = s0, c = s2;
+  uint32_t ga = g0, gc = g2;
+  if (better(s1, g1, a, ga)) { a = s1; ga = g1; }
+  if (better(s3, g3, c, gc)) { c = s3; gc = g3; }
+  if (G == 64) {
+    if (better(c, gc, a, ga)) { a = c; ga = gc; }
+    s = a; g = ga;
+  } else {                                   // two groups per wave: rows {0,1}, {2,3}
+    const bool hi = (threadIdx.x & 63) >= 32;
+    s = hi ? c : a;
+    g = hi ? gc : ga;
+  }
+}
+
+// Insert (s, g) into a sorted (score desc, g asc) register list of capacity C.
+template <int C>
+__device__ __forceinline__ void list_insert(double (&ls)[C], uint32_t (&lg)[C], double s, uint32_t g) {
+  if (!better(s, g, ls[C - 1], lg[C - 1])) return;
+  ls[C - 1] = s; lg[C - 1] = g;
+#pragma unroll
+  for (int q = C - 1; q > 0; --q) {
+    if (better(ls[q], lg[q], ls[q - 1], lg[q - 1])) {
+      const double ts = ls[q]; ls[q] = ls[q - 1]; ls[q - 1] = ts;
+      const uint32_t tg = lg[q]; lg[q] = lg[q - 1]; lg[q - 1] = tg;
+    }
+  }
+}
+
+// Expansion index g of end position e -> (span slot j, hypothesis rank r,
+// candidate i) in the reference's generation order (beam.py:31-42).
+struct Exp {
+  int j, r, i, d;
+};
+__device__ __forceinline__ Exp decode_g(int g, const int (&pre)[MAX_SPAN + 1],
+                                        const int (&ss)[MAX_SPAN + 1]) {
+  Exp x;
+  int j = 0;
+#pragma unroll
+  for (int q = 1; q < MAX_SPAN; ++q) j = (g >= pre[q]) ? q : j;
+  const int m = ss[j + 1] - ss[j];
+  const int local = g - pre[j];
+  x.r = local / m;
+  x.i = local - x.r * m;
+  x.j = j;
+  x.d = MAX_SPAN - j;
+  return x;
+}
+
 template <int KT, int G, bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(256)
 lt_beam_k(DecodeParams p) {
   constexpr int SPB = 256 / G;               // sentences per block
+  constexpr int LCAP = 4;                    // expansions per lane per chunk
+  constexpr int STAGE = G;                   // candidate records staged in LDS
   static_assert(KT <= G, "beam width must not exceed the lane group");
   __shared__ Entry ring[SPB][RING][KT];
   __shared__ int32_t cntl[SPB][RING];
+  __shared__ NodeRec stage[SPB][STAGE];
 
   const int grp = threadIdx.x / G;
   const int gl = threadIdx.x % G;
@@ -541,6 +653,7 @@ lt_beam_k(DecodeParams p) {
   const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
   Entry (&R)[RING][KT] = ring[grp];
+  NodeRec* __restrict__ st = stage[grp];
   Counts cnt;
 
   if (gl == 0) {                             // beam[0] = [BOS] (beam.py:21-23)
@@ -552,15 +665,23 @@ lt_beam_k(DecodeParams p) {
     R[0][0] = e0;
     cntl[grp][0] = 1;
   }
+  // span starts and staged candidate records of end position 1
+  int ss[MAX_SPAN + 1];
+#pragma unroll
+  for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = n >= 1 ? ssp[j] : 0;
+  {
+    const Cand c0 = load_cand(B, (n >= 1 && gl < ss[MAX_SPAN] - ss[0]) ? nbase + (uint32_t)(ss[0] + gl) : INV);
+    NodeRec r0;
+    r0.word = c0.word; r0.morph = c0.morph; r0.tag = c0.tag; r0.mask = c0.mask;
+    r0.pre = c0.pre; r0.f4 = c0.f4; r0.f5 = c0.f5; r0.f6 = c0.f6;
+    st[gl] = r0;
+  }
   __builtin_amdgcn_wave_barrier();
 
   for (int e = 1; e <= n; ++e) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): last position's prefetch
     const int dmax = min(e, p.max_len);
-    const int32_t* sse = ssp + (e - 1) * MAX_SPAN;
-    int ss[MAX_SPAN + 1];
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = sse[j];
-    // expansions per span slot j (d = 8 - j, begin b = e - d ascending)
+    const int A0 = ss[0];
     int pre[MAX_SPAN + 1];
     pre[0] = 0;
 #pragma unroll
@@ -571,63 +692,65 @@ lt_beam_k(DecodeParams p) {
     }
     const int X = pre[MAX_SPAN];
 
-    // lane-local top-k of this lane's expansions
-    double ls[KT];
-    uint32_t lg[KT];
+    // prefetch of end position e+1: span starts and candidate records
+    int ssn[MAX_SPAN + 1];
+    const int en = min(e + 1, n);
 #pragma unroll
-    for (int q = 0; q < KT; ++q) { ls[q] = -INFINITY; lg[q] = INV; }
+    for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = ssp[(en - 1) * MAX_SPAN + j];
+    Cand nxt = load_cand(B, e < n ? nbase + (uint32_t)(ss[MAX_SPAN] + gl) : INV);
+    __builtin_amdgcn_sched_barrier(0);
 
-    for (int g = gl; g < X; g += G) {
-      int j = 0;
-#pragma unroll
-      for (int q = 1; q < MAX_SPAN; ++q) j = (g >= pre[q]) ? q : j;
-      const int m = ss[j + 1] - ss[j];
-      const int local = g - pre[j];
-      const int r = local / m;
-      const int i = local - r * m;
-      const int d = MAX_SPAN - j;
-      const Entry& he = R[(e - d) % RING][r];
-      const uint32_t gn = nbase + (uint32_t)(ss[j] + i);
-      const Cand c = load_cand(B, gn);
-      Hyp h;
-      h.score = he.score; h.f6 = he.f6;
-      h.jword = he.jword; h.jmorph = he.jmorph; h.jtag = he.jtag; h.jmask = he.jmask;
-      h.iword = he.iword; h.imorph = he.imorph; h.imask = he.imask; h.depth = he.depth;
-      // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
-      if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;
-      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt) : 0.0;
-      const double sc = h.score + increment(p, c, tri, gn);     // beam.py:115
-      if (COUNT) ++cnt.exp;
-      // insert (sc, g) into the lane-local sorted list; g grows per lane, so
-      // an equal score lands after the earlier expansion (stable).
-      if (better(sc, (uint32_t)g, ls[KT - 1], lg[KT - 1])) {
-        ls[KT - 1] = sc; lg[KT - 1] = (uint32_t)g;
-#pragma unroll
-        for (int q = KT - 1; q > 0; --q) {
-          if (better(ls[q], lg[q], ls[q - 1], lg[q - 1])) {
-            const double ts = ls[q]; ls[q] = ls[q - 1]; ls[q - 1] = ts;
-            const uint32_t tg = lg[q]; lg[q] = lg[q - 1]; lg[q - 1] = tg;
-          }
-        }
-      }
-    }
-
-    // merge: k rounds of group argmax over the lanes' list heads (beam.py:85)
-    double sel_s = 0.0;
-    uint32_t sel_g = INV;
+    // chunks of G*LCAP expansions merged into the running top-k (lanes < k)
+    double rs = -INFINITY;
+    uint32_t rg = INV;
     int nsel = 0;
-    for (int t = 0; t < k; ++t) {
-      double bs = ls[0];
-      uint32_t bg = lg[0];
-      group_argmax<G>(bs, bg);
-      if (bg == INV) break;
-      if (lg[0] == bg) {
+    for (int base = 0; base < X; base += G * LCAP) {
+      double ls[LCAP + 1];
+      uint32_t lg[LCAP + 1];
 #pragma unroll
-        for (int q = 0; q < KT - 1; ++q) { ls[q] = ls[q + 1]; lg[q] = lg[q + 1]; }
-        ls[KT - 1] = -INFINITY; lg[KT - 1] = INV;
+      for (int q = 0; q <= LCAP; ++q) { ls[q] = -INFINITY; lg[q] = INV; }
+      for (int t = 0; t < LCAP; ++t) {
+        const int g = base + t * G + gl;
+        if (g >= X) break;
+        const Exp x = decode_g(g, pre, ss);
+        const int node = ss[x.j] + x.i;
+        const int so = node - A0;
+        Cand c;
+        if (so < STAGE) {
+          const NodeRec& nr = st[so];
+          c.word = nr.word; c.morph = nr.morph; c.tag = nr.tag; c.mask = nr.mask;
+          c.pre = nr.pre; c.f4 = nr.f4; c.f5 = nr.f5; c.f6 = nr.f6;
+        } else {
+          c = load_cand(B, nbase + (uint32_t)node);
+        }
+        const Hyp h = read_entry(R[(e - x.d) % RING][x.r]);
+        // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
+        if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (x.d < dmax)) continue;
+        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt) : 0.0;
+        const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
+        if (COUNT) ++cnt.exp;
+        list_insert<LCAP + 1>(ls, lg, sc, (uint32_t)g);
       }
-      if (gl == t) { sel_s = bs; sel_g = bg; }
-      ++nsel;
+      if (gl < k) list_insert<LCAP + 1>(ls, lg, rs, rg);   // running entry (earlier g)
+      // k rounds of group argmax over list heads (stable sort + [:k], beam.py:85)
+      double ns = -INFINITY;
+      uint32_t ng = INV;
+      nsel = 0;
+      for (int t = 0; t < k; ++t) {
+        double bs = ls[0];
+        uint32_t bg = lg[0];
+        group_argmax_fast<G>(bs, bg);
+        if (bg == INV) break;
+        if (lg[0] == bg) {
+#pragma unroll
+          for (int q = 0; q < LCAP; ++q) { ls[q] = ls[q + 1]; lg[q] = lg[q + 1]; }
+          ls[LCAP] = -INFINITY; lg[LCAP] = INV;
+        }
+        if (gl == t) { ns = bs; ng = bg; }
+        ++nsel;
+      }
+      rs = ns;
+      rg = ng;
     }
 
     // lanes t < nsel materialise beam[e][t] (Sequence.add, beam.py:112-116)
@@ -635,23 +758,18 @@ lt_beam_k(DecodeParams p) {
     uint32_t bpv = 0;
     const bool writer = gl < nsel;
     if (writer) {
-      const int g = (int)sel_g;
-      int j = 0;
-#pragma unroll
-      for (int q = 1; q < MAX_SPAN; ++q) j = (g >= pre[q]) ? q : j;
-      const int m = ss[j + 1] - ss[j];
-      const int local = g - pre[j];
-      const int r = local / m;
-      const int i = local - r * m;
-      const int d = MAX_SPAN - j;
-      const Entry& h = R[(e - d) % RING][r];
-      const int node = ss[j] + i;
-      const Cand c = load_cand(B, nbase + (uint32_t)node);
-      ne.score = sel_s; ne.f6 = c.f6;
+      const Exp x = decode_g((int)rg, pre, ss);
+      const int node = ss[x.j] + x.i;
+      const int so = node - A0;
+      const Cand c = so < STAGE ? Cand{st[so].word, st[so].morph, st[so].tag, st[so].mask,
+                                        st[so].pre, st[so].f4, st[so].f5, st[so].f6}
+                                : load_cand(B, nbase + (uint32_t)node);
+      const Entry& h = R[(e - x.d) % RING][x.r];
+      ne.score = rs; ne.f6 = c.f6;
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
       ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
       ne.depth = h.depth + 1;
-      bpv = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+      bpv = bp_pack((uint32_t)node, (uint32_t)x.d, (uint32_t)x.r);
     }
     __builtin_amdgcn_wave_barrier();
     if (writer) {
@@ -659,6 +777,16 @@ lt_beam_k(DecodeParams p) {
       bp[(int64_t)e * bstride + gl] = bpv;
     }
     if (gl == 0) cntl[grp][e % RING] = nsel;
+    // stage the next position's candidates
+    pin(nxt);
+    {
+      NodeRec r1;
+      r1.word = nxt.word; r1.morph = nxt.morph; r1.tag = nxt.tag; r1.mask = nxt.mask;
+      r1.pre = nxt.pre; r1.f4 = nxt.f4; r1.f5 = nxt.f5; r1.f6 = nxt.f6;
+      st[gl] = r1;
+    }
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) { pin(ssn[j]); ss[j] = ssn[j]; }
     __builtin_amdgcn_wave_barrier();
   }
 

@@ -420,29 +420,32 @@ def pack_fast(raw, model, lay=None, cols=None):
 # ---------------------------------------------------------------------------
 # Word rendering (reference input form)
 # ---------------------------------------------------------------------------
-def to_words(raw, model, word_cls=None, sentences=None):
-    """Render sentences as ``(bindex, chars)`` over ``word_cls`` nodes and the
-    model as ``(feature_dic, coefficients)``."""
+def render_sentences(raw, sentences, word_cls=None):
+    """``(bindex, chars)`` lattices of ``word_cls`` nodes for the given sentences."""
     from .word import Word
     word_cls = word_cls or Word
-    ids = raw.ids
-    R = ids.render
-    sentences = range(raw.S) if sentences is None else sentences
+    R = raw.ids.render
     out = []
     node_sent = raw.char_sent[raw.node_char]
+    starts = np.searchsorted(node_sent, np.arange(raw.S + 1))
     for s in sentences:
         n = int(raw.sent_n[s])
         c0 = int(raw.sent_char_off[s])
         chars = ''.join(chr(0xAC00 + int(c)) for c in raw.chars[c0:c0 + n])
         bindex = [[] for _ in range(n)]
-        sel = np.flatnonzero(node_sent == s)
-        for t in sel:
+        for t in range(int(starts[s]), int(starts[s + 1])):
             b = int(raw.node_char[t]) - c0
             d = int(raw.node_d[t])
             w = word_cls(R(raw.word[t]), R(raw.morph[t]), None, POS_TAGS[int(raw.tag[t])], None,
                          int(raw.length[t]), b, b + d, bool(raw.is_l[t]))
             bindex[b].append(w)
         out.append((bindex, chars))
+    return out
+
+
+def render_model(raw, model):
+    """The model as ``(feature_dic over Python tuples, coefficients)``."""
+    R = raw.ids.render
     dic = {}
     for row, i in zip(model.probed, model.probed_idx):
         cls = int(row[0])
@@ -454,4 +457,12 @@ def to_words(raw, model, word_cls=None, sentences=None):
         dic[(5, R(row[0]), R(row[1]), bool(row[2]))] = int(i)
     for v, i in model.keys6.items():
         dic[(6, v)] = i
-    return out, dic, model.coef
+    return dic, model.coef
+
+
+def to_words(raw, model, word_cls=None, sentences=None):
+    """Render sentences as ``(bindex, chars)`` over ``word_cls`` nodes and the
+    model as ``(feature_dic, coefficients)``."""
+    sentences = range(raw.S) if sentences is None else sentences
+    dic, coef = render_model(raw, model)
+    return render_sentences(raw, sentences, word_cls), dic, coef

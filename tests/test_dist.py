@@ -1,0 +1,79 @@
+"""Multi-process (gloo, world_size 2, CPU) coverage of the sharding path: shard
+ranges tile the batch, per-rank decodes of the shards reassemble to the
+single-process decode, and the host group's barrier/max/sum/gather work.
+The per-rank decode here is the C restatement (oracle) standing in for the
+device, which the CPU container does not have."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from lattice_based_tagger_amd import dist, synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_shard_range_tiles_and_balances():
+    rng = np.random.default_rng(0)
+    w = rng.integers(40, 100, size=1001)
+    for world in (1, 2, 3, 8):
+        cuts = [dist.shard_range(w, world, r) for r in range(world)]
+        assert cuts[0][0] == 0 and cuts[-1][1] == len(w)
+        for (a, b), (c, d) in zip(cuts, cuts[1:]):
+            assert b == c and a <= b
+        loads = [w[a:b].sum() for a, b in cuts]
+        assert max(loads) - min(loads) <= 2 * w.max()
+    assert dist.shard_range([], 4, 3) == (0, 0)
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from oracle import lt_oracle
+    g = dist.HostGroup()
+    raw = synth.make_lattices(96, seed=11, eojeols=6)
+    sm = synth.make_model(raw, seed=11, n_features=4000)
+    packed, keys, coefs = synth.pack_fast(raw, sm)
+    lo, hi = dist.shard_range(packed.sent_n, g.ranks.world, g.ranks.rank)
+    count, length, score, codes, ex, tu = lt_oracle.decode(packed, keys, coefs, 2, s0=lo, s1=hi)
+    cum = np.concatenate([[0], np.cumsum(packed.sent_n.astype(np.int64))])
+    mine = (lo, hi, count[lo:hi].copy(), length[lo:hi].copy(), score[lo:hi].copy(),
+            codes[2 * cum[lo]:2 * cum[hi]].copy())
+    g.barrier()
+    total = g.sum(float(hi - lo))
+    mx = g.max(float(rank))
+    parts = g.gather(mine)
+    if rank == 0:
+        full = lt_oracle.decode(packed, keys, coefs, 2)
+        ok = total == len(packed.sent_n) and mx == world - 1
+        got_count = np.concatenate([p[2] for p in parts])
+        got_len = np.concatenate([p[3] for p in parts])
+        got_score = np.concatenate([p[4] for p in parts])
+        got_codes = np.concatenate([p[5] for p in parts])
+        ok = ok and np.array_equal(got_count, full[0]) and np.array_equal(got_len, full[1])
+        ok = ok and np.array_equal(got_score.view(np.uint64), full[2].view(np.uint64))
+        ok = ok and np.array_equal(got_codes, full[3])
+        out_q.put(bool(ok))
+    g.close()
+
+
+def test_two_rank_gloo_shards_reassemble():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True
