@@ -4,9 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -62,20 +64,26 @@ struct lt_ctx {
   unsigned long long* d_counters = nullptr;
 };
 
-struct lt_model {
-  lt_ctx* ctx = nullptr;
-  void* d_table = nullptr;
-  int64_t slots = 0;
-  uint32_t seed = 0;
-  int narrow = 0;          // 16 B SlotN (all ids < 2^20) or 32 B SlotW
-};
-
 namespace {
 
 struct KeyRec {
   uint32_t a, b, c, cls;
   double coef;
 };
+
+}  // namespace
+
+struct lt_model {
+  lt_ctx* ctx = nullptr;
+  void* d_table = nullptr;
+  int64_t slots = 0;
+  uint32_t seed = 0;
+  int narrow = 0;          // 16 B SlotN (all ids < 2^20) or 32 B SlotW
+  std::vector<KeyRec> keys;  // host copy (narrow models): hot-table selection
+  uint64_t uid = 0;          // unique per created model (hot-table cache key)
+};
+
+namespace {
 
 // Cuckoo table build (two choices, one slot per bucket).  Returns false when
 // the random walk fails; the caller reseeds / grows and retries.
@@ -160,6 +168,11 @@ struct lt_batch {
   // pinned host results
   int32_t *h_count = nullptr, *h_len = nullptr, *h_codes = nullptr;
   double* h_score = nullptr;
+  // component frequencies of the batch's nodes (ids < 2^20) and the hot table
+  // built for the last model decoded with this batch
+  std::vector<uint32_t> f_word, f_tag, f_morph;
+  uint64_t hot_uid = 0;      // lt_model::uid the hot table was built for (0: none)
+  SlotN* d_hot = nullptr;
 };
 
 extern "C" {
@@ -276,6 +289,9 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
   m->slots = slots;
   m->seed = seed;
   m->narrow = narrow ? 1 : 0;
+  if (narrow) m->keys.swap(keys);
+  static std::atomic<uint64_t> next_uid{1};
+  m->uid = next_uid.fetch_add(1);
   hipError_t e = hipMalloc(&m->d_table, (size_t)(slots * slot_bytes));
   if (e == hipSuccess)
     e = hipMemcpyAsync(m->d_table, narrow ? (const void*)tn.data() : (const void*)tw.data(),
@@ -365,7 +381,7 @@ static void batch_free(lt_batch* b) {
   if (!b) return;
   void* dev[] = {b->d_order, b->d_sent_n, b->d_span_start, b->d_node_off, b->d_span_off,
                  b->d_bp_off, b->d_cum_n, b->d_nodes, b->d_post, b->d_bp, b->d_count,
-                 b->d_len, b->d_codes, b->d_score};
+                 b->d_len, b->d_codes, b->d_score, b->d_hot};
   for (void* p : dev) dfree(p);
   void* host[] = {b->h_count, b->h_len, b->h_codes, b->h_score};
   for (void* p : host)
@@ -442,6 +458,19 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     }
   }
   up(&b->d_nodes, recs.data(), recs.size());
+  {
+    const uint32_t lim = 1u << NARROW_ID_BITS;
+    b->f_word.assign(lim, 0u);
+    b->f_tag.assign(lim, 0u);
+    b->f_morph.assign(lim, 0u);
+    for (int64_t i = 0; i < d->n_nodes; ++i) {
+      const uint32_t w = (uint32_t)d->node_word[i], t = (uint32_t)d->node_tag[i],
+                     mo = (uint32_t)d->node_morph0[i];
+      if (w < lim) ++b->f_word[w];
+      if (t < lim) ++b->f_tag[t];
+      if (mo < lim) ++b->f_morph[mo];
+    }
+  }
   up(&b->d_post, d->node_post, (size_t)d->n_post * (size_t)d->n_nodes);
   const size_t nres = (size_t)S * max_k;
   const size_t ncodes = (size_t)b->total_chars * max_k;
@@ -474,6 +503,62 @@ lt_status lt_batch_destroy(lt_batch* b) {
 
 int64_t lt_batch_code_slots(const lt_batch* b, int k) { return b ? b->total_chars * (int64_t)k : 0; }
 
+// ----------------------------------------------------------- hot table --
+// Keys of a narrow model ranked by estimated probe frequency in this batch:
+// the product of the relative frequencies of the key's components among the
+// batch's nodes (word / tag / morph0 slots per feature class), the hottest
+// placed first into a direct-mapped HOT_SLOTS table (a key whose slot is
+// taken is simply not cached).
+static lt_status build_hot(lt_ctx* c, const lt_model* m, lt_batch* b) {
+  if (b->hot_uid == m->uid) return LT_OK;
+  b->hot_uid = 0;
+  if (!m->narrow) return LT_OK;
+  // opt-in (LT_HOT=1) until it pays: it trades global probe traffic for LDS
+  // reads and VALU, and the k=1 kernel is currently VALU/latency bound
+  static const bool enabled = [] {
+    const char* v = std::getenv("LT_HOT");
+    return v && v[0] == '1';
+  }();
+  if (!enabled) return LT_OK;
+  const double inv = b->n_nodes ? 1.0 / (double)b->n_nodes : 0.0;
+  auto fw = [&](uint32_t x) { return b->f_word[x] * inv; };
+  auto ft = [&](uint32_t x) { return b->f_tag[x] * inv; };
+  auto fm = [&](uint32_t x) { return b->f_morph[x] * inv; };
+  const size_t F = m->keys.size();
+  std::vector<std::pair<double, uint32_t>> score(F);
+  for (size_t i = 0; i < F; ++i) {
+    const KeyRec& k = m->keys[i];
+    double v = 0.0;
+    switch (k.cls) {
+      case 0: v = fw(k.a) * fw(k.b) * ft(k.c); break;
+      case 1: v = fw(k.a) * ft(k.b); break;
+      case 2: v = ft(k.a) * fw(k.b) * ft(k.c); break;
+      case 3: v = ft(k.a) * ft(k.b); break;
+      case 7: v = fw(k.a) * fw(k.b) * fw(k.c); break;
+      case 8: v = fm(k.a) * fm(k.b); break;
+    }
+    score[i] = {v, (uint32_t)i};
+  }
+  const size_t top = std::min(F, (size_t)HOT_SLOTS * 4);
+  std::partial_sort(score.begin(), score.begin() + top, score.end(),
+                    [](const std::pair<double, uint32_t>& x, const std::pair<double, uint32_t>& y) {
+                      return x.first > y.first || (x.first == y.first && x.second < y.second);
+                    });
+  std::vector<SlotN> hot(HOT_SLOTS, SlotN{0ull, 0.0});
+  for (size_t r = 0; r < top; ++r) {
+    if (score[r].first <= 0.0) break;
+    const KeyRec& k = m->keys[score[r].second];
+    SlotN& sl = hot[hot_slot(key_base<true>(k.a, k.b, k.c, k.cls))];
+    if (sl.key == 0) { sl.key = narrow_key(k.a, k.b, k.c, k.cls); sl.coef = k.coef; }
+  }
+  if (!b->d_hot) HIP_TRY(hipMalloc((void**)&b->d_hot, HOT_SLOTS * sizeof(SlotN)));
+  HIP_TRY(hipMemcpyAsync(b->d_hot, hot.data(), HOT_SLOTS * sizeof(SlotN), hipMemcpyHostToDevice,
+                         c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  b->hot_uid = m->uid;
+  return LT_OK;
+}
+
 // --------------------------------------------------------------- decode --
 static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, DecodeParams& p) {
   if (!c || !m || !b) return fail(LT_EINVAL, "decode: NULL argument");
@@ -485,6 +570,9 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.table = m->d_table;
   p.slots = (uint32_t)m->slots;
   p.seed = m->seed;
+  lt_status hs = build_hot(c, m, b);
+  if (hs != LT_OK) return hs;
+  p.hot = (b->hot_uid == m->uid) ? b->d_hot : nullptr;
   p.narrow = m->narrow;
   p.has_tri = b->has_tri;
   p.n_sent = b->n_sent;

@@ -101,6 +101,13 @@ LT_HD void cuckoo_slots(KeyBase kb, uint32_t seed, uint32_t slots, uint32_t& i1,
   i2 = slot_of(mix1(kb.b2 ^ (seed * 0x9E3779B1u + 0x632BE5ABu)), slots);
 }
 
+// Hot-key table: a direct-mapped subset of the model (the keys with the
+// highest estimated probe frequency in a batch), staged in LDS by every
+// block.  Optional: a key missing from it is looked up in the full table.
+constexpr int HOT_SLOTS = 1024;
+constexpr uint32_t HOT_SEED = 0x6A09E667u;
+LT_HD uint32_t hot_slot(KeyBase kb) { return mix1(kb.b1 ^ HOT_SEED) & (HOT_SLOTS - 1); }
+
 // Device node record (AoS, 48 B = 3 x 16 B loads), built by the library from
 // the SoA arrays of lt_batch_desc.
 struct alignas(16) NodeRec {

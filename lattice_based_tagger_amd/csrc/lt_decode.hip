@@ -86,40 +86,43 @@ __device__ __forceinline__ Cand load_cand(const Bufs& B, uint32_t gn) {
   return c;
 }
 
-// Buffer -> LDS DMA of one node record per lane (three 16 B planes; lane l's
-// bytes land at plane + 16*l).  `planes` points at this wave's 3 x 64 x 16 B
-// region; no VGPR holds the data.
+// Buffer -> LDS DMA of a block of consecutive node records.  A group of G
+// lanes stages the records [first, first + G) of its sentence: instruction p
+// (p = 0..2) has lane l fetch the contiguous 16 B chunk p*G + l of the block,
+// so each instruction touches 16*G contiguous bytes (4 cache lines per 16
+// lanes) instead of one line per lane.  The DMA writes lane l's 16 B at
+// wave_planes + p*1024 + 16*lane; `gbase` is the group's first lane in its
+// wave.  No VGPR holds the data.
 typedef __attribute__((address_space(3))) void lds_void;
-__device__ __forceinline__ void dma_cand(const Bufs& B, uint32_t gn, uint4* planes) {
-  const uint32_t o = gn == INV ? OOB : gn * (uint32_t)sizeof(NodeRec);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(planes), 16, o, 0, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(planes + 64), 16,
-                                           o == OOB ? OOB : o + 16u, 0, 0, 0);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(planes + 128), 16,
-                                           o == OOB ? OOB : o + 32u, 0, 0, 0);
+template <int G>
+__device__ __forceinline__ void dma_block(const Bufs& B, uint32_t first, bool valid, uint4* wave_planes,
+                                          int gl) {
+  const uint32_t base = first * (uint32_t)sizeof(NodeRec);
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const uint32_t o = valid ? base + (uint32_t)(pl * G + gl) * 16u : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wave_planes + pl * 64), 16, o, 0, 0, 0);
+  }
 }
-__device__ __forceinline__ Cand read_staged(const uint4* planes, int lane) {
-  const uint4 a = planes[lane], b = planes[64 + lane], c4 = planes[128 + lane];
+// record r (0 <= r < G) of the staged block
+template <int G>
+__device__ __forceinline__ Cand read_block(const uint4* wave_planes, int gbase, int r) {
+  uint4 q[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int c = 3 * r + t;
+    q[t] = wave_planes[(c / G) * 64 + gbase + (c % G)];
+  }
   Cand c;
-  c.word = a.x; c.morph = a.y; c.tag = a.z; c.mask = a.w;
-  c.pre = dbl(b.x, b.y); c.f4 = dbl(b.z, b.w);
-  c.f5 = dbl(c4.x, c4.y); c.f6 = dbl(c4.z, c4.w);
+  c.word = q[0].x; c.morph = q[0].y; c.tag = q[0].z; c.mask = q[0].w;
+  c.pre = dbl(q[1].x, q[1].y); c.f4 = dbl(q[1].z, q[1].w);
+  c.f5 = dbl(q[2].x, q[2].y); c.f6 = dbl(q[2].z, q[2].w);
   return c;
 }
 
 // Pin prefetched values in registers: the empty asm makes them opaque, so the
 // compiler cannot re-issue ("rematerialise") the loads at their later use.
-__device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ void pin(double& x) {
-  uint64_t b = __builtin_bit_cast(uint64_t, x);
-  asm volatile("" : "+v"(b));
-  x = __builtin_bit_cast(double, b);
-}
-__device__ __forceinline__ void pin(Cand& c) {
-  pin(c.word); pin(c.morph); pin(c.tag); pin(c.mask);
-  pin(c.pre); pin(c.f4); pin(c.f5); pin(c.f6);
-}
 
 // Hypothesis fields the scorer needs (from the LDS frontier).
 struct Hyp {
@@ -260,9 +263,9 @@ struct Counts {
 //   probe_finish  -- match / collision chains, numpy-order sum
 template <bool NARROW>
 struct Probe {
-  typename Tab<NARROW>::S s1[6], s2[6];   // the two cuckoo candidates
-  typename Tab<NARROW>::Key key[6];       // expected key of probe q
+  typename Tab<NARROW>::S s1[6], s2[6];   // the two cuckoo candidates (valid where needed)
   uint32_t need;                           // bit q: probe q is needed
+  uint32_t gneed;                          // bit q: probe q went to the global table
 };
 
 // Key components of probe q for (h, c); recomputed where needed instead of
@@ -307,21 +310,46 @@ __device__ __forceinline__ uint32_t probe_need(const Hyp& h, const Cand& c) {
   return need;
 }
 
+// hot: the block's LDS copy of the batch hot table (HOT_SLOTS SlotN), or
+// nullptr.  A needed probe first reads its one hot slot; only a hot miss
+// issues the two global cuckoo loads.
 template <bool NARROW>
 __device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uint32_t slots,
                                             uint32_t seed, const Hyp& h, const Cand& c,
-                                            uint32_t need) {
+                                            uint32_t need, const uint4* hot) {
   using T = Tab<NARROW>;
   P.need = need;
   const Keys K = make_keys(h, c, use_j8_of(h, c));
+  uint32_t gneed = need;
+  if constexpr (NARROW) {
+    if (hot) {
+      // the hot slot is read into s1 (no extra registers); a hit keeps it
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+        if ((need >> q) & 1u) {
+          const uint4 hv = hot[hot_slot(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]))];
+          P.s1[q].key = ((uint64_t)hv.y << 32) | hv.x;
+          P.s1[q].coef = __builtin_bit_cast(double, (u32x2){hv.z, hv.w});
+        }
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+        if (((need >> q) & 1u) && T::hit(P.s1[q], T::key(K.a[q], K.b[q], K.c[q], PCLS[q])))
+          gneed &= ~(1u << q);
+    }
+  }
+  P.gneed = gneed;
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
-    uint32_t i1, i2;
-    cuckoo_slots(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
-    P.key[q] = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
-    const bool nq = (need >> q) & 1u;
-    P.s1[q] = T::load(B.tab, nq ? i1 * T::SZ : OOB);
-    P.s2[q] = T::load(B.tab, nq ? i2 * T::SZ : OOB);
+    // exec-masked, not out-of-range: an OOB lane still costs the address
+    // unit (TA) a slot, an inactive lane does not
+    // (slots stay undefined when not needed; probe_finish reads them only
+    // under the same predicate)
+    if ((gneed >> q) & 1u) {
+      uint32_t i1, i2;
+      cuckoo_slots(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
+      P.s1[q] = T::load(B.tab, i1 * T::SZ);
+      P.s2[q] = T::load(B.tab, i2 * T::SZ);
+    }
   }
 }
 
@@ -330,14 +358,21 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
                                                const Cand& c, Counts& cnt) {
   using T = Tab<NARROW>;
   const uint32_t jm = h.jmask, km = c.mask, im = h.imask;
+  // keys recomputed from (h, c), which stay live anyway
+  const Keys K = make_keys(h, c, use_j8_of(h, c));
   bool pr6[6];
   double cf[6];
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
-    const bool m1 = T::hit(P.s1[q], P.key[q]);
-    const bool m2 = T::hit(P.s2[q], P.key[q]);
-    pr6[q] = ((P.need >> q) & 1u) && (m1 || m2);
-    cf[q] = m1 ? P.s1[q].coef : P.s2[q].coef;
+    pr6[q] = false;
+    cf[q] = 0.0;
+    if ((P.need >> q) & 1u) {
+      const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
+      const bool m1 = T::hit(P.s1[q], key);                // hot hits land in s1
+      const bool m2 = ((P.gneed >> q) & 1u) && T::hit(P.s2[q], key);
+      pr6[q] = m1 || m2;
+      cf[q] = m1 ? P.s1[q].coef : P.s2[q].coef;
+    }
   }
   double v[9];
   bool pr[9];
@@ -360,9 +395,10 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
 
 template <bool NARROW, bool COUNT>
 __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_t seed,
-                                          const Hyp& h, const Cand& c, Counts& cnt) {
+                                          const Hyp& h, const Cand& c, Counts& cnt,
+                                          const uint4* hot) {
   Probe<NARROW> P;
-  probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c));
+  probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c), hot);
   return probe_finish<NARROW, COUNT>(P, h, c, cnt);
 }
 
@@ -396,11 +432,21 @@ __device__ __forceinline__ Hyp read_hyp(const VEntry& e) {
 }
 
 template <bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
 lt_viterbi_k(DecodeParams p) {
   __shared__ VEntry ring[V_SPB][RING];
   __shared__ uint32_t bpl[V_SPB][V_BP_LDS];
   __shared__ uint4 stg[4][3 * 64];             // per wave: 3 planes x 64 lanes x 16 B
+  __shared__ uint4 hotl[NARROW ? HOT_SLOTS : 1];
+
+  const bool use_hot = NARROW && p.hot != nullptr;
+  if (use_hot) {                                 // stage the batch hot table (all threads)
+    const uint4* src = reinterpret_cast<const uint4*>(p.hot);
+#pragma unroll
+    for (int i = 0; i < HOT_SLOTS / 256; ++i) hotl[i * 256 + threadIdx.x] = src[i * 256 + threadIdx.x];
+    __syncthreads();
+  }
+  const uint4* hot = use_hot ? hotl : nullptr;
 
   const int grp = threadIdx.x / V_G;
   const int gl = threadIdx.x % V_G;
@@ -434,8 +480,8 @@ lt_viterbi_k(DecodeParams p) {
   int A1 = ssp[n >= 1 ? 8 : 0];
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   uint4* const wst = stg[wv];
-  const int lane = (int)(threadIdx.x & 63);
-  dma_cand(B, (n >= 1 && gl < A1 - A0) ? nbase + (uint32_t)(A0 + gl) : INV, wst);
+  const int gbase = (int)(threadIdx.x & 63) - gl;
+  dma_block<V_G>(B, nbase + (uint32_t)A0, n >= 1, wst, gl);
   int em9 = 0;
   for (int e = 1; e <= n; ++e) {
     // everything still outstanding was issued a full position ago (prefetch,
@@ -445,7 +491,7 @@ lt_viterbi_k(DecodeParams p) {
     em9 = em9 == RING - 1 ? 0 : em9 + 1;
     const int dmax = min(e, p.max_len);
     const int X = A1 - A0;
-    const Cand cur = read_staged(wst, lane);   // this position's candidate (staged by DMA)
+    const Cand cur = read_block<V_G>(wst, gbase, gl);   // this position's candidate (staged by DMA)
 
     double best_s = -INFINITY;
     uint32_t best_g = INV;
@@ -463,17 +509,21 @@ lt_viterbi_k(DecodeParams p) {
     // node past the batch end reads as zeros).  Issued ahead of the probes.
     int A2 = ssp[min(e + 1, n) * 8];
     __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): cur is out of the staging area
-    dma_cand(B, e < n ? nbase + (uint32_t)(A1 + gl) : INV, wst);
+    dma_block<V_G>(B, nbase + (uint32_t)A1, e < n, wst, gl);
     __builtin_amdgcn_sched_barrier(0);
 
     // probes of candidate gl (unneeded ones read nothing)
     Probe<NARROW> P;
     probe_issue<NARROW>(P, B, slots, seed, h0, cur,
-                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u);
+                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, hot);
+    // re-read the hypothesis from LDS instead of holding it in VGPRs across
+    // the probe wait (the compiler barrier stops the reload being merged)
+    asm volatile("" ::: "memory");
+    const Hyp h1 = read_hyp(R[act ? bm0 : 0]);
     if (!skip0) {
-      const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h0, cur, cnt) : 0.0;
+      const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h1, cur, cnt) : 0.0;
       if (COUNT) ++cnt.exp;
-      best_s = h0.score + increment(p, cur, tri, nbase + (uint32_t)(A0 + gl));  // beam.py:115
+      best_s = h1.score + increment(p, cur, tri, nbase + (uint32_t)(A0 + gl));  // beam.py:115
       best_g = (uint32_t)gl;
     }
     // more than 16 candidates ending at e (rare): serial extra rounds
@@ -484,7 +534,7 @@ lt_viterbi_k(DecodeParams p) {
       bm += bm < 0 ? RING : 0;
       const Hyp h = read_hyp(R[bm]);
       if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;   // beam.py:43-45
-      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt) : 0.0;
+      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, hot) : 0.0;
       if (COUNT) ++cnt.exp;
       const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)(A0 + g));
       if (better(sc, (uint32_t)g, best_s, best_g)) { best_s = sc; best_g = (uint32_t)g; }
@@ -496,7 +546,7 @@ lt_viterbi_k(DecodeParams p) {
     __builtin_amdgcn_wave_barrier();
     if (wg != INV && best_g == wg) {                 // the winner writes beam[e] (beam.py:112-116)
       Cand c = cur;
-      Hyp h = h0;
+      Hyp h = h1;
       int d = d0;
       if (wg != (uint32_t)gl) {                      // won in an extra round: reload
         c = load_cand(B, nbase + (uint32_t)(A0 + (int)wg));
@@ -636,7 +686,7 @@ lt_beam_k(DecodeParams p) {
   static_assert(KT <= G, "beam width must not exceed the lane group");
   __shared__ Entry ring[SPB][RING][KT];
   __shared__ int32_t cntl[SPB][RING];
-  __shared__ NodeRec stage[SPB][STAGE];
+  __shared__ uint4 stg[2][4][3 * 64];        // [position parity][wave][plane x lane]
 
   const int grp = threadIdx.x / G;
   const int gl = threadIdx.x % G;
@@ -653,7 +703,8 @@ lt_beam_k(DecodeParams p) {
   const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
   Entry (&R)[RING][KT] = ring[grp];
-  NodeRec* __restrict__ st = stage[grp];
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int gbase = (int)(threadIdx.x & 63) - gl;      // first lane of this group in its wave
   Counts cnt;
 
   if (gl == 0) {                             // beam[0] = [BOS] (beam.py:21-23)
@@ -669,17 +720,12 @@ lt_beam_k(DecodeParams p) {
   int ss[MAX_SPAN + 1];
 #pragma unroll
   for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = n >= 1 ? ssp[j] : 0;
-  {
-    const Cand c0 = load_cand(B, (n >= 1 && gl < ss[MAX_SPAN] - ss[0]) ? nbase + (uint32_t)(ss[0] + gl) : INV);
-    NodeRec r0;
-    r0.word = c0.word; r0.morph = c0.morph; r0.tag = c0.tag; r0.mask = c0.mask;
-    r0.pre = c0.pre; r0.f4 = c0.f4; r0.f5 = c0.f5; r0.f6 = c0.f6;
-    st[gl] = r0;
-  }
+  dma_block<G>(B, nbase + (uint32_t)ss[0], n >= 1, stg[1][wv], gl);
   __builtin_amdgcn_wave_barrier();
 
   for (int e = 1; e <= n; ++e) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): last position's prefetch
+    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): this position's records landed
+    const uint4* const cst = stg[e & 1][wv];
     const int dmax = min(e, p.max_len);
     const int A0 = ss[0];
     int pre[MAX_SPAN + 1];
@@ -692,12 +738,14 @@ lt_beam_k(DecodeParams p) {
     }
     const int X = pre[MAX_SPAN];
 
-    // prefetch of end position e+1: span starts and candidate records
+    // prefetch of end position e+1: span starts (registers) and candidate
+    // records (DMA into the other parity buffer, last read a position ago)
     int ssn[MAX_SPAN + 1];
     const int en = min(e + 1, n);
 #pragma unroll
     for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = ssp[(en - 1) * MAX_SPAN + j];
-    Cand nxt = load_cand(B, e < n ? nbase + (uint32_t)(ss[MAX_SPAN] + gl) : INV);
+    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
+    dma_block<G>(B, nbase + (uint32_t)ss[MAX_SPAN], e < n, stg[(e + 1) & 1][wv], gl);
     __builtin_amdgcn_sched_barrier(0);
 
     // chunks of G*LCAP expansions merged into the running top-k (lanes < k)
@@ -715,18 +763,11 @@ lt_beam_k(DecodeParams p) {
         const Exp x = decode_g(g, pre, ss);
         const int node = ss[x.j] + x.i;
         const int so = node - A0;
-        Cand c;
-        if (so < STAGE) {
-          const NodeRec& nr = st[so];
-          c.word = nr.word; c.morph = nr.morph; c.tag = nr.tag; c.mask = nr.mask;
-          c.pre = nr.pre; c.f4 = nr.f4; c.f5 = nr.f5; c.f6 = nr.f6;
-        } else {
-          c = load_cand(B, nbase + (uint32_t)node);
-        }
+        const Cand c = so < STAGE ? read_block<G>(cst, gbase, so) : load_cand(B, nbase + (uint32_t)node);
         const Hyp h = read_entry(R[(e - x.d) % RING][x.r]);
         // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
         if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (x.d < dmax)) continue;
-        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt) : 0.0;
+        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, nullptr) : 0.0;
         const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
         if (COUNT) ++cnt.exp;
         list_insert<LCAP + 1>(ls, lg, sc, (uint32_t)g);
@@ -761,9 +802,7 @@ lt_beam_k(DecodeParams p) {
       const Exp x = decode_g((int)rg, pre, ss);
       const int node = ss[x.j] + x.i;
       const int so = node - A0;
-      const Cand c = so < STAGE ? Cand{st[so].word, st[so].morph, st[so].tag, st[so].mask,
-                                        st[so].pre, st[so].f4, st[so].f5, st[so].f6}
-                                : load_cand(B, nbase + (uint32_t)node);
+      const Cand c = so < STAGE ? read_block<G>(cst, gbase, so) : load_cand(B, nbase + (uint32_t)node);
       const Entry& h = R[(e - x.d) % RING][x.r];
       ne.score = rs; ne.f6 = c.f6;
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
@@ -777,14 +816,6 @@ lt_beam_k(DecodeParams p) {
       bp[(int64_t)e * bstride + gl] = bpv;
     }
     if (gl == 0) cntl[grp][e % RING] = nsel;
-    // stage the next position's candidates
-    pin(nxt);
-    {
-      NodeRec r1;
-      r1.word = nxt.word; r1.morph = nxt.morph; r1.tag = nxt.tag; r1.mask = nxt.mask;
-      r1.pre = nxt.pre; r1.f4 = nxt.f4; r1.f5 = nxt.f5; r1.f6 = nxt.f6;
-      st[gl] = r1;
-    }
 #pragma unroll
     for (int j = 0; j <= MAX_SPAN; ++j) { pin(ssn[j]); ss[j] = ssn[j]; }
     __builtin_amdgcn_wave_barrier();

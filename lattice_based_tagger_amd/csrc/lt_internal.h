@@ -11,6 +11,7 @@ struct DecodeParams {
   const void* table;            // SlotN[] or SlotW[] (cuckoo, two choices)
   uint32_t slots;
   uint32_t seed;
+  const SlotN* hot;             // HOT_SLOTS-slot LDS hot table (narrow only) or NULL
   int32_t narrow;               // 1: SlotN, 0: SlotW
   int32_t has_tri;
   // batch (device pointers)
