@@ -30,6 +30,8 @@
 // are summed in numpy's pairwise order; ties go to the lower
 // generation index (Python's stable sort).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <cstring>
 #include <math.h>
 #include "lt_common.h"
 #include "lt_internal.h"
@@ -597,6 +599,271 @@ lt_viterbi_k(DecodeParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// beam_size = 1, packed lanes.  A wave owns W sentences and walks their end
+// positions in lockstep; at each position the candidates of all W sentences
+// are packed onto the 64 lanes (one contiguous lane segment per sentence,
+// segment starts from scalar prefix sums), so lanes are not left idle by short
+// positions or finished sentences.  If the candidates exceed the lanes, each
+// segment is shrunk and its lanes take candidates g, g+L, g+2L...
+// Per-sentence argmax: LDS max over an order-preserving 64-bit score key, then
+// LDS min over the generation index among the lanes holding the maximum --
+// exactly the reference's (score desc, generation asc) order.
+// ---------------------------------------------------------------------------
+constexpr int P_WPB = 4;                // waves per block
+
+__device__ __forceinline__ unsigned long long ord_key(double sc) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, sc + 0.0);      // -0.0 -> +0.0
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// per-sentence record of one end position (LDS): first candidate (global
+// node index), lanes in the segment, candidates, first candidate (local)
+struct alignas(16) SegRec {
+  uint32_t nb, L, X, a;
+};
+// per-sentence static record (LDS)
+struct alignas(16) SentRec {
+  uint32_t n, bp_lo, bp_hi, in_lds;
+};
+
+template <int W, bool NARROW, bool COUNT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+lt_viterbi_pk(DecodeParams p) {
+  constexpr int BPL = W <= 6 ? 256 : 128;       // end positions whose backpointer stays in LDS
+  __shared__ VEntry ring[P_WPB][W][RING];
+  __shared__ uint32_t bpl[P_WPB][W][BPL];
+  __shared__ uint4 stg[P_WPB][3 * 64];
+  __shared__ SegRec seg[P_WPB][2][W];
+  __shared__ SentRec srec[P_WPB][W];
+  __shared__ unsigned long long amax[P_WPB][2][W];
+  __shared__ uint32_t amin[P_WPB][2][W];
+
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = (int)(threadIdx.x & 63);
+  const int slot0 = (blockIdx.x * P_WPB + wv) * W;
+  if (slot0 >= p.n_sent) return;                // whole wave
+  const Bufs B = make_bufs(p);
+  const uint32_t slots = p.slots, seed = p.seed;
+  const int has_tri = p.has_tri;
+  const int bstride = p.bp_stride;
+  uint4* const wst = stg[wv];
+  VEntry (*const R)[RING] = ring[wv];
+  Counts cnt;
+
+  // lane w < W owns sentence w of the wave
+  const bool own = lane < W && slot0 + lane < p.n_sent;
+  const int sid = own ? p.order[slot0 + lane] : 0;
+  const int nw = own ? p.sent_n[sid] : 0;
+  const uint32_t nbase = own ? (uint32_t)p.node_off[sid] : 0u;
+  const int32_t* const ssp = p.span_start + (own ? p.span_off[sid] : 0);
+  if (own) {
+    const int64_t bo = p.bp_off[sid];
+    SentRec r;
+    r.n = (uint32_t)nw; r.bp_lo = (uint32_t)bo; r.bp_hi = (uint32_t)(bo >> 32);
+    r.in_lds = nw < BPL ? 1u : 0u;
+    srec[wv][lane] = r;
+    const Cand b0 = load_cand(B, nbase);       // beam[0] = [BOS] (beam.py:21-23)
+    VEntry e0;
+    e0.score = 0.0; e0.f6 = b0.f6;
+    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
+    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+    R[lane][0] = e0;
+  }
+  if (lane < W) {
+    amax[wv][0][lane] = 0ull; amax[wv][1][lane] = 0ull;
+    amin[wv][0][lane] = INV; amin[wv][1][lane] = INV;
+  }
+  int nmax = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) nmax = max(nmax, __builtin_amdgcn_readlane(nw, w));
+
+  // span starts A_e = ssp[(min(e, n+1) - 1) * 8] of the owned sentence
+  int A0 = own ? ssp[0] : 0;
+  int A1 = own ? ssp[min(1, nw) * 8] : 0;
+  int A2 = own ? ssp[min(2, nw) * 8] : 0;
+
+  // lane mapping of end position e from (A_e, A_{e+1}) of every sentence:
+  // writes seg[buf][w], returns this lane's sentence (W = idle) and first
+  // candidate, and the candidate's global node index.
+  auto map_position = [&](int e, int Ae, int Ae1, int buf, int& ms, int& mg, uint32_t& gnode) {
+    const int X = (lane < W && e <= nw) ? Ae1 - Ae : 0;
+    int Xs[W];
+    int T = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) { Xs[w] = __builtin_amdgcn_readlane(X, w); T += Xs[w]; }
+    int Ls[W];
+    if (T <= 64) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) Ls[w] = Xs[w];
+    } else {                                    // rare: fold each segment
+      const int c = (T + (64 - W) - 1) / (64 - W);
+#pragma unroll
+      for (int w = 0; w < W; ++w) Ls[w] = (Xs[w] + c - 1) / c;
+    }
+    int sidx = 0, pst = 0, run = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      run += Ls[w];
+      if (lane >= run) { sidx = w + 1; pst = run; }
+    }
+    if (lane < W) {
+      int myL = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) myL = (lane == w) ? Ls[w] : myL;
+      SegRec r;
+      r.nb = nbase + (uint32_t)Ae; r.L = (uint32_t)myL; r.X = (uint32_t)X; r.a = (uint32_t)Ae;
+      seg[wv][buf][lane] = r;
+    }
+    ms = sidx;
+    mg = lane - pst;
+    __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): seg written
+    const SegRec r = seg[wv][buf][sidx < W ? sidx : 0];
+    gnode = sidx < W ? r.nb + (uint32_t)mg : INV;
+  };
+
+  int ms, mg;
+  uint32_t gn;
+  map_position(1, A0, A1, 1, ms, mg, gn);
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const uint32_t o = gn != INV ? gn * (uint32_t)sizeof(NodeRec) + pl * 16u : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wst + pl * 64), 16, o, 0, 0, 0);
+  }
+
+  int em9 = 0;
+  for (int e = 1; e <= nmax; ++e) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): staged records, span starts
+    em9 = em9 == RING - 1 ? 0 : em9 + 1;
+    const int dmax = min(e, p.max_len);
+    const int cb = e & 1;
+    const bool act = ms < W;
+    const SegRec sr = seg[wv][cb][act ? ms : 0];
+    const uint32_t gn0 = gn;
+    Cand cur;
+    {
+      const uint4 q0 = wst[lane], q1 = wst[64 + lane], q2 = wst[128 + lane];
+      cur.word = q0.x; cur.morph = q0.y; cur.tag = q0.z; cur.mask = q0.w;
+      cur.pre = dbl(q1.x, q1.y); cur.f4 = dbl(q1.z, q1.w);
+      cur.f5 = dbl(q2.x, q2.y); cur.f6 = dbl(q2.z, q2.w);
+    }
+    const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
+    int bm0 = em9 - d0;
+    bm0 += bm0 < 0 ? RING : 0;
+    const int msr = act ? ms : 0;
+    const Hyp h0 = read_hyp(R[msr][act ? bm0 : 0]);
+    const bool skip0 = !act || ((h0.jmask & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));
+
+    // next position: span start prefetch (owner lanes), lane mapping, staged records
+    const int A3 = own ? ssp[min(e + 2, nw) * 8] : 0;
+    int ms1 = W, mg1 = 0;
+    uint32_t gn1 = INV;
+    if (e < nmax) map_position(e + 1, A1, A2, cb ^ 1, ms1, mg1, gn1);
+    __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      const uint32_t o = gn1 != INV ? gn1 * (uint32_t)sizeof(NodeRec) + pl * 16u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wst + pl * 64), 16, o, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    Probe<NARROW> P;
+    probe_issue<NARROW>(P, B, slots, seed, h0, cur,
+                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, nullptr);
+    asm volatile("" ::: "memory");
+    const Hyp h1 = read_hyp(R[msr][act ? bm0 : 0]);
+    double best_s = -INFINITY;
+    uint32_t best_g = INV;
+    if (!skip0) {
+      const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h1, cur, cnt) : 0.0;
+      if (COUNT) ++cnt.exp;
+      best_s = h1.score + increment(p, cur, tri, gn0);              // beam.py:115
+      best_g = (uint32_t)mg;
+    }
+    // folded segments (rare): this lane's further candidates g + L, g + 2L ...
+    if (act) {
+      for (int g = mg + (int)sr.L; g < (int)sr.X; g += (int)sr.L) {
+        const Cand c = load_cand(B, sr.nb + (uint32_t)g);
+        const int d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
+        int bm = em9 - d;
+        bm += bm < 0 ? RING : 0;
+        const Hyp h = read_hyp(R[msr][bm]);
+        if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;   // beam.py:43-45
+        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, nullptr) : 0.0;
+        if (COUNT) ++cnt.exp;
+        const double sc = h.score + increment(p, c, tri, sr.nb + (uint32_t)g);
+        if (better(sc, (uint32_t)g, best_s, best_g)) { best_s = sc; best_g = (uint32_t)g; }
+      }
+    }
+
+    // per-sentence argmax (beam.py:112-116): max score key, then min generation
+    const unsigned long long key = best_g != INV ? ord_key(best_s) : 0ull;
+    if (key) __hip_atomic_fetch_max(&amax[wv][cb][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const unsigned long long mk = key ? amax[wv][cb][msr] : 0ull;
+    const bool top = key && key == mk;
+    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], best_g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const uint32_t mgw = top ? amin[wv][cb][msr] : INV;
+    if (lane < W) {                              // reset the other parity for the next position
+      amax[wv][cb ^ 1][lane] = 0ull;
+      amin[wv][cb ^ 1][lane] = INV;
+    }
+    if (top && mgw == best_g) {                  // the winner writes beam[e]
+      Cand c = cur;
+      Hyp h = h1;
+      int d = d0;
+      if (best_g != (uint32_t)mg) {              // won with a folded candidate: reload
+        c = load_cand(B, sr.nb + best_g);
+        d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
+        int bm = em9 - d;
+        bm += bm < 0 ? RING : 0;
+        h = read_hyp(R[msr][bm]);
+      }
+      VEntry ne;
+      ne.score = best_s; ne.f6 = c.f6;
+      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
+      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
+      ne.depth = h.depth + 1;
+      R[msr][em9] = ne;
+      const uint32_t bpv = bp_pack(sr.a + best_g, (uint32_t)d, 0u);
+      const SentRec si = srec[wv][msr];
+      if (si.in_lds) bpl[wv][msr][e] = bpv;
+      else p.bp[(((int64_t)si.bp_hi << 32) | si.bp_lo) + (int64_t)e * bstride] = bpv;
+    }
+    __builtin_amdgcn_wave_barrier();
+    A0 = A1; A1 = A2; A2 = A3;
+    ms = ms1; mg = mg1; gn = gn1;
+  }
+
+  // matures = beam[n] + EOS (beam.py:59-61); backtrace, one owner lane per sentence
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  if (own) {
+    const VEntry& f = R[lane][nw % RING];
+    p.out_count[sid] = 1;
+    p.out_score[sid] = f.score + 0.0;
+    p.out_len[sid] = (int32_t)f.depth;
+    int32_t* codes = p.out_codes + p.cum_n[sid];
+    const bool in_lds = nw < BPL;
+    const uint32_t* bpg = p.bp + p.bp_off[sid];
+    int pos = nw;
+    for (int step = (int)f.depth - 1; step >= 0; --step) {
+      const uint32_t v = in_lds ? bpl[wv][lane][pos] : bpg[(int64_t)pos * bstride];
+      codes[step] = (int32_t)bp_node(v);
+      pos -= (int)bp_d(v);
+    }
+  }
+  if (COUNT) {
+    const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
+                             pb = group_sum<64>(cnt.probe);
+    if (lane == 0) {
+      atomicAdd(p.counters + 0, ex);
+      atomicAdd(p.counters + 1, tu);
+      atomicAdd(p.counters + 2, pb);
+    }
+  }
+}
+
 // ===========================================================================
 // beam_size 2..32
 // ===========================================================================
@@ -854,8 +1121,38 @@ lt_beam_k(DecodeParams p) {
   }
 }
 
+// k=1 kernel: packed lanes (default) or one 16-lane row per sentence
+// (LT_VITERBI=row16, kept for comparison).
+constexpr int P_W = 6;                  // sentences per wave, packed kernel
+
+static int viterbi_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("LT_VITERBI");
+    if (e && std::strcmp(e, "row16") == 0) return 0;
+    if (e && std::strcmp(e, "pk4") == 0) return 4;
+    if (e && std::strcmp(e, "pk8") == 0) return 8;
+    return P_W;
+  }();
+  return v;
+}
+
+template <int W, bool NARROW, bool COUNT>
+hipError_t launch_pk(const DecodeParams& p, hipStream_t st) {
+  constexpr int SPB = W * P_WPB;
+  const int blocks = (p.n_sent + SPB - 1) / SPB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((lt_viterbi_pk<W, NARROW, COUNT>), dim3(blocks), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
 template <bool NARROW, bool COUNT>
 hipError_t launch_v(const DecodeParams& p, hipStream_t st) {
+  switch (viterbi_variant()) {
+    case 4: return launch_pk<4, NARROW, COUNT>(p, st);
+    case 6: return launch_pk<6, NARROW, COUNT>(p, st);
+    case 8: return launch_pk<8, NARROW, COUNT>(p, st);
+    default: break;
+  }
   const int blocks = (p.n_sent + V_SPB - 1) / V_SPB;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((lt_viterbi_k<NARROW, COUNT>), dim3(blocks), dim3(256), 0, st, p);
