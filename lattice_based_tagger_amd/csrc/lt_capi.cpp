@@ -80,6 +80,8 @@ struct lt_model {
   uint32_t seed = 0;
   int narrow = 0;          // 16 B SlotN (all ids < 2^20) or 32 B SlotW
   std::vector<KeyRec> keys;  // host copy (narrow models): hot-table selection
+  double* d_d3 = nullptr;    // dense class-3 table or NULL
+  uint32_t d3mul = 0;
   uint64_t uid = 0;          // unique per created model (hot-table cache key)
 };
 
@@ -230,6 +232,45 @@ lt_status lt_sync(lt_ctx* c) {
 }
 
 // ---------------------------------------------------------------- model --
+// Dense class-3 table (see lt_common.h): the tag values of the class-3 keys,
+// a multiplier whose d3_index is injective on them, and the coefficient
+// array.  Left disabled (mul 0) when there are more than D3_DIM values, no
+// multiplier is found, or a coefficient collides with the absent marker.
+static void build_dense3(const std::vector<KeyRec>& keys, uint32_t& mul, std::vector<double>& tab) {
+  mul = 0;
+  std::vector<uint32_t> vals;
+  for (const KeyRec& k : keys)
+    if (k.cls == 3) {
+      vals.push_back(k.a);
+      vals.push_back(k.b);
+      uint64_t bits;
+      std::memcpy(&bits, &k.coef, 8);
+      if (bits == D3_ABSENT) return;
+    }
+  if (vals.empty()) return;
+  std::sort(vals.begin(), vals.end());
+  vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+  if (vals.size() > (size_t)D3_DIM) return;
+  uint32_t m = 0x9E3779B1u;
+  for (int trial = 0; trial < 20000 && !mul; ++trial, m = m * 0x2C1B3C6Du + 0x297A2D39u) {
+    const uint32_t cand = m | 1u;
+    uint64_t used = 0;
+    bool inj = true;
+    for (uint32_t v : vals) {
+      const uint64_t bit = 1ull << d3_index(v, cand);
+      if (used & bit) { inj = false; break; }
+      used |= bit;
+    }
+    if (inj) mul = cand;
+  }
+  if (!mul) return;
+  double absent;
+  std::memcpy(&absent, &D3_ABSENT, 8);
+  tab.assign((size_t)D3_DIM * D3_DIM, absent);
+  for (const KeyRec& k : keys)
+    if (k.cls == 3) tab[(size_t)d3_index(k.a, mul) * D3_DIM + d3_index(k.b, mul)] = k.coef;
+}
+
 lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
   if (!c || !d || !out) return fail(LT_EINVAL, "lt_model_create: NULL argument");
   *out = nullptr;
@@ -282,6 +323,9 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
     }
   }
   if (!ok) return fail(LT_EINVAL, "lt_model_create: cuckoo table build failed");
+  uint32_t d3mul = 0;
+  std::vector<double> d3;
+  build_dense3(keys, d3mul, d3);
   HIP_TRY(hipSetDevice(c->device));
   lt_model* m = new (std::nothrow) lt_model;
   if (!m) return fail(LT_ENOMEM, "lt_model_create: out of host memory");
@@ -296,9 +340,14 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
   if (e == hipSuccess)
     e = hipMemcpyAsync(m->d_table, narrow ? (const void*)tn.data() : (const void*)tw.data(),
                        (size_t)(slots * slot_bytes), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && d3mul) {
+    m->d3mul = d3mul;
+    e = dalloc_copy(&m->d_d3, d3.data(), d3.size(), c->stream);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     dfree(m->d_table);
+    dfree(m->d_d3);
     delete m;
     return fail(LT_EHIP, "lt_model_create: %s", hipGetErrorString(e));
   }
@@ -310,6 +359,7 @@ lt_status lt_model_destroy(lt_model* m) {
   if (!m) return LT_OK;
   (void)hipSetDevice(m->ctx->device);
   dfree(m->d_table);
+  dfree(m->d_d3);
   delete m;
   return LT_OK;
 }
@@ -573,6 +623,12 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   lt_status hs = build_hot(c, m, b);
   if (hs != LT_OK) return hs;
   p.hot = (b->hot_uid == m->uid) ? b->d_hot : nullptr;
+  static const bool d3_off = [] {
+    const char* v = std::getenv("LT_D3");
+    return v && v[0] == '0';
+  }();
+  p.d3 = d3_off ? nullptr : m->d_d3;
+  p.d3mul = m->d3mul;
   p.narrow = m->narrow;
   p.has_tri = b->has_tri;
   p.n_sent = b->n_sent;

@@ -108,6 +108,16 @@ constexpr int HOT_SLOTS = 1024;
 constexpr uint32_t HOT_SEED = 0x6A09E667u;
 LT_HD uint32_t hot_slot(KeyBase kb) { return mix1(kb.b1 ^ HOT_SEED) & (HOT_SLOTS - 1); }
 
+// Dense class-3 table: the (t_j, t_k) keys of a model whose class-3 tag values
+// are few (<= D3_DIM) live in a D3_DIM x D3_DIM coefficient array, indexed by
+// a multiplicative hash the library picks to be injective on those values.
+// The node pre-filter bits (J3A / K3B) guarantee both tags of a needed probe
+// are among them, so the slot needs no key check; absent pairs hold D3_ABSENT.
+constexpr int D3_BITS = 5;
+constexpr int D3_DIM = 1 << D3_BITS;
+constexpr uint64_t D3_ABSENT = 0x7FF5A5A55A5A0001ull;     // a NaN payload
+LT_HD uint32_t d3_index(uint32_t v, uint32_t mul) { return (v * mul) >> (32 - D3_BITS); }
+
 // Device node record (AoS, 48 B = 3 x 16 B loads), built by the library from
 // the SoA arrays of lt_batch_desc.
 struct alignas(16) NodeRec {

@@ -268,6 +268,14 @@ struct Probe {
   typename Tab<NARROW>::S s1[6], s2[6];   // the two cuckoo candidates (valid where needed)
   uint32_t need;                           // bit q: probe q is needed
   uint32_t gneed;                          // bit q: probe q went to the global table
+  uint32_t lpres;                          // bit q: resolved from LDS and present (coef in s1)
+};
+
+// LDS-resident parts of the model a block stages at its start.
+struct Aux {
+  const uint4* hot;       // hot-key table (HOT_SLOTS SlotN) or nullptr
+  const double* d3;       // dense class-3 table (D3_DIM^2) or nullptr
+  uint32_t d3mul;
 };
 
 // Key components of probe q for (h, c); recomputed where needed instead of
@@ -315,31 +323,63 @@ __device__ __forceinline__ uint32_t probe_need(const Hyp& h, const Cand& c) {
 // hot: the block's LDS copy of the batch hot table (HOT_SLOTS SlotN), or
 // nullptr.  A needed probe first reads its one hot slot; only a hot miss
 // issues the two global cuckoo loads.
+// Stage the LDS parts of the model (all threads of the block, before any
+// early exit): the hot table when `hotl` is given and the batch has one, and
+// the dense class-3 table when the model has one.
+template <bool NARROW>
+__device__ __forceinline__ Aux stage_aux(const DecodeParams& p, uint4* hotl, double* d3l) {
+  Aux a;
+  const bool use_hot = NARROW && hotl != nullptr && p.hot != nullptr;
+  if (use_hot) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.hot);
+    for (int i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) hotl[i] = src[i];
+  }
+  if (p.d3) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.d3);
+    uint4* dst = reinterpret_cast<uint4*>(d3l);
+    for (int i = threadIdx.x; i < D3_DIM * D3_DIM / 2; i += blockDim.x) dst[i] = src[i];
+  }
+  if (use_hot || p.d3) __syncthreads();
+  a.hot = use_hot ? hotl : nullptr;
+  a.d3 = p.d3 ? d3l : nullptr;
+  a.d3mul = p.d3mul;
+  return a;
+}
+
 template <bool NARROW>
 __device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uint32_t slots,
                                             uint32_t seed, const Hyp& h, const Cand& c,
-                                            uint32_t need, const uint4* hot) {
+                                            uint32_t need, const Aux& aux) {
   using T = Tab<NARROW>;
   P.need = need;
   const Keys K = make_keys(h, c, use_j8_of(h, c));
-  uint32_t gneed = need;
+  uint32_t gneed = need, lpres = 0;
+  if (aux.d3 && ((need >> 3) & 1u)) {        // class 3 from the dense LDS table
+    const double v = aux.d3[d3_index(h.jtag, aux.d3mul) * D3_DIM + d3_index(c.tag, aux.d3mul)];
+    P.s1[3].coef = v;
+    gneed &= ~8u;
+    lpres |= (__builtin_bit_cast(uint64_t, v) != D3_ABSENT) ? 8u : 0u;
+  }
   if constexpr (NARROW) {
-    if (hot) {
+    if (aux.hot) {
       // the hot slot is read into s1 (no extra registers); a hit keeps it
 #pragma unroll
       for (int q = 0; q < 6; ++q)
-        if ((need >> q) & 1u) {
-          const uint4 hv = hot[hot_slot(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]))];
+        if ((gneed >> q) & 1u) {
+          const uint4 hv = aux.hot[hot_slot(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]))];
           P.s1[q].key = ((uint64_t)hv.y << 32) | hv.x;
           P.s1[q].coef = __builtin_bit_cast(double, (u32x2){hv.z, hv.w});
         }
 #pragma unroll
       for (int q = 0; q < 6; ++q)
-        if (((need >> q) & 1u) && T::hit(P.s1[q], T::key(K.a[q], K.b[q], K.c[q], PCLS[q])))
+        if (((gneed >> q) & 1u) && T::hit(P.s1[q], T::key(K.a[q], K.b[q], K.c[q], PCLS[q]))) {
           gneed &= ~(1u << q);
+          lpres |= 1u << q;
+        }
     }
   }
   P.gneed = gneed;
+  P.lpres = lpres;
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     // exec-masked, not out-of-range: an OOB lane still costs the address
@@ -368,12 +408,15 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
   for (int q = 0; q < 6; ++q) {
     pr6[q] = false;
     cf[q] = 0.0;
-    if ((P.need >> q) & 1u) {
+    if ((P.gneed >> q) & 1u) {
       const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
-      const bool m1 = T::hit(P.s1[q], key);                // hot hits land in s1
-      const bool m2 = ((P.gneed >> q) & 1u) && T::hit(P.s2[q], key);
+      const bool m1 = T::hit(P.s1[q], key);
+      const bool m2 = T::hit(P.s2[q], key);
       pr6[q] = m1 || m2;
       cf[q] = m1 ? P.s1[q].coef : P.s2[q].coef;
+    } else if ((P.lpres >> q) & 1u) {          // resolved from LDS
+      pr6[q] = true;
+      cf[q] = P.s1[q].coef;
     }
   }
   double v[9];
@@ -398,9 +441,9 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
 template <bool NARROW, bool COUNT>
 __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_t seed,
                                           const Hyp& h, const Cand& c, Counts& cnt,
-                                          const uint4* hot) {
+                                          const Aux& aux) {
   Probe<NARROW> P;
-  probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c), hot);
+  probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c), aux);
   return probe_finish<NARROW, COUNT>(P, h, c, cnt);
 }
 
@@ -439,16 +482,8 @@ lt_viterbi_k(DecodeParams p) {
   __shared__ VEntry ring[V_SPB][RING];
   __shared__ uint32_t bpl[V_SPB][V_BP_LDS];
   __shared__ uint4 stg[4][3 * 64];             // per wave: 3 planes x 64 lanes x 16 B
-  __shared__ uint4 hotl[NARROW ? HOT_SLOTS : 1];
-
-  const bool use_hot = NARROW && p.hot != nullptr;
-  if (use_hot) {                                 // stage the batch hot table (all threads)
-    const uint4* src = reinterpret_cast<const uint4*>(p.hot);
-#pragma unroll
-    for (int i = 0; i < HOT_SLOTS / 256; ++i) hotl[i * 256 + threadIdx.x] = src[i * 256 + threadIdx.x];
-    __syncthreads();
-  }
-  const uint4* hot = use_hot ? hotl : nullptr;
+  __shared__ double d3l[D3_DIM * D3_DIM];
+  const Aux aux = stage_aux<NARROW>(p, nullptr, d3l);
 
   const int grp = threadIdx.x / V_G;
   const int gl = threadIdx.x % V_G;
@@ -510,14 +545,16 @@ lt_viterbi_k(DecodeParams p) {
     // record goes straight to LDS by DMA once `cur` has been read out of it; a
     // node past the batch end reads as zeros).  Issued ahead of the probes.
     int A2 = ssp[min(e + 1, n) * 8];
-    __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): cur is out of the staging area
-    dma_block<V_G>(B, nbase + (uint32_t)A1, e < n, wst, gl);
-    __builtin_amdgcn_sched_barrier(0);
 
     // probes of candidate gl (unneeded ones read nothing)
     Probe<NARROW> P;
     probe_issue<NARROW>(P, B, slots, seed, h0, cur,
-                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, hot);
+                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, aux);
+    // DMA after the probes' own LDS reads (an LDS read behind a DMA waits for it)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): cur is out of the staging area
+    dma_block<V_G>(B, nbase + (uint32_t)A1, e < n, wst, gl);
+    __builtin_amdgcn_sched_barrier(0);
     // re-read the hypothesis from LDS instead of holding it in VGPRs across
     // the probe wait (the compiler barrier stops the reload being merged)
     asm volatile("" ::: "memory");
@@ -536,7 +573,7 @@ lt_viterbi_k(DecodeParams p) {
       bm += bm < 0 ? RING : 0;
       const Hyp h = read_hyp(R[bm]);
       if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;   // beam.py:43-45
-      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, hot) : 0.0;
+      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, aux) : 0.0;
       if (COUNT) ++cnt.exp;
       const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)(A0 + g));
       if (better(sc, (uint32_t)g, best_s, best_g)) { best_s = sc; best_g = (uint32_t)g; }
@@ -612,6 +649,24 @@ lt_viterbi_k(DecodeParams p) {
 // ---------------------------------------------------------------------------
 constexpr int P_WPB = 4;                // waves per block
 
+// Stage the records of the wave's packed candidates (lane l's node gn, INV =
+// none) into wave_planes: the 3 x 64 chunks of 16 B form one stream in lane
+// order, and DMA instruction pl has lane t fetch chunk 64*pl + t -- the part
+// (c mod 3) of lane (c / 3)'s record -- so consecutive lanes read consecutive
+// bytes of a sentence's node block.  Lane l's record ends up at chunks
+// 3l .. 3l+2.
+__device__ __forceinline__ void dma_packed(const Bufs& B, uint32_t gn, uint4* wave_planes, int lane) {
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const uint32_t c = (uint32_t)(64 * pl + lane);
+    const uint32_t j = (c * 171u) >> 9;           // c / 3 for c < 192
+    const uint32_t part = c - 3u * j;
+    const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)gn);
+    const uint32_t o = nj != INV ? nj * (uint32_t)sizeof(NodeRec) + part * 16u : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wave_planes + pl * 64), 16, o, 0, 0, 0);
+  }
+}
+
 __device__ __forceinline__ unsigned long long ord_key(double sc) {
   const uint64_t b = __builtin_bit_cast(uint64_t, sc + 0.0);      // -0.0 -> +0.0
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
@@ -630,7 +685,7 @@ struct alignas(16) SentRec {
 template <int W, bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
 lt_viterbi_pk(DecodeParams p) {
-  constexpr int BPL = W <= 6 ? 256 : 128;       // end positions whose backpointer stays in LDS
+  constexpr int BPL = W <= 4 ? 256 : 128;       // end positions whose backpointer stays in LDS
   __shared__ VEntry ring[P_WPB][W][RING];
   __shared__ uint32_t bpl[P_WPB][W][BPL];
   __shared__ uint4 stg[P_WPB][3 * 64];
@@ -638,6 +693,8 @@ lt_viterbi_pk(DecodeParams p) {
   __shared__ SentRec srec[P_WPB][W];
   __shared__ unsigned long long amax[P_WPB][2][W];
   __shared__ uint32_t amin[P_WPB][2][W];
+  __shared__ double d3l[D3_DIM * D3_DIM];
+  const Aux aux = stage_aux<NARROW>(p, nullptr, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
@@ -725,11 +782,7 @@ lt_viterbi_pk(DecodeParams p) {
   int ms, mg;
   uint32_t gn;
   map_position(1, A0, A1, 1, ms, mg, gn);
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {
-    const uint32_t o = gn != INV ? gn * (uint32_t)sizeof(NodeRec) + pl * 16u : OOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wst + pl * 64), 16, o, 0, 0, 0);
-  }
+  dma_packed(B, gn, wst, lane);
 
   int em9 = 0;
   for (int e = 1; e <= nmax; ++e) {
@@ -742,7 +795,7 @@ lt_viterbi_pk(DecodeParams p) {
     const uint32_t gn0 = gn;
     Cand cur;
     {
-      const uint4 q0 = wst[lane], q1 = wst[64 + lane], q2 = wst[128 + lane];
+      const uint4 q0 = wst[3 * lane], q1 = wst[3 * lane + 1], q2 = wst[3 * lane + 2];
       cur.word = q0.x; cur.morph = q0.y; cur.tag = q0.z; cur.mask = q0.w;
       cur.pre = dbl(q1.x, q1.y); cur.f4 = dbl(q1.z, q1.w);
       cur.f5 = dbl(q2.x, q2.y); cur.f6 = dbl(q2.z, q2.w);
@@ -759,17 +812,17 @@ lt_viterbi_pk(DecodeParams p) {
     int ms1 = W, mg1 = 0;
     uint32_t gn1 = INV;
     if (e < nmax) map_position(e + 1, A1, A2, cb ^ 1, ms1, mg1, gn1);
-    __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
-      const uint32_t o = gn1 != INV ? gn1 * (uint32_t)sizeof(NodeRec) + pl * 16u : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wst + pl * 64), 16, o, 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
 
     Probe<NARROW> P;
     probe_issue<NARROW>(P, B, slots, seed, h0, cur,
-                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, nullptr);
+                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, aux);
+    // the next position's records are DMA'd only now: an LDS read issued
+    // after a buffer->LDS DMA waits for it (vmcnt), so the probes' own LDS
+    // reads (dense class-3 table) must come first
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
+    dma_packed(B, gn1, wst, lane);
+    __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     const Hyp h1 = read_hyp(R[msr][act ? bm0 : 0]);
     double best_s = -INFINITY;
@@ -789,7 +842,7 @@ lt_viterbi_pk(DecodeParams p) {
         bm += bm < 0 ? RING : 0;
         const Hyp h = read_hyp(R[msr][bm]);
         if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;   // beam.py:43-45
-        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, nullptr) : 0.0;
+        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, aux) : 0.0;
         if (COUNT) ++cnt.exp;
         const double sc = h.score + increment(p, c, tri, sr.nb + (uint32_t)g);
         if (better(sc, (uint32_t)g, best_s, best_g)) { best_s = sc; best_g = (uint32_t)g; }
@@ -954,6 +1007,11 @@ lt_beam_k(DecodeParams p) {
   __shared__ Entry ring[SPB][RING][KT];
   __shared__ int32_t cntl[SPB][RING];
   __shared__ uint4 stg[2][4][3 * 64];        // [position parity][wave][plane x lane]
+  // the dense class-3 table only where its 8 KiB does not cost a block per CU
+  constexpr bool USE_D3 = KT <= 8;
+  __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
+  Aux aux{nullptr, nullptr, 0u};
+  if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
 
   const int grp = threadIdx.x / G;
   const int gl = threadIdx.x % G;
@@ -1034,7 +1092,7 @@ lt_beam_k(DecodeParams p) {
         const Hyp h = read_entry(R[(e - x.d) % RING][x.r]);
         // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
         if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (x.d < dmax)) continue;
-        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, nullptr) : 0.0;
+        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, aux) : 0.0;
         const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
         if (COUNT) ++cnt.exp;
         list_insert<LCAP + 1>(ls, lg, sc, (uint32_t)g);

@@ -12,6 +12,8 @@ struct DecodeParams {
   uint32_t slots;
   uint32_t seed;
   const SlotN* hot;             // HOT_SLOTS-slot LDS hot table (narrow only) or NULL
+  const double* d3;             // dense class-3 table (D3_DIM^2) or NULL
+  uint32_t d3mul;
   int32_t narrow;               // 1: SlotN, 0: SlotW
   int32_t has_tri;
   // batch (device pointers)

@@ -9,7 +9,12 @@ if [ -z "$NOTEST" ]; then
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
 fi
+# a variant is LT_VITERBI[+nod3][+hot][+kN]
 for V in ${VARIANTS:-row16 pk6}; do
-LT_VITERBI=$V timeout -k 10 600 python3 -u bench.py --steps 10 --warmup 2 --k 1 --no-cpu-baseline > gpurun_out/bench_v_$V.log 2>&1 || { echo BENCH_FAIL $V; tail -30 gpurun_out/bench_v_$V.log; exit 1; }
+VK=${V%%+*}; D3=1; HOT=0; KK=1
+case "$V" in *+nod3*) D3=0;; esac
+case "$V" in *+hot*) HOT=1;; esac
+case "$V" in *+k*) KK=${V##*+k};; esac
+LT_D3=$D3 LT_HOT=$HOT LT_VITERBI=$VK timeout -k 10 600 python3 -u bench.py --steps 10 --warmup 2 --k $KK --no-cpu-baseline > gpurun_out/bench_v_$V.log 2>&1 || { echo BENCH_FAIL $V; tail -30 gpurun_out/bench_v_$V.log; exit 1; }
 python3 -c "import json;d=json.loads(open('gpurun_out/bench_v_$V.log').read().strip().splitlines()[-1]);print('$V', round(d['value']), 'sents/s kernel_ms', round(d['roofline']['avg_kernel_ms'],3), 'frac', round(d['roofline']['frac'],4))"
 done
