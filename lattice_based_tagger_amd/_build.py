@@ -32,31 +32,39 @@ def _stale(target, deps):
     return any(os.path.getmtime(dp) > t for dp in deps)
 
 
-def build(force=False, verbose=True):
-    """Compile liblt.so if any source is newer than it.  Returns its path."""
+def build(force=False, verbose=True, defines=(), out=None):
+    """Compile liblt.so if any source is newer than it.  Returns its path.
+    ``defines``/``out``: an experiment build (e.g. ``('PK_WAVES=3',)``) to
+    another file, selected at run time with LT_LIBRARY."""
     os.makedirs(LIBDIR, exist_ok=True)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [__file__]
-    if not force and not _stale(LIB, deps):
-        return LIB
+    lib = out or LIB
+    if not force and not _stale(lib, deps):
+        return lib
     objs = []
     for src in SOURCES:
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + '.o')
-        cmd = [HIPCC, '--offload-arch=' + ARCH] + COMMON_FLAGS + ['-c', os.path.join(CSRC, src), '-o', obj]
+        cmd = [HIPCC, '--offload-arch=' + ARCH] + COMMON_FLAGS + ['-D' + d for d in defines] + [
+            '-c', os.path.join(CSRC, src), '-o', obj]
         if verbose:
             print(' '.join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + '.tmp'
+    tmp = lib + '.tmp'
     cmd = [HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', tmp] + objs + [
         '-Wl,-rpath,' + os.path.join(ROCM, 'lib'), '-Wl,--no-undefined']
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv)
+    # python -m lattice_based_tagger_amd._build [--force] [-DNAME=V ... -o OUT]
+    args = sys.argv[1:]
+    defs = [a[2:] for a in args if a.startswith('-D')]
+    out = args[args.index('-o') + 1] if '-o' in args else None
+    build(force='--force' in args or bool(defs), defines=defs, out=out)

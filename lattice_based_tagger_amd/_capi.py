@@ -59,7 +59,8 @@ def load(path=None):
     with _lock:
         if _lib is not None:
             return _lib
-        path = path or LIB
+        # LT_LIBRARY: an alternative in-tree build (kernel A/B experiments)
+        path = path or os.environ.get('LT_LIBRARY') or LIB
         if not os.path.exists(path):
             raise RuntimeError('liblt.so not built (%s); run __graft_entry__.build()' % path)
         lib = C.CDLL(path)

@@ -647,6 +647,12 @@ lt_viterbi_k(DecodeParams p) {
 // LDS min over the generation index among the lanes holding the maximum --
 // exactly the reference's (score desc, generation asc) order.
 // ---------------------------------------------------------------------------
+#ifndef PK_WAVES
+#define PK_WAVES 4
+#endif
+#ifndef PK_BPL
+#define PK_BPL 64
+#endif
 constexpr int P_WPB = 4;                // waves per block
 
 // Stage the records of the wave's packed candidates (lane l's node gn, INV =
@@ -656,13 +662,17 @@ constexpr int P_WPB = 4;                // waves per block
 // bytes of a sentence's node block.  Lane l's record ends up at chunks
 // 3l .. 3l+2.
 __device__ __forceinline__ void dma_packed(const Bufs& B, uint32_t gn, uint4* wave_planes, int lane) {
+  uint32_t nj[3], part[3];
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {
+  for (int pl = 0; pl < 3; ++pl) {               // all three permutes first: one LDS round trip
     const uint32_t c = (uint32_t)(64 * pl + lane);
     const uint32_t j = (c * 171u) >> 9;           // c / 3 for c < 192
-    const uint32_t part = c - 3u * j;
-    const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)gn);
-    const uint32_t o = nj != INV ? nj * (uint32_t)sizeof(NodeRec) + part * 16u : OOB;
+    part[pl] = c - 3u * j;
+    nj[pl] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)gn);
+  }
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const uint32_t o = nj[pl] != INV ? nj[pl] * (uint32_t)sizeof(NodeRec) + part[pl] * 16u : OOB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wave_planes + pl * 64), 16, o, 0, 0, 0);
   }
 }
@@ -673,9 +683,9 @@ __device__ __forceinline__ unsigned long long ord_key(double sc) {
 }
 
 // per-sentence record of one end position (LDS): first candidate (global
-// node index), lanes in the segment, candidates, first candidate (local)
+// node index), candidates, first candidate (local index)
 struct alignas(16) SegRec {
-  uint32_t nb, L, X, a;
+  uint32_t nb, X, a, pad;
 };
 // per-sentence static record (LDS)
 struct alignas(16) SentRec {
@@ -683,9 +693,9 @@ struct alignas(16) SentRec {
 };
 
 template <int W, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+__global__ void __launch_bounds__(256, NARROW ? PK_WAVES : 3)
 lt_viterbi_pk(DecodeParams p) {
-  constexpr int BPL = W <= 4 ? 256 : 128;       // end positions whose backpointer stays in LDS
+  constexpr int BPL = PK_BPL;                   // end positions whose backpointer stays in LDS
   __shared__ VEntry ring[P_WPB][W][RING];
   __shared__ uint32_t bpl[P_WPB][W][BPL];
   __shared__ uint4 stg[P_WPB][3 * 64];
@@ -718,7 +728,7 @@ lt_viterbi_pk(DecodeParams p) {
     const int64_t bo = p.bp_off[sid];
     SentRec r;
     r.n = (uint32_t)nw; r.bp_lo = (uint32_t)bo; r.bp_hi = (uint32_t)(bo >> 32);
-    r.in_lds = nw < BPL ? 1u : 0u;
+    r.in_lds = 0u;
     srec[wv][lane] = r;
     const Cand b0 = load_cand(B, nbase);       // beam[0] = [BOS] (beam.py:21-23)
     VEntry e0;
@@ -740,60 +750,50 @@ lt_viterbi_pk(DecodeParams p) {
   int A1 = own ? ssp[min(1, nw) * 8] : 0;
   int A2 = own ? ssp[min(2, nw) * 8] : 0;
 
-  // lane mapping of end position e from (A_e, A_{e+1}) of every sentence:
-  // writes seg[buf][w], returns this lane's sentence (W = idle) and first
-  // candidate, and the candidate's global node index.
-  auto map_position = [&](int e, int Ae, int Ae1, int buf, int& ms, int& mg, uint32_t& gnode) {
+  // Lanes of round r of end position e: the candidates of the W sentences
+  // form one list in sentence order (sentence w: X_w = A_{e+1} - A_e of
+  // them, generation order within); round r covers entries [64r, 64r + 64).
+  // `fresh` writes the sentences' records seg[buf][w] (first round of e).
+  // Returns the list length T; sets this lane's sentence (W = idle),
+  // candidate index and global node (INV = none).
+  auto map_round = [&](int e, int r, int Ae, int Ae1, int buf, bool fresh, int& ms, int& mg,
+                       uint32_t& gnode) -> int {
     const int X = (lane < W && e <= nw) ? Ae1 - Ae : 0;
-    int Xs[W];
-    int T = 0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) { Xs[w] = __builtin_amdgcn_readlane(X, w); T += Xs[w]; }
-    int Ls[W];
-    if (T <= 64) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) Ls[w] = Xs[w];
-    } else {                                    // rare: fold each segment
-      const int c = (T + (64 - W) - 1) / (64 - W);
-#pragma unroll
-      for (int w = 0; w < W; ++w) Ls[w] = (Xs[w] + c - 1) / c;
-    }
-    int sidx = 0, pst = 0, run = 0;
+    const int f = 64 * r + lane;
+    int run = 0, sidx = 0, pst = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
-      run += Ls[w];
-      if (lane >= run) { sidx = w + 1; pst = run; }
+      run += __builtin_amdgcn_readlane(X, w);
+      if (f >= run) { sidx = w + 1; pst = run; }
     }
-    if (lane < W) {
-      int myL = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) myL = (lane == w) ? Ls[w] : myL;
-      SegRec r;
-      r.nb = nbase + (uint32_t)Ae; r.L = (uint32_t)myL; r.X = (uint32_t)X; r.a = (uint32_t)Ae;
-      seg[wv][buf][lane] = r;
+    if (fresh && lane < W) {
+      SegRec rec;
+      rec.nb = nbase + (uint32_t)Ae; rec.X = (uint32_t)X; rec.a = (uint32_t)Ae; rec.pad = 0u;
+      seg[wv][buf][lane] = rec;
     }
     ms = sidx;
-    mg = lane - pst;
-    __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): seg written
-    const SegRec r = seg[wv][buf][sidx < W ? sidx : 0];
-    gnode = sidx < W ? r.nb + (uint32_t)mg : INV;
+    mg = f - pst;
+    const SegRec rr = seg[wv][buf][sidx < W ? sidx : 0];   // in order behind the write above
+    gnode = sidx < W ? rr.nb + (uint32_t)mg : INV;
+    return run;
   };
 
   int ms, mg;
   uint32_t gn;
-  map_position(1, A0, A1, 1, ms, mg, gn);
+  int rounds = (map_round(1, 0, A0, A1, 1, true, ms, mg, gn) + 63) >> 6;
   dma_packed(B, gn, wst, lane);
 
-  int em9 = 0;
-  for (int e = 1; e <= nmax; ++e) {
+  // macro-steps (e, r): round r of end position e
+  int e = 1, r = 0, em9 = 1;
+  while (e <= nmax) {
     __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): staged records, span starts
-    em9 = em9 == RING - 1 ? 0 : em9 + 1;
     const int dmax = min(e, p.max_len);
     const int cb = e & 1;
     const bool act = ms < W;
-    const SegRec sr = seg[wv][cb][act ? ms : 0];
+    const int msr = act ? ms : 0;
+    const SegRec sr = seg[wv][cb][msr];
     const uint32_t gn0 = gn;
-    Cand cur;
+    Cand cur;                                    // this lane's staged candidate
     {
       const uint4 q0 = wst[3 * lane], q1 = wst[3 * lane + 1], q2 = wst[3 * lane + 2];
       cur.word = q0.x; cur.morph = q0.y; cur.tag = q0.z; cur.mask = q0.w;
@@ -803,20 +803,27 @@ lt_viterbi_pk(DecodeParams p) {
     const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
     int bm0 = em9 - d0;
     bm0 += bm0 < 0 ? RING : 0;
-    const int msr = act ? ms : 0;
     const Hyp h0 = read_hyp(R[msr][act ? bm0 : 0]);
-    const bool skip0 = !act || ((h0.jmask & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));
+    const bool skip0 = !act || ((h0.jmask & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));   // beam.py:43-45
 
-    // next position: span start prefetch (owner lanes), lane mapping, staged records
-    const int A3 = own ? ssp[min(e + 2, nw) * 8] : 0;
-    int ms1 = W, mg1 = 0;
+    // next macro-step: another round of e, or round 0 of e + 1 (then also the
+    // span start two positions ahead for the owner lanes)
+    const bool last = r + 1 >= rounds;
+    int ms1 = W, mg1 = 0, nrounds = rounds;
     uint32_t gn1 = INV;
-    if (e < nmax) map_position(e + 1, A1, A2, cb ^ 1, ms1, mg1, gn1);
+    // (loaded on every round: a conditional load would make its value a phi,
+    // and the copy at the join would wait for the load right away)
+    const int A3 = own ? ssp[min(e + 2, nw) * 8] : 0;
+    if (last) {
+      if (e < nmax) nrounds = (map_round(e + 1, 0, A1, A2, cb ^ 1, true, ms1, mg1, gn1) + 63) >> 6;
+    } else {
+      map_round(e, r + 1, A0, A1, cb, false, ms1, mg1, gn1);
+    }
 
     Probe<NARROW> P;
     probe_issue<NARROW>(P, B, slots, seed, h0, cur,
                         (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, aux);
-    // the next position's records are DMA'd only now: an LDS read issued
+    // the next macro-step's records are DMA'd only now: an LDS read issued
     // after a buffer->LDS DMA waits for it (vmcnt), so the probes' own LDS
     // reads (dense class-3 table) must come first
     __builtin_amdgcn_sched_barrier(0);
@@ -826,66 +833,55 @@ lt_viterbi_pk(DecodeParams p) {
     asm volatile("" ::: "memory");
     const Hyp h1 = read_hyp(R[msr][act ? bm0 : 0]);
     double best_s = -INFINITY;
-    uint32_t best_g = INV;
     if (!skip0) {
       const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h1, cur, cnt) : 0.0;
       if (COUNT) ++cnt.exp;
       best_s = h1.score + increment(p, cur, tri, gn0);              // beam.py:115
-      best_g = (uint32_t)mg;
-    }
-    // folded segments (rare): this lane's further candidates g + L, g + 2L ...
-    if (act) {
-      for (int g = mg + (int)sr.L; g < (int)sr.X; g += (int)sr.L) {
-        const Cand c = load_cand(B, sr.nb + (uint32_t)g);
-        const int d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
-        int bm = em9 - d;
-        bm += bm < 0 ? RING : 0;
-        const Hyp h = read_hyp(R[msr][bm]);
-        if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;   // beam.py:43-45
-        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, aux) : 0.0;
-        if (COUNT) ++cnt.exp;
-        const double sc = h.score + increment(p, c, tri, sr.nb + (uint32_t)g);
-        if (better(sc, (uint32_t)g, best_s, best_g)) { best_s = sc; best_g = (uint32_t)g; }
-      }
     }
 
-    // per-sentence argmax (beam.py:112-116): max score key, then min generation
-    const unsigned long long key = best_g != INV ? ord_key(best_s) : 0ull;
+    // per-sentence argmax over the rounds of e (beam.py:112-116): max score
+    // key, then min generation index among the maxima.  A wave's LDS
+    // operations complete in order, so each read sees the updates issued
+    // before it.  A round that raises a sentence's maximum discards the
+    // earlier rounds' minimum (it belonged to a smaller key); ties with an
+    // earlier round keep it (earlier rounds hold smaller indices).
+    const unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
+    const unsigned long long mprev = (key && r > 0) ? amax[wv][cb][msr] : 0ull;
     if (key) __hip_atomic_fetch_max(&amax[wv][cb][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
     const unsigned long long mk = key ? amax[wv][cb][msr] : 0ull;
     const bool top = key && key == mk;
-    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], best_g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (top && mk != mprev) amin[wv][cb][msr] = INV;
+    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], (uint32_t)mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t mgw = top ? amin[wv][cb][msr] : INV;
     if (lane < W) {                              // reset the other parity for the next position
       amax[wv][cb ^ 1][lane] = 0ull;
       amin[wv][cb ^ 1][lane] = INV;
     }
-    if (top && mgw == best_g) {                  // the winner writes beam[e]
-      Cand c = cur;
-      Hyp h = h1;
-      int d = d0;
-      if (best_g != (uint32_t)mg) {              // won with a folded candidate: reload
-        c = load_cand(B, sr.nb + best_g);
-        d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
-        int bm = em9 - d;
-        bm += bm < 0 ? RING : 0;
-        h = read_hyp(R[msr][bm]);
-      }
+    if (top && mgw == (uint32_t)mg) {            // the (round's) winner writes beam[e]
       VEntry ne;
-      ne.score = best_s; ne.f6 = c.f6;
-      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
-      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
-      ne.depth = h.depth + 1;
+      ne.score = best_s; ne.f6 = cur.f6;
+      ne.jword = cur.word; ne.jmorph = cur.morph; ne.jtag = cur.tag; ne.jmask = cur.mask;
+      ne.iword = h1.jword; ne.imorph = h1.jmorph; ne.imask = h1.jmask | F_WI;
+      ne.depth = h1.depth + 1;
       R[msr][em9] = ne;
-      const uint32_t bpv = bp_pack(sr.a + best_g, (uint32_t)d, 0u);
-      const SentRec si = srec[wv][msr];
-      if (si.in_lds) bpl[wv][msr][e] = bpv;
-      else p.bp[(((int64_t)si.bp_hi << 32) | si.bp_lo) + (int64_t)e * bstride] = bpv;
+      const uint32_t bpv = bp_pack(sr.a + (uint32_t)mg, (uint32_t)d0, 0u);
+      if (e < BPL) {
+        bpl[wv][msr][e] = bpv;
+      } else {                                   // positions past the LDS window (long sentences)
+        const SentRec si = srec[wv][msr];
+        p.bp[(((int64_t)si.bp_hi << 32) | si.bp_lo) + (int64_t)e * bstride] = bpv;
+      }
     }
     __builtin_amdgcn_wave_barrier();
-    A0 = A1; A1 = A2; A2 = A3;
+    if (last) {
+      A0 = A1; A1 = A2; A2 = A3;
+      ++e;
+      r = 0;
+      em9 = em9 == RING - 1 ? 0 : em9 + 1;
+      rounds = nrounds;
+    } else {
+      ++r;
+    }
     ms = ms1; mg = mg1; gn = gn1;
   }
 
@@ -897,11 +893,10 @@ lt_viterbi_pk(DecodeParams p) {
     p.out_score[sid] = f.score + 0.0;
     p.out_len[sid] = (int32_t)f.depth;
     int32_t* codes = p.out_codes + p.cum_n[sid];
-    const bool in_lds = nw < BPL;
     const uint32_t* bpg = p.bp + p.bp_off[sid];
     int pos = nw;
     for (int step = (int)f.depth - 1; step >= 0; --step) {
-      const uint32_t v = in_lds ? bpl[wv][lane][pos] : bpg[(int64_t)pos * bstride];
+      const uint32_t v = pos < BPL ? bpl[wv][lane][pos] : bpg[(int64_t)pos * bstride];
       codes[step] = (int32_t)bp_node(v);
       pos -= (int)bp_d(v);
     }
@@ -1189,6 +1184,8 @@ static int viterbi_variant() {
     if (e && std::strcmp(e, "row16") == 0) return 0;
     if (e && std::strcmp(e, "pk4") == 0) return 4;
     if (e && std::strcmp(e, "pk8") == 0) return 8;
+    if (e && std::strcmp(e, "pk5") == 0) return 5;
+    if (e && std::strcmp(e, "pk7") == 0) return 7;
     return P_W;
   }();
   return v;
@@ -1207,7 +1204,9 @@ template <bool NARROW, bool COUNT>
 hipError_t launch_v(const DecodeParams& p, hipStream_t st) {
   switch (viterbi_variant()) {
     case 4: return launch_pk<4, NARROW, COUNT>(p, st);
+    case 5: return launch_pk<5, NARROW, COUNT>(p, st);
     case 6: return launch_pk<6, NARROW, COUNT>(p, st);
+    case 7: return launch_pk<7, NARROW, COUNT>(p, st);
     case 8: return launch_pk<8, NARROW, COUNT>(p, st);
     default: break;
   }

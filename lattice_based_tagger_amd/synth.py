@@ -75,7 +75,8 @@ def _zipf_ids(rng, size, vocab, a):
     return (np.searchsorted(cdf, rng.random(size)) + 1).astype(np.int32)
 
 
-def make_lattices(n_sent, seed=0, eojeols=20, eojeol_len=(2, 5), vocab=200_000, zipf_a=1.1):
+def make_lattices(n_sent, seed=0, eojeols=20, eojeol_len=(2, 5), vocab=200_000, zipf_a=1.1,
+                  extra_lambda=EXTRA_LAMBDA, dup_rate=DUP_RATE):
     rng = np.random.default_rng(seed)
     S = int(n_sent)
     elen = rng.integers(eojeol_len[0], eojeol_len[1] + 1, size=(S, eojeols), dtype=np.int32)
@@ -96,7 +97,7 @@ def make_lattices(n_sent, seed=0, eojeols=20, eojeol_len=(2, 5), vocab=200_000, 
     dd = np.arange(1, MAX_SPAN + 1, dtype=np.int32)[None, :]
     valid = dd <= remain
     nonempty = (rng.random((T, MAX_SPAN)) < SPAN_P[None, :]) & valid
-    cnt = np.where(nonempty, 1 + rng.poisson(EXTRA_LAMBDA, size=(T, MAX_SPAN)), 0).astype(np.int32)
+    cnt = np.where(nonempty, 1 + rng.poisson(extra_lambda, size=(T, MAX_SPAN)), 0).astype(np.int32)
 
     N = int(cnt.sum())
     flat = np.repeat(np.arange(T * MAX_SPAN, dtype=np.int64), cnt.ravel())
@@ -113,7 +114,7 @@ def make_lattices(n_sent, seed=0, eojeols=20, eojeol_len=(2, 5), vocab=200_000, 
                       rng.integers(1, 10, size=N, dtype=np.int32), node_d).astype(np.int32)
     is_l = starts[node_char].astype(np.int8)
     # exact duplicates of the span's first candidate
-    dup = (idx_in_span > 0) & (rng.random(N) < DUP_RATE)
+    dup = (idx_in_span > 0) & (rng.random(N) < dup_rate)
     first = span_first[flat]
     for arr in (word, morph, tag, length):
         arr[dup] = arr[first[dup]]

@@ -54,8 +54,8 @@ def test_single_sentence_drop_in(gpu_decoder):
     assert [float(x.score).hex() for x in m] == [e[1] for e in exp]
 
 
-def _synthetic(n_sent, seed, n_features):
-    raw = synth.make_lattices(n_sent, seed=seed)
+def _synthetic(n_sent, seed, n_features, **kw):
+    raw = synth.make_lattices(n_sent, seed=seed, **kw)
     lay = synth.layout(raw)
     cols = synth.node_columns(raw, lay)
     sm = synth.make_model(raw, lay, cols, seed=seed, n_features=n_features)
@@ -81,6 +81,25 @@ def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
     assert np.array_equal(count, o_count)
     assert np.array_equal(length, o_len)
     assert np.array_equal(score.view(np.uint64), o_score.view(np.uint64))   # 0 ULP
+    assert np.array_equal(codes, o_codes)
+    assert (ex, tu) == (o_ex, o_tu)
+
+
+@pytest.mark.parametrize('k', [1, 5])
+def test_dense_lattices_with_ties_match_c_oracle(gpu_decoder, k):
+    """Dense lattices (about 30 candidates per end position, half of the extra
+    ones exact duplicates of the span's first candidate, hence score ties):
+    the k=1 kernel packs more candidates than lanes into several rounds per
+    position with sentences straddling rounds; the beam kernel runs several
+    chunks per position.  Bit-exact against the C restatement."""
+    packed, keys, coefs = _synthetic(4096 if k == 1 else 1024, seed=300 + k, n_features=200_000,
+                                     eojeols=6, extra_lambda=3.0, dup_rate=0.5)
+    (count, length, score, codes), (ex, tu, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
+    o_count, o_len, o_score, o_codes, o_ex, o_tu = lt_oracle.decode(packed, keys, coefs, k,
+                                                                    nthreads=16)
+    assert np.array_equal(count, o_count)
+    assert np.array_equal(length, o_len)
+    assert np.array_equal(score.view(np.uint64), o_score.view(np.uint64))
     assert np.array_equal(codes, o_codes)
     assert (ex, tu) == (o_ex, o_tu)
 
