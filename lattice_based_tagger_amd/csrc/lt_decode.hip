@@ -1200,6 +1200,336 @@ hipError_t launch_pk(const DecodeParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// beam_size 2..32, one sentence per wave.  The expansions of end position e
+// (beam.py:27-58: spans j, hypothesis ranks r, candidates i, in generation
+// order g) are scored in rounds of 64 lanes; each lane keeps only the
+// expansion's order key and index in LDS.  Top-k (stable sort by score, [:k],
+// beam.py:85) is exact rank counting: the rank of an entry is the number of
+// entries with a larger key, or an equal key and a smaller index.  A position
+// with more expansions than a chunk carries its running top-k into the next
+// chunk's ranking.  Only the k winners are materialised into beam[e].
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double ord_score(unsigned long long k) {
+  const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return __builtin_bit_cast(double, b);
+}
+
+template <int KT, int WPB, bool NARROW, bool COUNT>
+__global__ void __launch_bounds__(64 * WPB)
+lt_beam_pk(DecodeParams p) {
+  constexpr int RPC = KT <= 16 ? 2 : 4;         // scoring rounds per chunk
+  constexpr int CH = 64 * RPC;                  // expansions per chunk
+  constexpr int KTP = KT < 4 ? 4 : KT;          // running-list room (multiple of 4)
+  constexpr int LN = KTP + CH;                  // ranked list: running top-k + chunk
+  static_assert(KTP % 4 == 0, "list alignment");
+  constexpr int STAGE = 64;                     // candidate records staged per position
+  __shared__ Entry ring[WPB][RING][KT];
+  __shared__ int32_t cntl[WPB][RING];
+  __shared__ uint4 stg[2][WPB][3 * 64];         // [position parity][wave]
+  __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][LN];
+  __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][LN];
+  __shared__ unsigned long long tkey[WPB][KT];
+  __shared__ uint32_t tgen[WPB][KT];
+  constexpr bool USE_D3 = KT <= 4;              // (its 8 KiB would cost a block per CU above)
+  __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
+  Aux aux{nullptr, nullptr, 0u};
+  if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
+
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = (int)(threadIdx.x & 63);
+  const int slot = blockIdx.x * WPB + wv;
+  if (slot >= p.n_sent) return;                 // whole wave
+  const Bufs B = make_bufs(p);
+  const int s = p.order[slot];
+  const int n = p.sent_n[s];
+  const uint32_t nbase = (uint32_t)p.node_off[s];
+  const int32_t* __restrict__ ssp = p.span_start + p.span_off[s];
+  uint32_t* __restrict__ bp = p.bp + p.bp_off[s];
+  const int k = p.k;
+  const int bstride = p.bp_stride;
+  const uint32_t slots = p.slots, seed = p.seed;
+  const int has_tri = p.has_tri;
+  Entry (&R)[RING][KT] = ring[wv];
+  int32_t* const cnt9 = cntl[wv];
+  unsigned long long* const LK = lkey[wv];
+  uint32_t* const LG = lgen[wv];
+  Counts cnt;
+
+  if (lane == 0) {                              // beam[0] = [BOS] (beam.py:21-23)
+    const Cand b0 = load_cand(B, nbase);
+    Entry e0;
+    e0.score = 0.0; e0.f6 = b0.f6;
+    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
+    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+    R[0][0] = e0;
+    cnt9[0] = 1;
+  }
+  int ss[MAX_SPAN + 1];
+#pragma unroll
+  for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = n >= 1 ? ssp[j] : 0;
+  dma_block<64>(B, nbase + (uint32_t)ss[0], n >= 1, stg[1][wv], lane);
+  __builtin_amdgcn_wave_barrier();
+
+  for (int e = 1; e <= n; ++e) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): this position's records landed
+    const uint4* const cst = stg[e & 1][wv];
+    const int dmax = min(e, p.max_len);
+    const int em9 = e % RING;
+    const int A0 = ss[0];
+    int pre[MAX_SPAN + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int j = 0; j < MAX_SPAN; ++j) {
+      const int d = MAX_SPAN - j;
+      const int c = (d <= dmax) ? cnt9[(e - d) % RING] : 0;
+      pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
+    }
+    const int M = pre[MAX_SPAN];
+    int ssn[MAX_SPAN + 1];
+    const int en = min(e + 1, n);
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = ssp[(en - 1) * MAX_SPAN + j];
+
+    // expansion g -> span slot j (d = 8 - j), hypothesis rank r, candidate i
+    auto decode = [&](int g, int& j, int& r, int& i) {
+      j = 0;
+#pragma unroll
+      for (int q = 1; q < MAX_SPAN; ++q) j += (g >= pre[q]) ? 1 : 0;
+      int pj = pre[0], m = ss[1] - ss[0];
+#pragma unroll
+      for (int q = 1; q < MAX_SPAN; ++q)
+        if (j == q) { pj = pre[q]; m = ss[q + 1] - ss[q]; }
+      const int local = g - pj;
+      // local / m through a float reciprocal (local < 2^24), corrected by one
+      r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
+      i = local - r * m;
+      if (i < 0) { --r; i += m; }
+      else if (i >= m) { ++r; i -= m; }
+    };
+
+    int nrun = 0;
+    const int last0 = min(RPC, (M + 63) >> 6) - 1;   // DMA of e+1 after this round of chunk 0
+    for (int base = 0; base < M; base += CH) {
+      unsigned long long myk[RPC];
+      uint32_t myg[RPC];
+#pragma unroll
+      for (int t = 0; t < RPC; ++t) {
+        myk[t] = 0ull;
+        myg[t] = INV;
+        if (base + 64 * t >= M) continue;        // uniform
+        const int g = base + 64 * t + lane;
+        const bool act = g < M;
+        int j = 0, r = 0, i = 0;
+        if (act) decode(g, j, r, i);
+        const int d = MAX_SPAN - j;
+        const int node = ss[j] + i;
+        const int so = node - A0;
+        Cand c;
+        if (!act) {
+          c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
+        } else if (so < STAGE) {
+          c = read_block<64>(cst, 0, so);
+        } else {
+          c = load_cand(B, nbase + (uint32_t)node);
+        }
+        const int hb = act ? (e - d) % RING : 0;
+        const int hr = act ? r : 0;
+        const Hyp h0 = read_entry(R[hb][hr]);
+        // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
+        const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));
+        Probe<NARROW> P;
+        probe_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
+        if (base == 0 && t == last0) {
+          // next position's records, into the other parity buffer (an LDS
+          // read behind this DMA waits for it: issued after the reads of
+          // the scoring rounds of chunk 0)
+          __builtin_amdgcn_sched_barrier(0);
+          dma_block<64>(B, nbase + (uint32_t)ss[MAX_SPAN], e < n, stg[(e + 1) & 1][wv], lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("" ::: "memory");
+        const Hyp h1 = read_entry(R[hb][hr]);
+        if (!skip) {
+          const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h1, c, cnt) : 0.0;
+          if (COUNT) ++cnt.exp;
+          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
+          myk[t] = ord_key(sc);
+          myg[t] = (uint32_t)g;
+        }
+        LK[KTP + 64 * t + lane] = myk[t];
+        LG[KTP + 64 * t + lane] = myg[t];
+      }
+      // Top-k of this chunk's entries and the running top-k.  The rank of an
+      // entry is the number of entries with a larger key, or an equal key and
+      // a smaller generation index (0 keys -- skipped / idle -- never win).
+      const int R0 = min(RPC, (M - base + 63) >> 6);         // rounds used (uniform)
+      const unsigned long long rk = lane < nrun ? LK[KTP - nrun + lane] : 0ull;
+      const uint32_t rg = lane < nrun ? LG[KTP - nrun + lane] : INV;
+      int valid = nrun;
+#pragma unroll
+      for (int t = 0; t < RPC; ++t)
+        if (t < R0) valid += __builtin_popcountll(__ballot(myk[t] != 0ull));
+      if (R0 == 1 && nrun == 0) {
+        // one entry per lane: rank against the 64 entries of the list
+        int rank = 0;
+#pragma unroll 2
+        for (int q = KTP; q < KTP + 64; q += 4) {
+          const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
+          const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
+          const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
+          const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
+          const uint32_t gq[4] = {gg.x, gg.y, gg.z, gg.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) rank += (kq[u] > myk[0] || (kq[u] == myk[0] && gq[u] < myg[0])) ? 1 : 0;
+        }
+        if (myk[0] != 0ull && rank < k) { tkey[wv][rank] = myk[0]; tgen[wv][rank] = myg[0]; }
+      } else {
+        // several entries per lane: prune with tau = the k-th largest of the
+        // lanes' maxima -- at least k entries are >= tau, so an entry below it
+        // ranks >= k; every entry better than one >= tau is itself >= tau, so
+        // ranks taken among the entries >= tau are exact.
+        unsigned long long mx = rk;
+#pragma unroll
+        for (int t = 0; t < RPC; ++t)
+          if (t < R0) mx = myk[t] > mx ? myk[t] : mx;
+        unsigned long long* const MX = LK + KTP;                 // chunk entries are in registers now
+        MX[lane] = mx;
+        if (lane == 0) tkey[wv][0] = ~0ull;
+        int gtc = 0;
+#pragma unroll 4
+        for (int q = 0; q < 64; q += 2) {
+          const ulonglong2 m2 = *reinterpret_cast<const ulonglong2*>(&MX[q]);
+          gtc += (m2.x > mx ? 1 : 0) + (m2.y > mx ? 1 : 0);
+        }
+        const int nz = __builtin_popcountll(__ballot(mx != 0ull));
+        if (mx != 0ull && gtc < k)
+          __hip_atomic_fetch_min(&tkey[wv][0], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned long long tau = nz >= k ? tkey[wv][0] : 1ull;
+        // compact the entries >= tau to the list head (in lane order per slot)
+        int nc = 0;
+        auto push = [&](unsigned long long key, uint32_t g) {
+          const bool c = key >= tau && key != 0ull;
+          const unsigned long long bal = __ballot(c);
+          const int at = nc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (c) { LK[at] = key; LG[at] = g; }
+          nc += __builtin_popcountll(bal);
+        };
+        if (nrun > 0) push(rk, rg);
+#pragma unroll
+        for (int t = 0; t < RPC; ++t)
+          if (t < R0) push(myk[t], myg[t]);
+        const int nc4 = (nc + 3) & ~3;
+        if (lane < nc4 - nc) { LK[nc + lane] = 0ull; LG[nc + lane] = INV; }
+        // rank candidate c = lane + 64 v among the nc candidates
+        for (int c0 = 0; c0 < nc; c0 += 64) {
+          const int c = c0 + lane;
+          const unsigned long long ck = c < nc ? LK[c] : 0ull;
+          const uint32_t cg = c < nc ? LG[c] : INV;
+          int rank = 0;
+          for (int q = 0; q < nc4; q += 4) {
+            const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
+            const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
+            const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
+            const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
+            const uint32_t gq[4] = {gg.x, gg.y, gg.z, gg.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) rank += (kq[u] > ck || (kq[u] == ck && gq[u] < cg)) ? 1 : 0;
+          }
+          if (c < nc && rank < k) { tkey[wv][rank] = ck; tgen[wv][rank] = cg; }
+        }
+      }
+      nrun = min(k, valid);
+      // running list for the next chunk / beam[e]: at [KTP - nrun, KTP), zero
+      // padding below it (in order behind the writes above)
+      const int nrp2 = (nrun + 3) & ~3;
+      if (lane < nrp2) {
+        const int dst = KTP - nrp2 + lane, src = lane - (nrp2 - nrun);
+        LK[dst] = src >= 0 ? tkey[wv][src] : 0ull;
+        LG[dst] = src >= 0 ? tgen[wv][src] : INV;
+      }
+    }
+
+    // beam[e] = the running top-k (Sequence.add, beam.py:112-116)
+    Entry ne;
+    uint32_t bpv = 0;
+    const bool writer = lane < nrun;
+    if (writer) {
+      const unsigned long long key = LK[KTP - nrun + lane];
+      int j, r, i;
+      decode((int)LG[KTP - nrun + lane], j, r, i);
+      const int d = MAX_SPAN - j;
+      const int node = ss[j] + i;
+      const int so = node - A0;
+      const Cand c = so < STAGE ? read_block<64>(cst, 0, so) : load_cand(B, nbase + (uint32_t)node);
+      const Entry& h = R[(e - d) % RING][r];
+      ne.score = ord_score(key); ne.f6 = c.f6;
+      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
+      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
+      ne.depth = h.depth + 1;
+      bpv = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (writer) {
+      R[em9][lane] = ne;
+      bp[(int64_t)e * bstride + lane] = bpv;
+    }
+    if (lane == 0) cnt9[em9] = nrun;
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = ssn[j];
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // matures = beam[n] + EOS (beam.py:59-61); backtrace per mature rank
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const int nm = cnt9[n % RING];
+  if (lane == 0) p.out_count[s] = nm;
+  if (lane >= nm && lane < k) {                 // unused mature slots read as empty
+    p.out_score[(int64_t)s * k + lane] = 0.0;
+    p.out_len[(int64_t)s * k + lane] = 0;
+  }
+  if (lane < nm) {
+    const Entry& f = R[n % RING][lane];
+    const int64_t o = (int64_t)s * k + lane;
+    p.out_score[o] = f.score + 0.0;
+    p.out_len[o] = (int32_t)f.depth;
+    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)lane * n;
+    int pos = n, rank = lane;
+    for (int step = (int)f.depth - 1; step >= 0; --step) {
+      const uint32_t v = bp[(int64_t)pos * bstride + rank];
+      codes[step] = (int32_t)bp_node(v);
+      pos -= (int)bp_d(v);
+      rank = (int)bp_rank(v);
+    }
+  }
+  if (COUNT) {
+    const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
+                             pb = group_sum<64>(cnt.probe);
+    if (lane == 0) {
+      atomicAdd(p.counters + 0, ex);
+      atomicAdd(p.counters + 1, tu);
+      atomicAdd(p.counters + 2, pb);
+    }
+  }
+}
+
+template <int KT, int WPB, bool NARROW, bool COUNT>
+hipError_t launch_bp(const DecodeParams& p, hipStream_t st) {
+  const int blocks = (p.n_sent + WPB - 1) / WPB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((lt_beam_pk<KT, WPB, NARROW, COUNT>), dim3(blocks), dim3(64 * WPB), 0, st, p);
+  return hipGetLastError();
+}
+
+static bool beam_v1() {
+  static const bool v = [] {
+    const char* e = std::getenv("LT_BEAM");
+    return e && std::strcmp(e, "v1") == 0;
+  }();
+  return v;
+}
+
 template <bool NARROW, bool COUNT>
 hipError_t launch_v(const DecodeParams& p, hipStream_t st) {
   switch (viterbi_variant()) {
@@ -1227,6 +1557,16 @@ hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
 
 template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
+  if (kt > 1 && !beam_v1()) {
+    switch (kt) {
+      case 2: return launch_bp<2, 4, NARROW, COUNT>(p, st);
+      case 4: return launch_bp<4, 4, NARROW, COUNT>(p, st);
+      case 8: return launch_bp<8, 4, NARROW, COUNT>(p, st);
+      case 16: return launch_bp<16, 2, NARROW, COUNT>(p, st);
+      case 32: return launch_bp<32, 2, NARROW, COUNT>(p, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (kt) {
     case 1: return launch_v<NARROW, COUNT>(p, st);
     case 2: return launch_b<2, 32, NARROW, COUNT>(p, st);
