@@ -145,6 +145,47 @@ def cpu_baseline(raw, sm, budget_s):
                       % (done, float(raw.sent_n[:done].mean()), dt)}
 
 
+def cpu_baseline_c(packed, keys, coefs, k, budget_s):
+    """The C restatement (oracle/lt_oracle.c: sorted-key binary search, OpenMP
+    over sentences) on the host cores available to this job, on a bounded
+    prefix of the same batch sized to about budget_s seconds."""
+    from oracle import lt_oracle
+    threads = max(1, min(int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1)), 64))
+    S = len(packed.sent_n)
+    n = min(S, 2048)
+    t0 = time.perf_counter()
+    lt_oracle.decode(packed, keys, coefs, k, 0, n, nthreads=threads)
+    dt = time.perf_counter() - t0
+    if dt < budget_s and n < S:
+        n = int(min(S, n * max(1.0, budget_s / max(dt, 1e-3))))
+        t0 = time.perf_counter()
+        lt_oracle.decode(packed, keys, coefs, k, 0, n, nthreads=threads)
+        dt = time.perf_counter() - t0
+    return {'value': n / dt, 'unit': 'sentences/s', 'cores': threads, 'kind': 'port',
+            'sample': 'first %d sentences of the batch, k=%d, oracle/lt_oracle.c (C restatement of '
+                      'beam.py:5-61, OpenMP over sentences, %d threads; includes its per-call '
+                      'sorted-key model build), %.2f s' % (n, k, threads, dt)}
+
+
+def traffic_from_profiles(kernel, k, sentences, features, seed):
+    """HBM bytes per launch of this configuration from the newest committed PMC
+    summary (profiles/*traffic*.json, written by tools/traffic_summary.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
+    FETCH_SIZE doubled per the gfx950 correction), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*traffic*.json'))):
+        try:
+            entries = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for e in entries:
+            if (e.get('kernel'), e.get('k'), e.get('sentences'), e.get('features'), e.get('seed')) == \
+                    (kernel, k, sentences, features, seed):
+                best = (e['traffic_bytes_per_launch'], os.path.relpath(f, ROOT))
+    return best
+
+
 def cpu_model():
     try:
         for line in open('/proc/cpuinfo'):
@@ -201,6 +242,8 @@ def main():
     pcie_rate = d.sum(float(a.sentences * pcie_steps)) / d.max(tp)
 
     count, length, score, codes = db.results(a.k)
+    kernel = (lib.lt_kernel_name(a.k) or b'?').decode()
+    traffic = traffic_from_profiles(kernel, a.k, a.sentences, a.features, a.seed)
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     B = algorithmic_bytes(raw, packed, tuples, length, a.k)
     achieved = B / avg_kernel_s / 1e9
@@ -237,8 +280,10 @@ def main():
                 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS,
-                'traffic': None,
-                'kernel': 'lt_viterbi_k' if a.k == 1 else 'lt_beam_k',
+                'traffic': traffic[0] if traffic else None,
+                'traffic_unit': 'HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)',
+                'traffic_source': traffic[1] if traffic else None,
+                'kernel': kernel,
                 'algorithmic_bytes_per_launch': B,
                 'avg_kernel_ms': avg_kernel_s * 1e3,
             },
@@ -250,6 +295,7 @@ def main():
         }
         if not a.no_cpu_baseline and d.world == 1:
             line['cpu_baseline'] = cpu_baseline(raw, sm, a.cpu_seconds)
+            line['cpu_baseline_c'] = cpu_baseline_c(packed, keys, coefs, a.k, a.cpu_seconds / 2)
         else:
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)

@@ -119,6 +119,9 @@ lt_status lt_decode_launch(lt_ctx* ctx, const lt_model* model, lt_batch* batch, 
 /* Device time of the last decode kernel (HIP events on the ctx stream), ms.
  * Valid after lt_sync. */
 lt_status lt_last_kernel_ms(lt_ctx* ctx, float* ms);
+/* Name of the HIP kernel lt_decode_launch runs for beam k (profiling:
+ * matches the rocprofv3 kernel name prefix); NULL for an unsupported k. */
+const char* lt_kernel_name(int k);
 
 /* Results of beam_search's `matures` (beam.py:59-61), per sentence s:
  *   count[s]               number of matures (<= k)

@@ -19,7 +19,7 @@ _STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED
 EXPORTED_SYMBOLS = (
     'lt_abi_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
     'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
-    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms',
+    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms', 'lt_kernel_name',
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
 )
 
@@ -80,6 +80,7 @@ def load(path=None):
             'lt_batch_code_slots': (i64, [vp, C.c_int]),
             'lt_decode_launch': (i32, [vp, vp, vp, C.c_int]),
             'lt_last_kernel_ms': (i32, [vp, C.POINTER(C.c_float)]),
+            'lt_kernel_name': (C.c_char_p, [C.c_int]),
             'lt_result_fetch': (i32, [vp, vp]),
             'lt_result_view': (i32, [vp, C.POINTER(Result)]),
             'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),

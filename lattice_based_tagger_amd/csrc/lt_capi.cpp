@@ -670,6 +670,8 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   return LT_OK;
 }
 
+const char* lt_kernel_name(int k) { return kernel_name_for(k); }
+
 lt_status lt_last_kernel_ms(lt_ctx* c, float* ms) {
   if (!c || !ms) return fail(LT_EINVAL, "lt_last_kernel_ms: NULL argument");
   HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));

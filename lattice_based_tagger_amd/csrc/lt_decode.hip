@@ -1582,6 +1582,13 @@ hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
 
 namespace lt {
 
+const char* kernel_name_for(int k) {
+  const int kt = beam_template_for(k);
+  if (kt < 0) return nullptr;
+  if (kt > 1) return beam_v1() ? "lt_beam_k" : "lt_beam_pk";
+  return viterbi_variant() == 0 ? "lt_viterbi_k" : "lt_viterbi_pk";
+}
+
 int beam_template_for(int k) {
   if (k <= 1) return 1;
   if (k <= 2) return 2;

@@ -42,6 +42,7 @@ struct DecodeParams {
 };
 
 int beam_template_for(int k);
+const char* kernel_name_for(int k);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count);
 
 }  // namespace lt
