@@ -1373,8 +1373,9 @@ lt_beam_pk(DecodeParams p) {
       if (R0 == 1 && nrun == 0) {
         // one entry per lane: rank against the 64 entries of the list
         int rank = 0;
+        const int qe = KTP + ((min(64, M - base) + 3) & ~3);   // entries past M are 0
 #pragma unroll 2
-        for (int q = KTP; q < KTP + 64; q += 4) {
+        for (int q = KTP; q < qe; q += 4) {
           const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
           const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
           const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
