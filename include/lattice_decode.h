@@ -69,6 +69,29 @@ typedef struct {
 } lt_model_desc;
 
 lt_status lt_model_create(lt_ctx* ctx, const lt_model_desc* desc, lt_model** out);
+
+/* ---- model images (SURVEY §8(f) model pack format) -------------------------
+ * The host-side part of lt_model_create -- validated keys, built cuckoo table,
+ * dense class-3 table -- as a self-contained image that can be written to a
+ * file once (after scan_features, features/utils.py:50-55) and uploaded on
+ * later runs without rebuilding (replaces the per-run set_encoder work,
+ * beam/score_funcs.py:106-125).  lt_image_build needs no GPU. */
+typedef struct lt_image lt_image;
+typedef struct {
+  int32_t narrow;        /* 1: 16 B slots {key64, coef}; 0: 32 B slots */
+  uint32_t seed;         /* cuckoo hash seed */
+  int64_t slots;         /* table slots */
+  const void* table;     /* slots * (narrow ? 16 : 32) bytes */
+  int64_t table_bytes;
+  uint32_t d3mul;        /* dense class-3 index multiplier; 0 = none */
+  const double* d3;      /* 32 x 32 float64, or NULL */
+} lt_model_image;
+lt_status lt_image_build(const lt_model_desc* desc, lt_image** out);
+/* Pointers into the image (valid until lt_image_destroy). */
+lt_status lt_image_view(const lt_image* image, lt_model_image* view);
+lt_status lt_image_destroy(lt_image* image);
+/* Upload an image (e.g. memory-mapped from a model file); no table build. */
+lt_status lt_model_create_from_image(lt_ctx* ctx, const lt_model_image* image, lt_model** out);
 lt_status lt_model_destroy(lt_model* model);
 /* Hash-table slots allocated on the device (32 B each). */
 int64_t lt_model_slots(const lt_model* model);

@@ -21,6 +21,7 @@ EXPORTED_SYMBOLS = (
     'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
     'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms', 'lt_kernel_name',
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
+    'lt_image_build', 'lt_image_view', 'lt_image_destroy', 'lt_model_create_from_image',
 )
 
 
@@ -81,6 +82,10 @@ def load(path=None):
             'lt_decode_launch': (i32, [vp, vp, vp, C.c_int]),
             'lt_last_kernel_ms': (i32, [vp, C.POINTER(C.c_float)]),
             'lt_kernel_name': (C.c_char_p, [C.c_int]),
+            'lt_image_build': (i32, [vp, C.POINTER(vp)]),
+            'lt_image_view': (i32, [vp, vp]),
+            'lt_image_destroy': (i32, [vp]),
+            'lt_model_create_from_image': (i32, [vp, vp, C.POINTER(vp)]),
             'lt_result_fetch': (i32, [vp, vp]),
             'lt_result_view': (i32, [vp, C.POINTER(Result)]),
             'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),
@@ -136,6 +141,47 @@ class Context:
             pass
 
 
+class ModelImageView(C.Structure):
+    _fields_ = [('narrow', C.c_int32), ('seed', C.c_uint32), ('slots', C.c_int64),
+                ('table', C.c_void_p), ('table_bytes', C.c_int64),
+                ('d3mul', C.c_uint32), ('d3', C.c_void_p)]
+
+
+class ModelImage:
+    """Host-side model image (lt_image): the built cuckoo table and dense
+    class-3 table of a key set, without a GPU.  ``arrays()`` copies them out
+    (for a model file); ``DeviceModel.from_image`` uploads them."""
+
+    def __init__(self, keys, coefs, lib=None):
+        lib = lib or load()
+        keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 4)
+        coefs = np.ascontiguousarray(coefs, dtype=np.float64)
+        desc = ModelDesc(keys.shape[0], _ptr(keys), _ptr(coefs))
+        h = C.c_void_p()
+        check(lib.lt_image_build(C.byref(desc), C.byref(h)))
+        self.handle, self._lib = h, lib
+
+    def arrays(self):
+        v = ModelImageView()
+        check(self._lib.lt_image_view(self.handle, C.byref(v)))
+        table = np.frombuffer((C.c_uint8 * v.table_bytes).from_address(v.table), dtype=np.uint8).copy()
+        d3 = (np.frombuffer((C.c_double * 1024).from_address(v.d3), dtype=np.float64).copy()
+              if v.d3mul else np.zeros(0, dtype=np.float64))
+        return {'narrow': int(v.narrow), 'seed': int(v.seed), 'slots': int(v.slots),
+                'd3mul': int(v.d3mul), 'table': table, 'd3': d3}
+
+    def close(self):
+        if self.handle:
+            self._lib.lt_image_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DeviceModel:
     """Hash table of the probed feature classes on one device (lt_model)."""
 
@@ -148,6 +194,24 @@ class DeviceModel:
         self.handle = h
         self.ctx = ctx
         self.slots = ctx._lib.lt_model_slots(h)
+
+    @classmethod
+    def from_image(cls, ctx, image):
+        """Upload a model image: a dict as returned by ``ModelImage.arrays``
+        (arrays may be memory-mapped from a model file)."""
+        table = np.ascontiguousarray(image['table'], dtype=np.uint8)
+        d3 = np.ascontiguousarray(image['d3'], dtype=np.float64)
+        if image['d3mul'] and d3.size != 1024:
+            raise ValueError('dense class-3 table must hold 1024 coefficients')
+        v = ModelImageView(int(image['narrow']), int(image['seed']), int(image['slots']),
+                           table.ctypes.data, table.nbytes, int(image['d3mul']),
+                           d3.ctypes.data if image['d3mul'] else None)
+        h = C.c_void_p()
+        check(ctx._lib.lt_model_create_from_image(ctx.handle, C.byref(v), C.byref(h)))
+        self = cls.__new__(cls)
+        self.handle, self.ctx = h, ctx
+        self.slots = ctx._lib.lt_model_slots(h)
+        return self
 
     def close(self):
         if self.handle:

@@ -122,8 +122,11 @@ class Decoder:
     def device_model(self, model):
         dm = model._device_models.get(self.device)
         if dm is None:
-            dm = model._device_models[self.device] = _capi.DeviceModel(
-                self.ctx, model.keys, model.coefs)
+            if getattr(model, 'image', None) is not None:      # model pack: no table build
+                dm = _capi.DeviceModel.from_image(self.ctx, model.image)
+            else:
+                dm = _capi.DeviceModel(self.ctx, model.keys, model.coefs)
+            model._device_models[self.device] = dm
         return dm
 
     def decode_packed(self, model, packed, k):

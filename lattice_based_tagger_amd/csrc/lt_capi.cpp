@@ -10,6 +10,7 @@
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -271,13 +272,29 @@ static void build_dense3(const std::vector<KeyRec>& keys, uint32_t& mul, std::ve
     if (k.cls == 3) tab[(size_t)d3_index(k.a, mul) * D3_DIM + d3_index(k.b, mul)] = k.coef;
 }
 
-lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
-  if (!c || !d || !out) return fail(LT_EINVAL, "lt_model_create: NULL argument");
+// Host-side model image: validated keys, the built cuckoo table and the
+// dense class-3 table.  Built without a GPU (lt_image_build), uploaded by
+// lt_model_create_from_image; lt_model_create does both.
+struct lt_image {
+  int narrow = 0;
+  uint32_t seed = 0;
+  int64_t slots = 0;
+  std::vector<SlotN> tn;
+  std::vector<SlotW> tw;
+  uint32_t d3mul = 0;
+  std::vector<double> d3;
+  std::vector<KeyRec> keys;   // narrow images: kept for the optional hot table
+};
+
+lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
+  if (!d || !out) return fail(LT_EINVAL, "lt_image_build: NULL argument");
   *out = nullptr;
   if (d->n_keys < 0 || (d->n_keys > 0 && (!d->keys || !d->coefs)))
     return fail(LT_EINVAL, "lt_model_create: bad key arrays");
   if (d->n_keys > ((int64_t)1 << 29)) return fail(LT_EUNSUPPORTED, "lt_model_create: too many keys");
-  std::vector<KeyRec> keys;
+  std::unique_ptr<lt_image> img(new (std::nothrow) lt_image);
+  if (!img) return fail(LT_ENOMEM, "lt_model_create: out of host memory");
+  std::vector<KeyRec>& keys = img->keys;
   uint32_t max_id = 0;
   try {
     keys.resize((size_t)d->n_keys);
@@ -301,8 +318,6 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
   const bool narrow = max_id < (1u << NARROW_ID_BITS);
   const int64_t slot_bytes = narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
   int64_t slots = std::max<int64_t>(64, (int64_t)(d->n_keys / 0.45) + 1);   // load factor <= 0.45
-  std::vector<SlotN> tn;
-  std::vector<SlotW> tw;
   uint32_t seed = 0x2545F491u;
   bool ok = false;
   for (int attempt = 0; attempt < 24 && !ok; ++attempt) {
@@ -311,8 +326,8 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
                   (long long)slots);
     int64_t dup = -1;
     try {
-      ok = narrow ? cuckoo_build(keys, (uint32_t)slots, seed, tn, &dup)
-                  : cuckoo_build(keys, (uint32_t)slots, seed, tw, &dup);
+      ok = narrow ? cuckoo_build(keys, (uint32_t)slots, seed, img->tn, &dup)
+                  : cuckoo_build(keys, (uint32_t)slots, seed, img->tw, &dup);
     } catch (...) {
       return fail(LT_ENOMEM, "lt_model_create: cannot allocate %lld slots", (long long)slots);
     }
@@ -323,26 +338,50 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
     }
   }
   if (!ok) return fail(LT_EINVAL, "lt_model_create: cuckoo table build failed");
-  uint32_t d3mul = 0;
-  std::vector<double> d3;
-  build_dense3(keys, d3mul, d3);
+  build_dense3(keys, img->d3mul, img->d3);
+  img->narrow = narrow ? 1 : 0;
+  img->seed = seed;
+  img->slots = slots;
+  if (!narrow) std::vector<KeyRec>().swap(keys);
+  *out = img.release();
+  return LT_OK;
+}
+
+lt_status lt_image_view(const lt_image* img, lt_model_image* v) {
+  if (!img || !v) return fail(LT_EINVAL, "lt_image_view: NULL argument");
+  v->narrow = img->narrow;
+  v->seed = img->seed;
+  v->slots = img->slots;
+  v->table = img->narrow ? (const void*)img->tn.data() : (const void*)img->tw.data();
+  v->table_bytes = img->slots * (img->narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW));
+  v->d3mul = img->d3mul;
+  v->d3 = img->d3mul ? img->d3.data() : nullptr;
+  return LT_OK;
+}
+
+lt_status lt_image_destroy(lt_image* img) {
+  delete img;
+  return LT_OK;
+}
+
+static lt_status model_upload(lt_ctx* c, const lt_model_image* v, std::vector<KeyRec>* keys,
+                              lt_model** out) {
   HIP_TRY(hipSetDevice(c->device));
   lt_model* m = new (std::nothrow) lt_model;
   if (!m) return fail(LT_ENOMEM, "lt_model_create: out of host memory");
   m->ctx = c;
-  m->slots = slots;
-  m->seed = seed;
-  m->narrow = narrow ? 1 : 0;
-  if (narrow) m->keys.swap(keys);
+  m->slots = v->slots;
+  m->seed = v->seed;
+  m->narrow = v->narrow ? 1 : 0;
+  if (keys && m->narrow) m->keys.swap(*keys);
   static std::atomic<uint64_t> next_uid{1};
   m->uid = next_uid.fetch_add(1);
-  hipError_t e = hipMalloc(&m->d_table, (size_t)(slots * slot_bytes));
+  hipError_t e = hipMalloc(&m->d_table, (size_t)v->table_bytes);
   if (e == hipSuccess)
-    e = hipMemcpyAsync(m->d_table, narrow ? (const void*)tn.data() : (const void*)tw.data(),
-                       (size_t)(slots * slot_bytes), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess && d3mul) {
-    m->d3mul = d3mul;
-    e = dalloc_copy(&m->d_d3, d3.data(), d3.size(), c->stream);
+    e = hipMemcpyAsync(m->d_table, v->table, (size_t)v->table_bytes, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && v->d3mul) {
+    m->d3mul = v->d3mul;
+    e = dalloc_copy(&m->d_d3, v->d3, (size_t)D3_DIM * D3_DIM, c->stream);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
@@ -353,6 +392,32 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
   }
   *out = m;
   return LT_OK;
+}
+
+lt_status lt_model_create_from_image(lt_ctx* c, const lt_model_image* v, lt_model** out) {
+  if (!c || !v || !out) return fail(LT_EINVAL, "lt_model_create_from_image: NULL argument");
+  *out = nullptr;
+  if (v->narrow != 0 && v->narrow != 1) return fail(LT_EINVAL, "model image: bad narrow flag");
+  if (v->slots < 64 || !v->table) return fail(LT_EINVAL, "model image: empty table");
+  const int64_t sb = v->narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
+  if (v->slots > (((int64_t)1 << 31) - 1) / sb || v->table_bytes != v->slots * sb)
+    return fail(LT_EINVAL, "model image: table size %lld does not match %lld slots",
+                (long long)v->table_bytes, (long long)v->slots);
+  if (v->d3mul && !v->d3) return fail(LT_EINVAL, "model image: dense table missing");
+  return model_upload(c, v, nullptr, out);
+}
+
+lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
+  if (!c || !d || !out) return fail(LT_EINVAL, "lt_model_create: NULL argument");
+  *out = nullptr;
+  lt_image* img = nullptr;
+  lt_status st = lt_image_build(d, &img);
+  if (st != LT_OK) return st;
+  lt_model_image v;
+  lt_image_view(img, &v);
+  st = model_upload(c, &v, &img->keys, out);
+  lt_image_destroy(img);
+  return st;
 }
 
 lt_status lt_model_destroy(lt_model* m) {

@@ -693,7 +693,7 @@ struct alignas(16) SentRec {
 };
 
 template <int W, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(256, NARROW ? PK_WAVES : 3)
+__global__ void __launch_bounds__(256, (NARROW && W <= 6) ? PK_WAVES : 3)
 lt_viterbi_pk(DecodeParams p) {
   constexpr int BPL = PK_BPL;                   // end positions whose backpointer stays in LDS
   __shared__ VEntry ring[P_WPB][W][RING];

@@ -74,6 +74,7 @@ def node_mask_from_vocab(vm_word, vm_morph, vm_tag):
 NODE_LOCAL_SCORERS = ('RegularizationScore', 'MorphemePreferenceScore',
                       'WordPreferenceScore')
 TRIGRAM_SCORER = 'SimpleTrigramFeatureScore'
+PACKED_TRIGRAM_SCORER = 'PackedTrigramFeatureScore'      # modelpack.py
 ENCODER_CLASSES = ('SimpleTrigramEncoder',)
 
 
@@ -105,7 +106,7 @@ class LoweredModel:
         self.trigram = None
         for f in funcs:
             name = type(f).__name__
-            if name == TRIGRAM_SCORER:
+            if name in (TRIGRAM_SCORER, PACKED_TRIGRAM_SCORER):
                 if self.trigram is not None:
                     raise NotImplementedError('at most one SimpleTrigramFeatureScore is supported')
                 self.trigram = f
@@ -121,8 +122,13 @@ class LoweredModel:
         self.coefs = np.zeros(0, dtype=np.float64)
         self.feature_dic = None
         self.coefficients = None
+        self.local = None           # packed models: {(cls, *comps): coef} of classes 4-6
+        self.image = None           # packed models: prebuilt device image
         if self.trigram is not None:
-            self._lower_trigram(self.trigram)
+            if type(self.trigram).__name__ == PACKED_TRIGRAM_SCORER:
+                self._lower_pack(self.trigram.pack)
+            else:
+                self._lower_trigram(self.trigram)
         self._device_models = {}
 
     @property
@@ -182,6 +188,12 @@ class LoweredModel:
         self.keys = np.asarray(keys, dtype=np.uint32).reshape(-1, 4)
         self.coefs = np.asarray(coefs, dtype=np.float64)
 
+    def _lower_pack(self, pack):
+        """A model pack already holds the lowered tables and the device image."""
+        self.vocab, self.vmask, self.keys, self.coefs, self.local = pack.lowered_parts()
+        self.image = pack.image
+        self.coefficients = pack.array('coefficients')
+
     # -- node-local helpers (used by the packer) ---------------------------
     def node_terms(self, w):
         """(pre, [post...]) for appending node ``w``: the node-local plugins'
@@ -193,6 +205,10 @@ class LoweredModel:
 
     def node_local_features(self, w, is_unk):
         """Coefficients (or None) of feature classes 4, 5 and 6 for node w."""
+        if self.local is not None:
+            loc = self.local
+            return (loc.get((4, w.len)), loc.get((5, w.word, w.tag0, w.is_l)),
+                    loc.get((6, min(8, w.len))) if is_unk else None)
         dic = self.feature_dic
         if dic is None:
             return None, None, None
