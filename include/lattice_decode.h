@@ -174,6 +174,38 @@ lt_status lt_decode(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k, 
 lt_status lt_count_ops(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k,
                        int64_t* expansions, int64_t* feature_tuples, int64_t* probes);
 
+/* ---- evaluate -------------------------------------------
+ * Batch form of BeamScoreFunctions.evaluate(seq) (score_funcs.py:44-48) for
+ * given paths (e.g. gold sequences):
+ *   total = ((0 + E_0) + E_1) + ...   over the scorers in constructor order,
+ *   node-local scorer t (score_funcs.py:62-63, 81-82, 96-97):
+ *       E_t = ((0 + v_t(w_0)) + v_t(w_1)) + ...  over every word of the path
+ *   trigram scorer (score_funcs.py:127-135): the Sequence.add replay
+ *       E = ((0 + inc_a) + inc_b) + ...  over the words not tagged BOS/EOS,
+ *       inc = the trigram score of (prev2, prev1, w) in the replayed path.
+ * Word records are lattice-node records as in lt_batch_desc; prev1/prev2 are
+ * the replayed predecessors of each word (global word index, -1 = None);
+ * prev1 = -2 marks a word the replay skips. */
+typedef struct {
+  int32_t n_paths;
+  int64_t n_words;
+  const int64_t* path_off;      /* [n_paths + 1] */
+  const int32_t* word;          /* [n_words] interned ids (0 = in no key) */
+  const int32_t* morph0;
+  const int32_t* tag;
+  const uint32_t* mask;         /* pre-filter bits + flags, as lt_batch_desc.node_mask */
+  const double* f4;
+  const double* f5;
+  const double* f6;
+  const int64_t* prev1;         /* [n_words] */
+  const int64_t* prev2;         /* [n_words] */
+  int32_t n_terms;              /* node-local scorers */
+  const double* terms;          /* [n_terms * n_words], scorer-major */
+  int32_t trigram_pos;          /* position of the trigram scorer among the n_terms + 1; -1 = none */
+} lt_paths_desc;
+/* Blocking: scores[n_paths] (host buffer) receives the totals. */
+lt_status lt_evaluate(lt_ctx* ctx, const lt_model* model, const lt_paths_desc* paths, double* scores);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,6 +8,8 @@ Public surface (mirrors the reference's ``lattice_tagger.beam``,
     MorphemePreferenceScore, WordPreferenceScore, SimpleTrigramFeatureScore
     WordsEncoder, SimpleTrigramEncoder, trigram_encoder
     Tagger, Word, tag constants
+    evaluate_batch (BeamScoreFunctions.evaluate for many paths on the GPU)
+    modelpack (trained-model files: save / load)
 
 Decoding runs in hand-written HIP kernels for gfx950 (``csrc/``) behind the
 C-ABI ``include/lattice_decode.h``; see DESIGN.md.
@@ -21,5 +23,6 @@ from .score_funcs import (BeamScoreFunction, BeamScoreFunctions, RegularizationS
 from .feature import WordsEncoder, SimpleTrigramEncoder, trigram_encoder
 from .beam import beam_search, beam_search_batch, Beam, Sequence, Decoder
 from .tagger import Tagger, sentence_lookup, sentence_lookup_as_begin_index
+from .evaluate import evaluate_batch
 
 __version__ = '0.1.0'

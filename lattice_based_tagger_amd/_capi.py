@@ -22,6 +22,7 @@ EXPORTED_SYMBOLS = (
     'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms', 'lt_kernel_name',
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
     'lt_image_build', 'lt_image_view', 'lt_image_destroy', 'lt_model_create_from_image',
+    'lt_evaluate',
 )
 
 
@@ -86,6 +87,7 @@ def load(path=None):
             'lt_image_view': (i32, [vp, vp]),
             'lt_image_destroy': (i32, [vp]),
             'lt_model_create_from_image': (i32, [vp, vp, C.POINTER(vp)]),
+            'lt_evaluate': (i32, [vp, vp, vp, vp]),
             'lt_result_fetch': (i32, [vp, vp]),
             'lt_result_view': (i32, [vp, C.POINTER(Result)]),
             'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),

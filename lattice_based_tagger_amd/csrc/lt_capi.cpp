@@ -737,6 +737,88 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
 
 const char* lt_kernel_name(int k) { return kernel_name_for(k); }
 
+// ------------------------------------------------------------- evaluate --
+lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, double* scores) {
+  if (!c || !m || !d || (!scores && d->n_paths > 0)) return fail(LT_EINVAL, "lt_evaluate: NULL argument");
+  if (m->ctx != c) return fail(LT_EINVAL, "lt_evaluate: model from another context");
+  if (d->n_paths < 0 || d->n_words < 0 || d->n_terms < 0)
+    return fail(LT_EINVAL, "lt_evaluate: negative size");
+  if (d->n_words * (int64_t)sizeof(NodeRec) >= ((int64_t)1 << 31))
+    return fail(LT_EUNSUPPORTED, "lt_evaluate: %lld words exceed one launch", (long long)d->n_words);
+  if (d->trigram_pos < -1 || d->trigram_pos > d->n_terms)
+    return fail(LT_EINVAL, "lt_evaluate: trigram_pos %d out of range", d->trigram_pos);
+  if (!d->path_off || (d->n_words > 0 && (!d->word || !d->morph0 || !d->tag || !d->mask || !d->f4 ||
+                                          !d->f5 || !d->f6 || !d->prev1 || !d->prev2)) ||
+      (d->n_terms > 0 && d->n_words > 0 && !d->terms))
+    return fail(LT_EINVAL, "lt_evaluate: NULL arrays");
+  if (d->path_off[0] != 0 || d->path_off[d->n_paths] != d->n_words)
+    return fail(LT_EINVAL, "lt_evaluate: path offsets do not cover the words");
+  for (int32_t s = 0; s < d->n_paths; ++s)
+    if (d->path_off[s + 1] < d->path_off[s]) return fail(LT_EINVAL, "lt_evaluate: path offsets decrease");
+  for (int64_t w = 0; w < d->n_words; ++w) {
+    const int64_t j = d->prev1[w], i = d->prev2[w];
+    if (j == -2) continue;
+    if (j < 0 || j >= d->n_words || i < -1 || i >= d->n_words)
+      return fail(LT_EINVAL, "lt_evaluate: word %lld has a bad predecessor", (long long)w);
+  }
+  for (int64_t x = 0; x < (int64_t)d->n_terms * d->n_words; ++x)
+    if (!std::isfinite(d->terms[x])) return fail(LT_EUNSUPPORTED, "lt_evaluate: non-finite term");
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<NodeRec> recs((size_t)d->n_words);
+  for (int64_t w = 0; w < d->n_words; ++w) {
+    NodeRec& r = recs[(size_t)w];
+    r.word = (uint32_t)d->word[w];
+    r.morph = (uint32_t)d->morph0[w];
+    r.tag = (uint32_t)d->tag[w];
+    r.mask = d->mask[w] & ~(D_MASK | F_WI);
+    r.pre = 0.0;
+    r.f4 = d->f4[w];
+    r.f5 = d->f5[w];
+    r.f6 = d->f6[w];
+  }
+  hipStream_t st = c->stream;
+  hipError_t e = hipSuccess;
+  NodeRec* d_words = nullptr;
+  int64_t *d_p1 = nullptr, *d_p2 = nullptr, *d_off = nullptr;
+  double *d_terms = nullptr, *d_inc = nullptr, *d_out = nullptr;
+  const size_t nw = (size_t)d->n_words, np = (size_t)d->n_paths;
+  e = dalloc_copy(&d_words, recs.data(), nw, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_p1, d->prev1, nw, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_p2, d->prev2, nw, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_off, d->path_off, np + 1, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_terms, d->terms, (size_t)d->n_terms * nw, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_inc, (const double*)nullptr, nw, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_out, (const double*)nullptr, np, st);
+  if (e == hipSuccess) {
+    EvalParams p{};
+    p.table = m->d_table;
+    p.slots = (uint32_t)m->slots;
+    p.seed = m->seed;
+    p.narrow = m->narrow;
+    p.has_tri = d->trigram_pos >= 0 ? 1 : 0;
+    p.d3 = m->d_d3;
+    p.d3mul = m->d3mul;
+    p.n_paths = d->n_paths;
+    p.n_words = d->n_words;
+    p.words = d_words;
+    p.prev1 = d_p1;
+    p.prev2 = d_p2;
+    p.path_off = d_off;
+    p.n_terms = d->n_terms;
+    p.terms = d_terms;
+    p.trigram_pos = d->trigram_pos;
+    p.inc = d_inc;
+    p.out = d_out;
+    e = launch_evaluate(p, st);
+  }
+  if (e == hipSuccess && np) e = hipMemcpyAsync(scores, d_out, np * sizeof(double), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  void* bufs[] = {d_words, d_p1, d_p2, d_off, d_terms, d_inc, d_out};
+  for (void* b : bufs) dfree(b);
+  if (e != hipSuccess) return fail(LT_EHIP, "lt_evaluate: %s", hipGetErrorString(e));
+  return LT_OK;
+}
+
 lt_status lt_last_kernel_ms(lt_ctx* c, float* ms) {
   if (!c || !ms) return fail(LT_EINVAL, "lt_last_kernel_ms: NULL argument");
   HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));

@@ -1531,6 +1531,68 @@ static bool beam_v1() {
   return v;
 }
 
+// ===========================================================================
+// Batch evaluate (BeamScoreFunctions.evaluate, score_funcs.py:44-48)
+// ===========================================================================
+// One lane per word: the trigram increment of the replayed path
+// (score_funcs.py:127-135 -> 137-144) -- the same probe / numpy-order sum code
+// as the decoder, with the hypothesis built from the word's replayed
+// predecessors.
+template <bool NARROW>
+__global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
+  __shared__ double d3l[D3_DIM * D3_DIM];
+  Aux aux{nullptr, nullptr, p.d3mul};
+  if (p.d3) {
+    const uint4* src = reinterpret_cast<const uint4*>(p.d3);
+    uint4* dst = reinterpret_cast<uint4*>(d3l);
+    for (int i = threadIdx.x; i < D3_DIM * D3_DIM / 2; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    aux.d3 = d3l;
+  }
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= p.n_words) return;
+  const int64_t j = p.prev1[w];
+  if (j == -2 || !p.has_tri) { p.inc[w] = 0.0; return; }
+  Bufs B;
+  B.node = make_rsrc(p.words, (uint64_t)p.n_words * sizeof(NodeRec));
+  B.tab = make_rsrc(p.table, (uint64_t)p.slots * (NARROW ? sizeof(SlotN) : sizeof(SlotW)));
+  const Cand c = load_cand(B, (uint32_t)w);
+  const Cand cj = load_cand(B, (uint32_t)j);
+  const int64_t i = p.prev2[w];
+  const Cand ci = load_cand(B, i >= 0 ? (uint32_t)i : INV);
+  Hyp h;
+  h.score = 0.0; h.f6 = cj.f6;
+  h.jword = cj.word; h.jmorph = cj.morph; h.jtag = cj.tag; h.jmask = cj.mask;
+  h.iword = ci.word; h.imorph = ci.morph; h.imask = i >= 0 ? (ci.mask | F_WI) : 0u;
+  h.depth = 0;
+  Counts cnt;
+  p.inc[w] = trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux);
+}
+
+// One lane per path: the exact-order sums.
+__global__ void __launch_bounds__(256) lt_eval_paths_k(EvalParams p) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= p.n_paths) return;
+  const int64_t w0 = p.path_off[s], w1 = p.path_off[s + 1];
+  double tri = 0.0;
+  for (int64_t w = w0; w < w1; ++w)
+    if (p.prev1[w] != -2) tri += p.inc[w];
+  double total = 0.0;
+  int t = 0;
+  for (int f = 0; f <= p.n_terms; ++f) {
+    if (f == p.trigram_pos) {
+      total += tri;
+    } else if (t < p.n_terms) {
+      const double* v = p.terms + (int64_t)t * p.n_words;
+      double e = 0.0;
+      for (int64_t w = w0; w < w1; ++w) e += v[w];
+      total += e;
+      ++t;
+    }
+  }
+  p.out[s] = total;
+}
+
 template <bool NARROW, bool COUNT>
 hipError_t launch_v(const DecodeParams& p, hipStream_t st) {
   switch (viterbi_variant()) {
@@ -1582,6 +1644,21 @@ hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
 }  // namespace
 
 namespace lt {
+
+hipError_t launch_evaluate(const EvalParams& p, hipStream_t st) {
+  if (p.n_words > 0) {
+    const int blocks = (int)((p.n_words + 255) / 256);
+    if (p.narrow) hipLaunchKernelGGL(lt_eval_words_k<true>, dim3(blocks), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(lt_eval_words_k<false>, dim3(blocks), dim3(256), 0, st, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (p.n_paths > 0) {
+    hipLaunchKernelGGL(lt_eval_paths_k, dim3((p.n_paths + 255) / 256), dim3(256), 0, st, p);
+    return hipGetLastError();
+  }
+  return hipSuccess;
+}
 
 const char* kernel_name_for(int k) {
   const int kt = beam_template_for(k);

@@ -41,6 +41,29 @@ struct DecodeParams {
   unsigned long long* counters; // [3] expansions, feature tuples, probes
 };
 
+// Batch evaluate (lt_evaluate): word increments, then per-path sums.
+struct EvalParams {
+  const void* table;
+  uint32_t slots;
+  uint32_t seed;
+  int32_t narrow;
+  int32_t has_tri;
+  const double* d3;
+  uint32_t d3mul;
+  int32_t n_paths;
+  int64_t n_words;
+  const NodeRec* words;         // AoS word records
+  const int64_t* prev1;
+  const int64_t* prev2;
+  const int64_t* path_off;
+  int32_t n_terms;
+  const double* terms;
+  int32_t trigram_pos;
+  double* inc;                  // [n_words] scratch
+  double* out;                  // [n_paths]
+};
+hipError_t launch_evaluate(const EvalParams& p, hipStream_t st);
+
 int beam_template_for(int k);
 const char* kernel_name_for(int k);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count);

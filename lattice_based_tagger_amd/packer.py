@@ -54,6 +54,30 @@ def _span_candidates(bindex_b, b, n, max_len):
     return groups
 
 
+def node_record(model, w):
+    """Device fields of lattice node ``w``: interned word / morph0 / tag ids,
+    pre-filter mask + flags, and the coefficients of the node-local feature
+    classes 4, 5, 6 (None when absent)."""
+    vocab, vmask = model.vocab, model.vmask
+    is_unk = w.tag0 == Unk
+    wid = vocab.get(w.word, 0)
+    mid = vocab.get(w.morph0, 0)
+    tid = vocab.get(w.tag0, 0)
+    m = L.node_mask_from_vocab(int(vmask[wid]), int(vmask[mid]), int(vmask[tid]))
+    if is_unk:
+        m |= L.F_UNK
+    if w.tag0 in CONTEXTUAL_TAGS:
+        m |= L.F_CTX
+    c4, c5, c6 = model.node_local_features(w, is_unk)
+    if c4 is not None:
+        m |= L.F_HAS4
+    if c5 is not None:
+        m |= L.F_HAS5
+    if c6 is not None:
+        m |= L.F_HAS6
+    return wid, mid, tid, m, c4, c5, c6
+
+
 def pack(sentences, model, max_len=8):
     """Pack ``sentences`` = iterable of ``(bindex, chars)``.
 
@@ -65,8 +89,6 @@ def pack(sentences, model, max_len=8):
     """
     if not 1 <= max_len <= MAX_SPAN:
         raise NotImplementedError('max_len must be in 1..%d' % MAX_SPAN)
-    vocab = model.vocab
-    vmask = model.vmask
     n_post = model.n_post
 
     sent_n, node_off, span_off = [], [0], [0]
@@ -77,22 +99,7 @@ def pack(sentences, model, max_len=8):
     node_objects = []
 
     def add_node(w):
-        is_unk = w.tag0 == Unk
-        wid = vocab.get(w.word, 0)
-        mid = vocab.get(w.morph0, 0)
-        tid = vocab.get(w.tag0, 0)
-        m = L.node_mask_from_vocab(int(vmask[wid]), int(vmask[mid]), int(vmask[tid]))
-        if is_unk:
-            m |= L.F_UNK
-        if w.tag0 in CONTEXTUAL_TAGS:
-            m |= L.F_CTX
-        c4, c5, c6 = model.node_local_features(w, is_unk)
-        if c4 is not None:
-            m |= L.F_HAS4
-        if c5 is not None:
-            m |= L.F_HAS5
-        if c6 is not None:
-            m |= L.F_HAS6
+        wid, mid, tid, m, c4, c5, c6 = node_record(model, w)
         p, q = model.node_terms(w)
         words.append(wid)
         morphs.append(mid)

@@ -17,7 +17,8 @@ Each fixture file ``<set>.json.gz`` holds data only:
           float.hex)
   cases:  chars, bindex (Word fields per node), max_len, model name and, per
           beam size, the reference's matures as (node codes, score.hex(),
-          score type) or the exception class name it raised.
+          score type) or the exception class name it raised, and
+          BeamScoreFunctions.evaluate(mature) of each (score.hex(), type).
 Node codes: [b, j] = bindex[b][j] (by identity), ["U", b, e] = synthesised
 Unknown node.
 """
@@ -96,11 +97,17 @@ def run_case(bindex, chars, funcs, max_len=8):
         except Exception as exc:          # the reference's own behaviour is the vector
             out[str(k)] = {'error': type(exc).__name__}
             continue
-        res = []
+        res, evs = [], []
         for m in matures:
             codes = [code_of(w, bindex) for w in m.sequences[1:-1]]
             res.append([codes, float(m.score).hex(), type(m.score).__name__])
-        out[str(k)] = {'matures': res}
+            # BeamScoreFunctions.evaluate of the returned path (score_funcs.py:44-48)
+            try:
+                ev = funcs.evaluate(m)
+                evs.append([float(ev).hex(), type(ev).__name__])
+            except Exception as exc:
+                evs.append({'error': type(exc).__name__})
+        out[str(k)] = {'matures': res, 'evaluate': evs}
     return out
 
 
