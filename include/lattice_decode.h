@@ -78,6 +78,7 @@ lt_status lt_model_create(lt_ctx* ctx, const lt_model_desc* desc, lt_model** out
  * beam/score_funcs.py:106-125).  lt_image_build needs no GPU. */
 typedef struct lt_image lt_image;
 typedef struct {
+  uint32_t hash_version; /* slot hash of the library that built the image */
   int32_t narrow;        /* 1: 16 B slots {key64, coef}; 0: 32 B slots */
   uint32_t seed;         /* cuckoo hash seed */
   int64_t slots;         /* table slots */

@@ -144,7 +144,8 @@ class Context:
 
 
 class ModelImageView(C.Structure):
-    _fields_ = [('narrow', C.c_int32), ('seed', C.c_uint32), ('slots', C.c_int64),
+    _fields_ = [('hash_version', C.c_uint32), ('narrow', C.c_int32), ('seed', C.c_uint32),
+                ('slots', C.c_int64),
                 ('table', C.c_void_p), ('table_bytes', C.c_int64),
                 ('d3mul', C.c_uint32), ('d3', C.c_void_p)]
 
@@ -169,7 +170,8 @@ class ModelImage:
         table = np.frombuffer((C.c_uint8 * v.table_bytes).from_address(v.table), dtype=np.uint8).copy()
         d3 = (np.frombuffer((C.c_double * 1024).from_address(v.d3), dtype=np.float64).copy()
               if v.d3mul else np.zeros(0, dtype=np.float64))
-        return {'narrow': int(v.narrow), 'seed': int(v.seed), 'slots': int(v.slots),
+        return {'hash_version': int(v.hash_version), 'narrow': int(v.narrow), 'seed': int(v.seed),
+                'slots': int(v.slots),
                 'd3mul': int(v.d3mul), 'table': table, 'd3': d3}
 
     def close(self):
@@ -205,7 +207,8 @@ class DeviceModel:
         d3 = np.ascontiguousarray(image['d3'], dtype=np.float64)
         if image['d3mul'] and d3.size != 1024:
             raise ValueError('dense class-3 table must hold 1024 coefficients')
-        v = ModelImageView(int(image['narrow']), int(image['seed']), int(image['slots']),
+        v = ModelImageView(int(image.get('hash_version', 1)), int(image['narrow']),
+                           int(image['seed']), int(image['slots']),
                            table.ctypes.data, table.nbytes, int(image['d3mul']),
                            d3.ctypes.data if image['d3mul'] else None)
         h = C.c_void_p()

@@ -88,17 +88,23 @@ struct lt_model {
 
 namespace {
 
-// Cuckoo table build (two choices, one slot per bucket).  Returns false when
-// the random walk fails; the caller reseeds / grows and retries.
-template <class SlotT>
-KeyBase base_of(const KeyRec& k) {
-  return key_base<sizeof(SlotT) == sizeof(SlotN)>(k.a, k.b, k.c, k.cls);
+// The two candidate slots of a key, as the kernels compute them.
+template <typename SlotT>
+void table_slots(const KeyRec& k, uint32_t seed, const NarrowHash& hk, uint32_t slots, uint32_t& i1,
+                 uint32_t& i2) {
+  if constexpr (sizeof(SlotT) == sizeof(SlotN))
+    narrow_slots(hk, k.a, k.b, k.c, k.cls, slots, i1, i2);
+  else
+    cuckoo_slots(key_base<false>(k.a, k.b, k.c, k.cls), seed, slots, i1, i2);
 }
 
+// Cuckoo table build (two choices, one slot per bucket).  Returns false when
+// the random walk fails; the caller reseeds / grows and retries.
 template <class SlotT>
 bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed,
                   std::vector<SlotT>& tab, int64_t* dup) {
   tab.assign(slots, SlotT{});
+  const NarrowHash hk = narrow_hash(seed);
   std::vector<int32_t> who(slots, -1);          // key index held by each slot
   uint64_t rng = 0x9E3779B97F4A7C15ull ^ seed;
   const int max_kicks = 2000;
@@ -107,7 +113,7 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
     uint32_t i1, i2;
     {
       const KeyRec& k = keys[(size_t)i];
-      cuckoo_slots(base_of<SlotT>(k), seed, slots, i1, i2);
+      table_slots<SlotT>(k, seed, hk, slots, i1, i2);
       for (uint32_t x : {i1, i2}) {
         const int32_t w = who[x];
         if (w >= 0 && keys[(size_t)w].a == k.a && keys[(size_t)w].b == k.b &&
@@ -121,7 +127,7 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
     bool placed = false;
     for (int kick = 0; kick < max_kicks; ++kick) {
       const KeyRec& k = keys[(size_t)cur];
-      cuckoo_slots(base_of<SlotT>(k), seed, slots, i1, i2);
+      table_slots<SlotT>(k, seed, hk, slots, i1, i2);
       uint32_t target;
       if (who[i1] < 0) target = i1;
       else if (who[i2] < 0) target = i2;
@@ -349,6 +355,7 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
 
 lt_status lt_image_view(const lt_image* img, lt_model_image* v) {
   if (!img || !v) return fail(LT_EINVAL, "lt_image_view: NULL argument");
+  v->hash_version = HASH_VERSION;
   v->narrow = img->narrow;
   v->seed = img->seed;
   v->slots = img->slots;
@@ -397,6 +404,9 @@ static lt_status model_upload(lt_ctx* c, const lt_model_image* v, std::vector<Ke
 lt_status lt_model_create_from_image(lt_ctx* c, const lt_model_image* v, lt_model** out) {
   if (!c || !v || !out) return fail(LT_EINVAL, "lt_model_create_from_image: NULL argument");
   *out = nullptr;
+  if (v->hash_version != HASH_VERSION)
+    return fail(LT_EUNSUPPORTED, "model image: hash version %u, this library uses %u (rebuild the image)",
+                v->hash_version, HASH_VERSION);
   if (v->narrow != 0 && v->narrow != 1) return fail(LT_EINVAL, "model image: bad narrow flag");
   if (v->slots < 64 || !v->table) return fail(LT_EINVAL, "model image: empty table");
   const int64_t sb = v->narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
@@ -685,6 +695,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.table = m->d_table;
   p.slots = (uint32_t)m->slots;
   p.seed = m->seed;
+  p.hk = narrow_hash(m->seed);
   lt_status hs = build_hot(c, m, b);
   if (hs != LT_OK) return hs;
   p.hot = (b->hot_uid == m->uid) ? b->d_hot : nullptr;
@@ -794,6 +805,7 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
     p.table = m->d_table;
     p.slots = (uint32_t)m->slots;
     p.seed = m->seed;
+    p.hk = narrow_hash(m->seed);
     p.narrow = m->narrow;
     p.has_tri = d->trigram_pos >= 0 ? 1 : 0;
     p.d3 = m->d_d3;

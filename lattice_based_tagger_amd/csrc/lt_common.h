@@ -101,6 +101,38 @@ LT_HD void cuckoo_slots(KeyBase kb, uint32_t seed, uint32_t slots, uint32_t& i1,
   i2 = slot_of(mix1(kb.b2 ^ (seed * 0x9E3779B1u + 0x632BE5ABu)), slots);
 }
 
+// Narrow tables (ids < 2^20) hash with full-rate 24-bit multiplies only:
+// slot = mulhi(mul24(a,Ka) ^ mul24(b,Kb) ^ mul24(c,Kc) ^ cls*Ks, slots), two
+// independent constant sets derived from the table seed (a failed build
+// reseeds, which changes every constant).  No 32-bit multiply per lookup
+// besides the range reduction (v_mul_u32_u24 is full rate; v_mul_lo_u32 is
+// quarter rate).
+constexpr uint32_t HASH_VERSION = 2;
+struct NarrowHash {
+  uint32_t k1a, k1b, k1c, k1s, k2a, k2b, k2c, k2s;
+};
+LT_HD NarrowHash narrow_hash(uint32_t seed) {
+  uint32_t x = seed;
+  uint32_t v[8];
+  for (int i = 0; i < 8; ++i) {
+    x = x * 0x9E3779B1u + 0x7F4A7C15u;
+    uint32_t y = x ^ (x >> 15);
+    y *= 0x2C1B3C6Du;
+    y ^= y >> 12;
+    y *= 0x297A2D39u;
+    y ^= y >> 15;
+    v[i] = (i == 3 || i == 7) ? (y | 1u) : ((y & 0xFFFFFFu) | 0x800001u);
+  }
+  return NarrowHash{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+}
+LT_HD void narrow_slots(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
+                        uint32_t slots, uint32_t& i1, uint32_t& i2) {
+  const uint32_t b1 = mul24(a, h.k1a) ^ mul24(b, h.k1b) ^ mul24(c, h.k1c) ^ (cls * h.k1s);
+  const uint32_t b2 = mul24(a, h.k2a) ^ mul24(b, h.k2b) ^ mul24(c, h.k2c) ^ (cls * h.k2s);
+  i1 = slot_of(b1, slots);
+  i2 = slot_of(b2, slots);
+}
+
 // Hot-key table: a direct-mapped subset of the model (the keys with the
 // highest estimated probe frequency in a batch), staged in LDS by every
 // block.  Optional: a key missing from it is looked up in the full table.

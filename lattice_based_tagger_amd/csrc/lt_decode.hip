@@ -276,6 +276,7 @@ struct Aux {
   const uint4* hot;       // hot-key table (HOT_SLOTS SlotN) or nullptr
   const double* d3;       // dense class-3 table (D3_DIM^2) or nullptr
   uint32_t d3mul;
+  NarrowHash hk;          // narrow table slot hash
 };
 
 // Key components of probe q for (h, c); recomputed where needed instead of
@@ -343,6 +344,7 @@ __device__ __forceinline__ Aux stage_aux(const DecodeParams& p, uint4* hotl, dou
   a.hot = use_hot ? hotl : nullptr;
   a.d3 = p.d3 ? d3l : nullptr;
   a.d3mul = p.d3mul;
+  a.hk = p.hk;
   return a;
 }
 
@@ -388,7 +390,8 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uin
     // under the same predicate)
     if ((gneed >> q) & 1u) {
       uint32_t i1, i2;
-      cuckoo_slots(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
+      if constexpr (NARROW) narrow_slots(aux.hk, K.a[q], K.b[q], K.c[q], PCLS[q], slots, i1, i2);
+      else cuckoo_slots(key_base<false>(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
       P.s1[q] = T::load(B.tab, i1 * T::SZ);
       P.s2[q] = T::load(B.tab, i2 * T::SZ);
     }
@@ -1005,7 +1008,7 @@ lt_beam_k(DecodeParams p) {
   // the dense class-3 table only where its 8 KiB does not cost a block per CU
   constexpr bool USE_D3 = KT <= 8;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
-  Aux aux{nullptr, nullptr, 0u};
+  Aux aux{nullptr, nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
 
   const int grp = threadIdx.x / G;
@@ -1233,7 +1236,7 @@ lt_beam_pk(DecodeParams p) {
   __shared__ uint32_t tgen[WPB][KT];
   constexpr bool USE_D3 = KT <= 4;              // (its 8 KiB would cost a block per CU above)
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
-  Aux aux{nullptr, nullptr, 0u};
+  Aux aux{nullptr, nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1541,7 +1544,7 @@ static bool beam_v1() {
 template <bool NARROW>
 __global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
   __shared__ double d3l[D3_DIM * D3_DIM];
-  Aux aux{nullptr, nullptr, p.d3mul};
+  Aux aux{nullptr, nullptr, p.d3mul, p.hk};
   if (p.d3) {
     const uint4* src = reinterpret_cast<const uint4*>(p.d3);
     uint4* dst = reinterpret_cast<uint4*>(d3l);

@@ -11,6 +11,7 @@ struct DecodeParams {
   const void* table;            // SlotN[] or SlotW[] (cuckoo, two choices)
   uint32_t slots;
   uint32_t seed;
+  NarrowHash hk;                // narrow tables: slot hash constants (from seed)
   const SlotN* hot;             // HOT_SLOTS-slot LDS hot table (narrow only) or NULL
   const double* d3;             // dense class-3 table (D3_DIM^2) or NULL
   uint32_t d3mul;
@@ -46,6 +47,7 @@ struct EvalParams {
   const void* table;
   uint32_t slots;
   uint32_t seed;
+  NarrowHash hk;
   int32_t narrow;
   int32_t has_tri;
   const double* d3;

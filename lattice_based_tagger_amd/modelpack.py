@@ -96,7 +96,7 @@ def save(path, scorer):
         blobs['table'] = image['table']
         if image['d3mul']:
             blobs['d3'] = image['d3']
-        meta['image'] = {k: image[k] for k in ('narrow', 'seed', 'slots', 'd3mul')}
+        meta['image'] = {k: image[k] for k in ('hash_version', 'narrow', 'seed', 'slots', 'd3mul')}
     entries, payload, off = {}, [], 0
     for name, b in blobs.items():
         raw = b if isinstance(b, bytes) else b.tobytes()
