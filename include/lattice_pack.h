@@ -1,0 +1,96 @@
+/* lattice_pack.h -- C-ABI of the native lattice packer (liblt.so).
+ *
+ * the lattice -> device-batch step in front of
+ * lt_batch_create.  It replaces, for whole corpora at once, what the reference
+ * decoder does with its inputs on every call:
+ *   - candidate gathering per span and Unknown-word synthesis
+ *     (lattice_tagger/beam/beam.py:25-38, from the bindex of
+ *     dictionary/lookup.py:344-369),
+ *   - the node-local scorers RegularizationScore / MorphemePreferenceScore /
+ *     WordPreferenceScore (beam/score_funcs.py:65-73, 84-88, 99-100) summed
+ *     in constructor order (score_funcs.py:50-54),
+ *   - the node-local trigram feature classes 4, 5, 6 (features/feature.py:95-110)
+ *     and the exact-membership pre-filter of the probed classes,
+ *   - string interning of word / morpheme / tag values (and of the Unknown
+ *     surfaces chars[b:e]) against the model's feature vocabulary.
+ * The output arrays are exactly lt_batch_desc's (include/lattice_decode.h).
+ *
+ * Strings are UTF-8; a string table is a blob plus n+1 byte offsets.  A
+ * "nullable" table marks None with off[i] == off[i+1] and null[i] = 1.
+ */
+#ifndef LATTICE_PACK_H
+#define LATTICE_PACK_H
+
+#include <stdint.h>
+#include "lattice_decode.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  const char* data;
+  const int64_t* off;      /* [n + 1] */
+  const uint8_t* null;     /* [n] or NULL (no None entries) */
+  int64_t n;
+} lt_strings;
+
+enum { LT_SCORER_REGULARIZATION = 0, LT_SCORER_MORPH_PREF = 1, LT_SCORER_WORD_PREF = 2 };
+
+/* The lowered scorer composite (lattice_based_tagger_amd/lowering.py). */
+typedef struct {
+  /* feature vocabulary: string vocab[i] has id vocab_id[i] (>= 1) */
+  lt_strings vocab;
+  const int32_t* vocab_id;
+  const uint32_t* vmask;         /* [n_vmask] key-slot bits per id */
+  int64_t n_vmask;
+  /* node-local feature classes (key -> coefficient) */
+  int64_t n4; const int64_t* c4_len; const double* c4_coef;        /* (4, len) */
+  int64_t n6; const int64_t* c6_len; const double* c6_coef;        /* (6, min(8, len)) */
+  lt_strings c5_word; lt_strings c5_tag; const int64_t* c5_isl;    /* (5, word, tag0, is_l) */
+  const double* c5_coef;
+  /* node-local scorers in constructor order; the first n_pre precede the
+   * trigram scorer (summed into `pre`), the rest are separate `post` terms */
+  int32_t n_local;
+  const int32_t* local_kind;     /* LT_SCORER_* */
+  const double* reg_params;      /* [3 * n_local]: unknown_penalty, known_preference, syllable_penalty */
+  int32_t n_pre;
+  /* preference tables: entry i belongs to scorer pref_scorer[i]:
+   * kind MORPH_PREF: (tag, morph) -> value; kind WORD_PREF: (tag, word) -> value */
+  lt_strings pref_tag; lt_strings pref_key;
+  const int32_t* pref_scorer; const double* pref_value;
+} lt_packer_desc;
+
+/* Lattices: sentence s has n_s = char_off[s+1] - char_off[s] characters
+ * (UTF-32 code points); begin slot g = char_off[s] + b holds the words
+ * [slot_off[g], slot_off[g+1]) in bindex order. */
+typedef struct {
+  int32_t n_sent;
+  const uint32_t* chars;         /* [char_off[n_sent]] */
+  const int64_t* char_off;       /* [n_sent + 1] */
+  const int64_t* slot_off;       /* [char_off[n_sent] + 1] */
+  int64_t n_words;
+  lt_strings word, morph0, tag0, morph1, tag1;   /* morph1 / tag1 nullable */
+  const int64_t* len;
+  const int64_t* e;              /* end position; a non-integral e is -1 (matches no span) */
+  const int64_t* is_l;
+} lt_lattice_desc;
+
+/* Packed batch (library-owned arrays, valid until the next pack or destroy).
+ * node_src: >= 0 dictionary word index, -1 BOS, -2 - (8 b + d - 1) Unknown
+ * node of span (b, b + d). */
+typedef struct {
+  lt_batch_desc batch;
+  const int64_t* node_src;
+} lt_packed;
+
+typedef struct lt_packer lt_packer;
+lt_status lt_packer_create(const lt_packer_desc* desc, lt_packer** out);
+lt_status lt_packer_destroy(lt_packer* packer);
+/* max_len as beam_search's (1..8).  Host only; no GPU needed. */
+lt_status lt_packer_pack(lt_packer* packer, const lt_lattice_desc* lattices, int max_len, lt_packed* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LATTICE_PACK_H */

@@ -14,6 +14,8 @@ high-throughput entry point.
 
 import weakref
 
+import os
+
 import numpy as np
 
 from . import _capi
@@ -140,6 +142,20 @@ class Decoder:
             db.close()
 
 
+def pack_lattices(sentences, model, max_len):
+    """Native packer (``native_packer``) when the model and lattices are
+    representable there, else the Python packer -- identical results."""
+    if os.environ.get('LT_NATIVE_PACK', '1') != '0':
+        from .native_packer import packer_for, Unsupported
+        npk = packer_for(model)
+        if npk is not None:
+            try:
+                return npk.pack(sentences, max_len)
+            except Unsupported:
+                pass
+    return pack(sentences, model, max_len)
+
+
 def _check_beam(beam_size):
     k = int(beam_size)
     if k < 0:
@@ -155,7 +171,7 @@ def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device
     sentences = list(sentences)
     k = _check_beam(beam_size)
     model = lowered_model(score_functions)
-    packed, objs = pack(sentences, model, max_len)
+    packed, objs = pack_lattices(sentences, model, max_len)
     if k == 0:
         # beam_size=0 keeps no hypothesis past BOS (beam.py:85 slices to [])
         return [[Sequence([bos_word(), eos_word(0)], 0)] if len(ch) == 0 else []

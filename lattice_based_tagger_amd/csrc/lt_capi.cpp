@@ -18,6 +18,7 @@
 #include "../../include/lattice_decode.h"
 #include "lt_common.h"
 #include "lt_internal.h"
+#include "lt_error.h"
 
 using namespace lt;
 
@@ -34,6 +35,20 @@ lt_status fail(lt_status st, const char* fmt, ...) {
   g_err = buf;
   return st;
 }
+
+}  // namespace
+
+lt_status lt::set_error(lt_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+namespace {
 
 #define HIP_TRY(expr)                                                          \
   do {                                                                         \

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define LT_HD __host__ __device__ __forceinline__
 #else
 #define LT_HD static inline

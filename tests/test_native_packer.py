@@ -1,0 +1,84 @@
+"""Native packer (include/lattice_pack.h): its arrays equal
+the Python packer's bit for bit on every golden set and on synthetic corpora,
+and its node views re-materialise the same Word objects."""
+
+import numpy as np
+import pytest
+
+from golden_io import SETS, load
+from lattice_based_tagger_amd import synth, score_funcs as SF, feature as FE
+from lattice_based_tagger_amd.beam import lowered_model
+from lattice_based_tagger_amd.native_packer import NativePacker, Unsupported
+from lattice_based_tagger_amd.packer import pack
+
+FIELDS = ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start', 'node_word', 'node_morph0',
+          'node_tag', 'node_mask', 'node_pre', 'node_f4', 'node_f5', 'node_f6', 'node_post')
+
+
+def _same(a, b):
+    for f in FIELDS:
+        x, y = getattr(a, f), getattr(b, f)
+        assert x.shape == y.shape, f
+        if x.dtype.kind == 'f':
+            assert np.array_equal(x.view(np.uint64), y.astype(np.float64).view(np.uint64)), f
+        else:
+            assert np.array_equal(x, y), f
+    assert (a.n_post, a.has_trigram, a.max_len) == (b.n_post, b.has_trigram, b.max_len)
+
+
+def _check(sentences, funcs, max_len):
+    model = lowered_model(funcs)
+    ref, objs = pack(sentences, model, max_len)
+    got, views = NativePacker(model).pack(sentences, max_len)
+    _same(got, ref)
+    for o, v in zip(objs, views):
+        assert len(o) == len(v)
+        for i, w in enumerate(o):
+            x = v[i]
+            if i == 0:
+                assert tuple(x) == tuple(w)
+            elif w.tag0 == 'Unknown' and x is not w:
+                assert tuple(x) == tuple(w)
+            else:
+                assert x is w
+
+
+@pytest.mark.parametrize('name', SETS)
+def test_native_matches_python_on_golden(name):
+    groups = {}
+    for c in load(name):
+        groups.setdefault((id(c.funcs), c.max_len), []).append(c)
+    for group in groups.values():
+        ok = [c for c in group if len(c.bindex) >= len(c.chars)]
+        if ok:
+            _check([(c.bindex, c.chars) for c in ok], ok[0].funcs, ok[0].max_len)
+
+
+@pytest.mark.parametrize('threads', ['1', '5'])
+def test_native_matches_python_on_synthetic(monkeypatch, threads):
+    monkeypatch.setenv('LT_PACK_THREADS', threads)
+    raw = synth.make_lattices(300, seed=5, extra_lambda=2.0, dup_rate=0.4)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=5, n_features=50_000)
+    dic, coef = synth.render_model(raw, sm)
+    funcs = SF.BeamScoreFunctions(
+        SF.MorphemePreferenceScore({'Noun': {'x': 1.5}}),
+        SF.RegularizationScore(),
+        SF.SimpleTrigramFeatureScore(FE.SimpleTrigramEncoder(dic), coef),
+        SF.WordPreferenceScore({'Verb': {'y': -0.25}}))
+    sents = synth.render_sentences(raw, range(raw.S))
+    for max_len in (8, 3):
+        _check(sents, funcs, max_len)
+
+
+def test_unsupported_inputs_are_refused():
+    from lattice_based_tagger_amd.word import Word
+    funcs = SF.BeamScoreFunctions(SF.RegularizationScore())
+    npk = NativePacker(lowered_model(funcs))
+    with pytest.raises(Unsupported):
+        npk.pack([([[Word('a', 'a', None, 'Noun', None, 1.5, 0, 1, False)]], 'a')])
+    with pytest.raises(Unsupported):
+        npk.pack([([[Word(3, 'a', None, 'Noun', None, 1, 0, 1, False)]], 'a')])
+    with pytest.raises(Unsupported):
+        NativePacker(lowered_model(SF.BeamScoreFunctions(SF.WordPreferenceScore({'Noun': {1: 2.0}}))))
