@@ -49,6 +49,9 @@ def parse():
                     help='budget of the pure-Python CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--gather', type=int, default=None,
+                    help='1: gather every rank\'s results to rank 0 with RCCL inside each step '
+                         '(default: on when WORLD_SIZE > 1)')
     return ap.parse_args()
 
 
@@ -87,6 +90,14 @@ class Dist:
         t = torch.tensor([v], dtype=torch.float64)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
         return float(t.item())
+
+    def broadcast_bytes(self, data):
+        """Rank 0's bytes on every rank (gloo; host only)."""
+        if not self.pg:
+            return data
+        obj = [data]
+        self.pg.broadcast_object_list(obj, src=0)
+        return obj[0]
 
     def close(self):
         if self.pg:
@@ -212,19 +223,36 @@ def main():
     t_up = time.perf_counter() - t_up
     expansions, tuples, probes = db.count_ops(dm, a.k)
 
-    for _ in range(a.warmup):
+    # result gather to rank 0 over RCCL/xGMI (the path's one exchange step)
+    gather = d.world > 1 if a.gather is None else bool(a.gather)
+    comm = None
+    if gather:
+        uid = d.broadcast_bytes(_capi.comm_unique_id() if d.rank == 0 else None)
+        comm = _capi.Comm(ctx, d.world, d.rank, uid)
+        comm.prepare(db, a.k, root=0)
+
+    def step():
         db.launch(dm, a.k)
+        if comm:
+            comm.launch(db)
         ctx.sync()
+
+    for _ in range(max(1, a.warmup)):
+        step()
 
     d.barrier()
     ctx.sync()
-    kern_ms = []
+    kern_ms, gather_ms = [], []
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        db.launch(dm, a.k)
-        ctx.sync()
+        step()
         kern_ms.append(ctx.kernel_ms())
+    if comm:
+        comm.sync()
+        gather_ms.append(comm.gather_ms())
     ctx.sync()
+    if comm:
+        comm.sync()
     t1 = time.perf_counter()
     d.barrier()
     elapsed = d.max(t1 - t0)
@@ -242,6 +270,28 @@ def main():
     pcie_rate = d.sum(float(a.sentences * pcie_steps)) / d.max(tp)
 
     count, length, score, codes = db.results(a.k)
+    gather_info = None
+    if comm:
+        # the last gather delivered every rank's results of the same batch
+        step()
+        db.fetch()
+        ctx.sync()
+        comm.sync()
+        count, length, score, codes = db.results(a.k)
+        if d.rank == 0:
+            comm.fetch()
+            ctx.sync()
+            g0 = comm.view(0)
+            for x, y in zip(g0, (count, length, score, codes)):
+                assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8)), \
+                    'gathered rank-0 block differs from the local results'
+            got = [comm.view(r) for r in range(d.world)]
+            assert all(int(g[0].shape[0]) == a.sentences and int((g[0] > 0).sum()) == a.sentences
+                       for g in got), 'gathered result blocks incomplete'
+        gather_info = {'collective': 'ncclGather x4 in one group (RCCL), root 0, on its own '
+                                     'stream: gather of step i overlaps decode of step i+1',
+                       'last_gather_ms': float(np.mean(gather_ms)) if gather_ms else None,
+                       'in_timed_region': True}
     kernel = (lib.lt_kernel_name(a.k) or b'?').decode()
     traffic = traffic_from_profiles(kernel, a.k, a.sentences, a.features, a.seed)
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
@@ -291,6 +341,7 @@ def main():
                                'table_probes': probes},
             'kernel_only_sentences_per_s': a.sentences / avg_kernel_s,
             'pcie_inclusive_sentences_per_s': pcie_rate,
+            'gather': gather_info,
             'host': {'gen_s': t_gen, 'h2d_s': t_up, 'nproc': os.cpu_count(), 'cpu': cpu_model()},
         }
         if not a.no_cpu_baseline and d.world == 1:
@@ -299,6 +350,8 @@ def main():
         else:
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)
+    if comm:
+        comm.close()
     db.close()
     dm.close()
     ctx.close()

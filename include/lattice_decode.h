@@ -175,6 +175,45 @@ lt_status lt_decode(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k, 
 lt_status lt_count_ops(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k,
                        int64_t* expansions, int64_t* feature_tuples, int64_t* probes);
 
+/* ---- multi-GPU result gather --------------------------------
+ * One process per GPU decodes its own shard of sentences: sentences are
+ * independent (beam_search keeps no cross-sentence state, beam.py:5-61, and
+ * Tagger.tag is per sentence, tagger.py:68-78), so the only exchange is one
+ * RCCL gather of every rank's decode results to a root rank over xGMI.
+ * RCCL is loaded on first use (dlopen of ROCm's librccl); the root's unique
+ * id travels between the processes through the caller (e.g. a gloo
+ * broadcast).  lt_comm_create, lt_gather_prepare and lt_gather_launch are
+ * collective: every rank of the communicator calls them in the same
+ * order. */
+#define LT_COMM_ID_BYTES 128
+typedef struct lt_comm lt_comm;
+/* Fresh communicator id (call on one rank, share with the others). */
+lt_status lt_comm_unique_id(uint8_t id[LT_COMM_ID_BYTES]);
+lt_status lt_comm_create(lt_ctx* ctx, int nranks, int rank, const uint8_t id[LT_COMM_ID_BYTES],
+                         lt_comm** out);
+lt_status lt_comm_destroy(lt_comm* comm);
+/* Agree on every rank's result sizes for beam k (<= the batch's max_k) and
+ * allocate two padded send slots (and, on the root, two receive slots).
+ * Blocking. */
+lt_status lt_gather_prepare(lt_comm* comm, lt_batch* batch, int k, int root);
+/* Gather the last decode's results (beam k of the prepare) to the root:
+ * a device copy into the next send slot on the ctx stream, then one RCCL
+ * group of four ncclGather calls (count, length, score, codes) on the
+ * communicator's own stream -- so the next decode on the ctx stream overlaps
+ * this gather.  Complete after lt_gather_sync. */
+lt_status lt_gather_launch(lt_comm* comm, lt_batch* batch);
+/* Wait for this rank's outstanding gathers (local, not collective). */
+lt_status lt_gather_sync(lt_comm* comm);
+/* Root only: D2H of the last gathered block into pinned host buffers (async
+ * on the ctx stream, after the gather; complete after lt_sync). */
+lt_status lt_gather_fetch(lt_comm* comm);
+/* Root only: rank r's results in the lt_result layout for beam k (host
+ * pointers valid until the next fetch), its sentence count and code slots. */
+lt_status lt_gather_view(lt_comm* comm, int r, lt_result* view, int32_t* n_sent, int64_t* code_slots);
+/* Device time of the last lt_gather_launch (HIP events around the RCCL
+ * group on the communicator stream), ms.  Valid after lt_gather_sync. */
+lt_status lt_last_gather_ms(lt_comm* comm, float* ms);
+
 /* ---- evaluate -------------------------------------------
  * Batch form of BeamScoreFunctions.evaluate(seq) (score_funcs.py:44-48) for
  * given paths (e.g. gold sequences):

@@ -18,8 +18,8 @@ ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = 'gfx950'
 
-SOURCES = ['lt_decode.hip', 'lt_capi.cpp', 'lt_packer.cpp']
-HEADERS = ['lt_common.h', 'lt_internal.h', 'lt_error.h', os.path.join('..', '..', 'include', 'lattice_decode.h'),
+SOURCES = ['lt_decode.hip', 'lt_capi.cpp', 'lt_packer.cpp', 'lt_comm.cpp']
+HEADERS = ['lt_common.h', 'lt_internal.h', 'lt_error.h', 'lt_handles.h', os.path.join('..', '..', 'include', 'lattice_decode.h'),
            os.path.join('..', '..', 'include', 'lattice_pack.h')]
 
 COMMON_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
@@ -53,7 +53,7 @@ def build(force=False, verbose=True, defines=(), out=None):
         objs.append(obj)
     tmp = lib + '.tmp'
     cmd = [HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', tmp] + objs + [
-        '-Wl,-rpath,' + os.path.join(ROCM, 'lib'), '-Wl,--no-undefined']
+        '-Wl,-rpath,' + os.path.join(ROCM, 'lib'), '-ldl', '-Wl,--no-undefined']
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -23,7 +23,10 @@ EXPORTED_SYMBOLS = (
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
     'lt_image_build', 'lt_image_view', 'lt_image_destroy', 'lt_model_create_from_image',
     'lt_evaluate',
+    'lt_comm_unique_id', 'lt_comm_create', 'lt_comm_destroy', 'lt_gather_prepare',
+    'lt_gather_launch', 'lt_gather_sync', 'lt_gather_fetch', 'lt_gather_view', 'lt_last_gather_ms',
 )
+LT_COMM_ID_BYTES = 128
 
 
 class LTError(RuntimeError):
@@ -93,6 +96,16 @@ def load(path=None):
             'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),
             'lt_count_ops': (i32, [vp, vp, vp, C.c_int, C.POINTER(i64), C.POINTER(i64),
                                    C.POINTER(i64)]),
+            'lt_comm_unique_id': (i32, [C.c_char_p]),
+            'lt_comm_create': (i32, [vp, C.c_int, C.c_int, C.c_char_p, C.POINTER(vp)]),
+            'lt_comm_destroy': (i32, [vp]),
+            'lt_gather_prepare': (i32, [vp, vp, C.c_int, C.c_int]),
+            'lt_gather_launch': (i32, [vp, vp]),
+            'lt_gather_sync': (i32, [vp]),
+            'lt_gather_fetch': (i32, [vp]),
+            'lt_gather_view': (i32, [vp, C.c_int, C.POINTER(Result), C.POINTER(i32),
+                                     C.POINTER(i64)]),
+            'lt_last_gather_ms': (i32, [vp, C.POINTER(C.c_float)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -295,6 +308,73 @@ class DeviceBatch:
     def close(self):
         if self.handle:
             self.ctx._lib.lt_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id():
+    """A fresh RCCL communicator id (bytes) -- created on one rank, shared
+    with the others by the caller (e.g. a gloo broadcast)."""
+    buf = C.create_string_buffer(LT_COMM_ID_BYTES)
+    check(load().lt_comm_unique_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """RCCL communicator of one rank (lt_comm): gathers every rank's decode
+    results to a root rank (include/lattice_decode.h, "multi-GPU result
+    gather").  All methods but ``view``/``gather_ms`` are collective."""
+
+    def __init__(self, ctx, nranks, rank, uid):
+        if len(uid) != LT_COMM_ID_BYTES:
+            raise ValueError('communicator id must be %d bytes' % LT_COMM_ID_BYTES)
+        h = C.c_void_p()
+        check(ctx._lib.lt_comm_create(ctx.handle, int(nranks), int(rank), bytes(uid), C.byref(h)))
+        self.handle, self.ctx = h, ctx
+        self.nranks, self.rank = int(nranks), int(rank)
+        self.k = 0
+
+    def prepare(self, batch, k, root=0):
+        check(self.ctx._lib.lt_gather_prepare(self.handle, batch.handle, int(k), int(root)))
+        self.k, self.root = int(k), int(root)
+
+    def launch(self, batch):
+        check(self.ctx._lib.lt_gather_launch(self.handle, batch.handle))
+
+    def sync(self):
+        check(self.ctx._lib.lt_gather_sync(self.handle))
+
+    def fetch(self):
+        check(self.ctx._lib.lt_gather_fetch(self.handle))
+
+    def gather_ms(self):
+        v = C.c_float()
+        check(self.ctx._lib.lt_last_gather_ms(self.handle, C.byref(v)))
+        return float(v.value)
+
+    def view(self, r):
+        """Root, after fetch + sync: numpy copies of rank r's (count, length,
+        score, codes), shaped as ``DeviceBatch.results``."""
+        v = Result()
+        S, slots = C.c_int32(), C.c_int64()
+        check(self.ctx._lib.lt_gather_view(self.handle, int(r), C.byref(v), C.byref(S), C.byref(slots)))
+        S, nc, k = S.value, slots.value, self.k
+
+        def arr(p, n, dt):
+            if n == 0:
+                return np.zeros(0, dtype=dt)
+            return np.ctypeslib.as_array(p, shape=(n,)).copy()
+        return (arr(v.count, S, np.int32), arr(v.length, S * k, np.int32).reshape(S, k),
+                arr(v.score, S * k, np.float64).reshape(S, k), arr(v.codes, nc, np.int32))
+
+    def close(self):
+        if self.handle:
+            self.ctx._lib.lt_comm_destroy(self.handle)
             self.handle = None
 
     def __del__(self):

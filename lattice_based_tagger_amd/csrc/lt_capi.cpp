@@ -19,6 +19,7 @@
 #include "lt_common.h"
 #include "lt_internal.h"
 #include "lt_error.h"
+#include "lt_handles.h"
 
 using namespace lt;
 
@@ -73,12 +74,6 @@ void dfree(void* p) {
 
 }  // namespace
 
-struct lt_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  unsigned long long* d_counters = nullptr;
-};
 
 namespace {
 
@@ -175,29 +170,6 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
 
 }  // namespace
 
-struct lt_batch {
-  lt_ctx* ctx = nullptr;
-  int32_t n_sent = 0, max_len = 8, n_post = 0, has_tri = 0, max_k = 1;
-  int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
-  int last_k = 0;
-  // device inputs
-  int32_t *d_order = nullptr, *d_sent_n = nullptr, *d_span_start = nullptr;
-  int64_t *d_node_off = nullptr, *d_span_off = nullptr, *d_bp_off = nullptr, *d_cum_n = nullptr;
-  NodeRec* d_nodes = nullptr;
-  double* d_post = nullptr;
-  // scratch + device results (sized for max_k)
-  uint32_t* d_bp = nullptr;
-  int32_t *d_count = nullptr, *d_len = nullptr, *d_codes = nullptr;
-  double* d_score = nullptr;
-  // pinned host results
-  int32_t *h_count = nullptr, *h_len = nullptr, *h_codes = nullptr;
-  double* h_score = nullptr;
-  // component frequencies of the batch's nodes (ids < 2^20) and the hot table
-  // built for the last model decoded with this batch
-  std::vector<uint32_t> f_word, f_tag, f_morph;
-  uint64_t hot_uid = 0;      // lt_model::uid the hot table was built for (0: none)
-  SlotN* d_hot = nullptr;
-};
 
 extern "C" {
 

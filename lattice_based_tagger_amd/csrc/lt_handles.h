@@ -1,0 +1,40 @@
+// lt_handles.h -- definitions of the opaque C-ABI handles shared by the
+// host-side translation units of liblt.so (lt_capi.cpp, lt_comm.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "lt_common.h"
+
+struct lt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  unsigned long long* d_counters = nullptr;
+};
+
+struct lt_batch {
+  lt_ctx* ctx = nullptr;
+  int32_t n_sent = 0, max_len = 8, n_post = 0, has_tri = 0, max_k = 1;
+  int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
+  int last_k = 0;
+  // device inputs
+  int32_t *d_order = nullptr, *d_sent_n = nullptr, *d_span_start = nullptr;
+  int64_t *d_node_off = nullptr, *d_span_off = nullptr, *d_bp_off = nullptr, *d_cum_n = nullptr;
+  lt::NodeRec* d_nodes = nullptr;
+  double* d_post = nullptr;
+  // scratch + device results (sized for max_k)
+  uint32_t* d_bp = nullptr;
+  int32_t *d_count = nullptr, *d_len = nullptr, *d_codes = nullptr;
+  double* d_score = nullptr;
+  // pinned host results
+  int32_t *h_count = nullptr, *h_len = nullptr, *h_codes = nullptr;
+  double* h_score = nullptr;
+  // component frequencies of the batch's nodes (ids < 2^20) and the hot table
+  // built for the last model decoded with this batch
+  std::vector<uint32_t> f_word, f_tag, f_morph;
+  uint64_t hot_uid = 0;      // lt_model::uid the hot table was built for (0: none)
+  lt::SlotN* d_hot = nullptr;
+};

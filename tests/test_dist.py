@@ -77,3 +77,29 @@ def test_two_rank_gloo_shards_reassemble():
         p.join(timeout=180)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) is True
+
+
+def _id_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    d = bench.Dist(world)
+    uid = bytes(range(128)) if rank == 0 else None       # stands in for lt_comm_unique_id()
+    got = d.broadcast_bytes(uid)
+    out_q.put((rank, got == bytes(range(128)), d.max(float(rank)), d.sum(1.0)))
+    d.close()
+
+
+def test_bench_dist_shares_the_communicator_id():
+    """bench.py's host group hands rank 0's RCCL id to every rank (gloo)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_id_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert res == [(0, True, 1.0, 2.0), (1, True, 1.0, 2.0)]
