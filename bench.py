@@ -209,8 +209,8 @@ def cpu_model():
 
 def main():
     a = parse()
+    lib = _capi.load()          # liblt binds its HIP runtime before torch (gloo) is imported
     d = Dist(a.gpus)
-    lib = _capi.load()
     if lib.lt_device_count() < 1:
         raise SystemExit('bench.py: no HIP device visible')
     t_gen = time.perf_counter()
@@ -290,6 +290,7 @@ def main():
                        for g in got), 'gathered result blocks incomplete'
         gather_info = {'collective': 'ncclGather x4 in one group (RCCL), root 0, on its own '
                                      'stream: gather of step i overlaps decode of step i+1',
+                       'rccl': (lib.lt_comm_library() or b'?').decode(),
                        'last_gather_ms': float(np.mean(gather_ms)) if gather_ms else None,
                        'in_timed_region': True}
     kernel = (lib.lt_kernel_name(a.k) or b'?').decode()

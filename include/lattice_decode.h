@@ -187,6 +187,9 @@ lt_status lt_count_ops(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int 
  * order. */
 #define LT_COMM_ID_BYTES 128
 typedef struct lt_comm lt_comm;
+/* Path of the RCCL library in use (the one next to the HIP runtime this
+ * library is bound to), loading it if needed; NULL if none loads. */
+const char* lt_comm_library(void);
 /* Fresh communicator id (call on one rank, share with the others). */
 lt_status lt_comm_unique_id(uint8_t id[LT_COMM_ID_BYTES]);
 lt_status lt_comm_create(lt_ctx* ctx, int nranks, int rank, const uint8_t id[LT_COMM_ID_BYTES],

@@ -23,7 +23,7 @@ EXPORTED_SYMBOLS = (
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
     'lt_image_build', 'lt_image_view', 'lt_image_destroy', 'lt_model_create_from_image',
     'lt_evaluate',
-    'lt_comm_unique_id', 'lt_comm_create', 'lt_comm_destroy', 'lt_gather_prepare',
+    'lt_comm_library', 'lt_comm_unique_id', 'lt_comm_create', 'lt_comm_destroy', 'lt_gather_prepare',
     'lt_gather_launch', 'lt_gather_sync', 'lt_gather_fetch', 'lt_gather_view', 'lt_last_gather_ms',
 )
 LT_COMM_ID_BYTES = 128
@@ -96,6 +96,7 @@ def load(path=None):
             'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),
             'lt_count_ops': (i32, [vp, vp, vp, C.c_int, C.POINTER(i64), C.POINTER(i64),
                                    C.POINTER(i64)]),
+            'lt_comm_library': (C.c_char_p, []),
             'lt_comm_unique_id': (i32, [C.c_char_p]),
             'lt_comm_create': (i32, [vp, C.c_int, C.c_int, C.c_char_p, C.POINTER(vp)]),
             'lt_comm_destroy': (i32, [vp]),

@@ -34,7 +34,7 @@ namespace {
 
 struct Rccl {
   bool ok = false;
-  std::string why;
+  std::string why, path;
   ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
@@ -49,17 +49,39 @@ const Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
+    // RCCL must run on the HIP runtime this library is bound to: a process
+    // that imported PyTorch-ROCm first has bound liblt to torch's bundled
+    // libamdhip64 (same soname), so take the librccl next to whichever
+    // libamdhip64 provides the HIP API (an already-loaded one is reused), then
+    // ROCm's.  RTLD_DEEPBIND keeps a freshly loaded RCCL on its own symbols
+    // when another RCCL is already in the process.
     std::vector<std::string> names;
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void*>(&hipGetDeviceCount), &info) && info.dli_fname) {
+      std::string dir(info.dli_fname);
+      const size_t slash = dir.rfind('/');
+      if (slash != std::string::npos) {
+        dir.resize(slash);
+        names.push_back(dir + "/librccl.so.1");
+        names.push_back(dir + "/librccl.so");
+      }
+    }
     if (const char* p = std::getenv("ROCM_PATH")) names.push_back(std::string(p) + "/lib/librccl.so.1");
     names.push_back("/opt/rocm/lib/librccl.so.1");
-    names.push_back("librccl.so.1");
     void* h = nullptr;
-    for (const std::string& n : names)
-      if ((h = dlopen(n.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+    for (const std::string& n : names) {
+      if ((h = dlopen(n.c_str(), RTLD_NOW | RTLD_NOLOAD))) break;             // already in the process
+      if ((h = dlopen(n.c_str(), RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND))) break;
+    }
     if (!h) {
       const char* e = dlerror();
-      r.why = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+      r.why = std::string("cannot load librccl: ") + (e ? e : "?");
       return;
+    }
+    {
+      Dl_info li;
+      void* f = dlsym(h, "ncclGetUniqueId");
+      r.path = (f && dladdr(f, &li) && li.dli_fname) ? li.dli_fname : "?";
     }
     bool all = true;
     auto sym = [&](auto& fn, const char* name) {
@@ -189,6 +211,11 @@ lt_status lt_comm_unique_id(uint8_t id[LT_COMM_ID_BYTES]) {
   NCCL_TRY(r.get_unique_id(&u));
   memcpy(id, &u, sizeof u);
   return LT_OK;
+}
+
+const char* lt_comm_library(void) {
+  const Rccl& r = rccl();
+  return r.ok ? r.path.c_str() : nullptr;
 }
 
 lt_status lt_comm_create(lt_ctx* ctx, int nranks, int rank, const uint8_t id[LT_COMM_ID_BYTES],
