@@ -18,9 +18,10 @@ ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = 'gfx950'
 
-SOURCES = ['lt_decode.hip', 'lt_capi.cpp', 'lt_packer.cpp', 'lt_comm.cpp']
+SOURCES = ['lt_decode.hip', 'lt_capi.cpp', 'lt_packer.cpp', 'lt_comm.cpp', 'lt_lookup.cpp']
 HEADERS = ['lt_common.h', 'lt_internal.h', 'lt_error.h', 'lt_handles.h', os.path.join('..', '..', 'include', 'lattice_decode.h'),
-           os.path.join('..', '..', 'include', 'lattice_pack.h')]
+           os.path.join('..', '..', 'include', 'lattice_pack.h'),
+           os.path.join('..', '..', 'include', 'lattice_lookup.h')]
 
 COMMON_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
                 '-Wall', '-Wno-unused-result', '-I' + os.path.join(HERE, '..', 'include')]

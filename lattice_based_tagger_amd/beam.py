@@ -172,13 +172,19 @@ def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device
     k = _check_beam(beam_size)
     model = lowered_model(score_functions)
     packed, objs = pack_lattices(sentences, model, max_len)
+    return decode_batch(packed, objs, [ch for _, ch in sentences], model, k, device)
+
+
+def decode_batch(packed, objs, chars_list, model, k, device=0):
+    """Decode a packed batch and re-materialise the matures: ``objs[s][i]`` is
+    the Word of sentence s's local node i, ``chars_list[s]`` its characters."""
     if k == 0:
         # beam_size=0 keeps no hypothesis past BOS (beam.py:85 slices to [])
         return [[Sequence([bos_word(), eos_word(0)], 0)] if len(ch) == 0 else []
-                for _, ch in sentences]
+                for ch in chars_list]
     count, length, score, codes, cum_n = Decoder.get(device).decode_packed(model, packed, k)
     out = []
-    for s, (_, chars) in enumerate(sentences):
+    for s, chars in enumerate(chars_list):
         n = len(chars)
         nodes = objs[s]
         base = k * int(cum_n[s])

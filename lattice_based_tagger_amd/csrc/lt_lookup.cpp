@@ -1,0 +1,745 @@
+// lt_lookup.cpp -- native lattice builder (include/lattice_lookup.h).
+//
+// Restates, over UTF-32 code points and for whole corpora at once, the
+// reference's lattice construction that Tagger.tag runs before beam_search
+// (lattice_tagger/tagger/tagger.py:72-74):
+//   sentence_lookup_as_begin_index   lookup.py:52-62, 358-369
+//   morpheme_lookup                  lookup.py:212-279
+//   lr_lookup                        lookup.py:171-210
+//   MorphemeDictionary.lookup/check  dictionary.py:230-242, 304-315
+//   analyze_morphology               lemmatizer.py:5-51
+//   get_lemma_candidates             lemmatizer.py:53-112
+// Node order is the reference's: lookup order within an eojeol, eojeols in
+// sentence order, then a stable grouping by begin position.
+//
+// One string table keys everything the lookup asks a dictionary about: a
+// string's tag bits (get_tags / check), its verb / adjective / eomi
+// membership (analyze_morphology) and its rule pairs (rules.get), so each
+// probe of a substring or candidate is one hash lookup.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/lattice_lookup.h"
+#include "lt_error.h"
+
+namespace {
+
+// ------------------------------------------------------- CPython str hash --
+// CPython 3.10 hashes a str as SipHash-2-4 (Python/pyhash.c) of its canonical
+// storage: 1, 2 or 4 bytes per code point by the string's largest code point
+// (Objects/unicodeobject.c unicode_hash -> _Py_HashBytes); -1 maps to -2.
+inline uint64_t rotl(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+
+inline void half_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, int s, int t) {
+  a += b;
+  c += d;
+  b = rotl(b, s) ^ a;
+  d = rotl(d, t) ^ c;
+  a = rotl(a, 32);
+}
+
+inline void double_round(uint64_t& v0, uint64_t& v1, uint64_t& v2, uint64_t& v3) {
+  half_round(v0, v1, v2, v3, 13, 16);
+  half_round(v2, v1, v0, v3, 17, 21);
+  half_round(v0, v1, v2, v3, 13, 16);
+  half_round(v2, v1, v0, v3, 17, 21);
+}
+
+uint64_t siphash24(uint64_t k0, uint64_t k1, const uint8_t* in, size_t sz) {
+  uint64_t b = (uint64_t)sz << 56;
+  uint64_t v0 = k0 ^ 0x736f6d6570736575ULL;
+  uint64_t v1 = k1 ^ 0x646f72616e646f6dULL;
+  uint64_t v2 = k0 ^ 0x6c7967656e657261ULL;
+  uint64_t v3 = k1 ^ 0x7465646279746573ULL;
+  while (sz >= 8) {
+    uint64_t mi;
+    memcpy(&mi, in, 8);                     // little-endian host
+    in += 8;
+    sz -= 8;
+    v3 ^= mi;
+    double_round(v0, v1, v2, v3);
+    v0 ^= mi;
+  }
+  uint64_t t = 0;
+  memcpy(&t, in, sz);
+  b |= t;
+  v3 ^= b;
+  double_round(v0, v1, v2, v3);
+  v0 ^= b;
+  v2 ^= 0xff;
+  double_round(v0, v1, v2, v3);
+  double_round(v0, v1, v2, v3);
+  return (v0 ^ v1) ^ (v2 ^ v3);
+}
+
+int64_t py_str_hash(const uint32_t* s, size_t n, uint64_t k0, uint64_t k1) {
+  if (n == 0) return 0;
+  uint32_t mx = 0;
+  for (size_t i = 0; i < n; ++i) mx = std::max(mx, s[i]);
+  const size_t kind = mx < 0x100 ? 1 : (mx < 0x10000 ? 2 : 4);
+  uint8_t stack[64];
+  std::vector<uint8_t> heap;
+  uint8_t* buf = stack;
+  if (n * kind > sizeof stack) {
+    heap.resize(n * kind);
+    buf = heap.data();
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t c = s[i];
+    if (kind == 1) buf[i] = (uint8_t)c;
+    else if (kind == 2) { buf[2 * i] = (uint8_t)c; buf[2 * i + 1] = (uint8_t)(c >> 8); }
+    else memcpy(buf + 4 * i, &c, 4);
+  }
+  int64_t x = (int64_t)siphash24(k0, k1, buf, n * kind);
+  return x == -1 ? -2 : x;
+}
+
+// Iteration order of the set {a, b} that BUILD_SET makes (a added first) in
+// a fresh 8-slot table (Objects/setobject.c set_add_entry, mask 7: no linear
+// probes, perturbation on collision).  True when b comes first.
+bool set2_second_first(int64_t ha, int64_t hb) {
+  const size_t mask = 7;
+  const size_t ia = (size_t)ha & mask;
+  size_t i = (size_t)hb & mask, perturb = (size_t)hb;
+  while (i == ia) {
+    perturb >>= 5;
+    i = (i * 5 + 1 + perturb) & mask;
+  }
+  return i < ia;
+}
+
+// ------------------------------------------------------------ utf-8 / 32 --
+bool utf8_decode(const char* s, size_t n, std::vector<uint32_t>& out) {
+  out.clear();
+  const uint8_t* p = (const uint8_t*)s;
+  size_t i = 0;
+  while (i < n) {
+    uint32_t c = p[i];
+    int extra;
+    if (c < 0x80) { extra = 0; }
+    else if ((c >> 5) == 6) { extra = 1; c &= 0x1F; }
+    else if ((c >> 4) == 14) { extra = 2; c &= 0x0F; }
+    else if ((c >> 3) == 30) { extra = 3; c &= 0x07; }
+    else return false;
+    if (extra && i + extra >= n) return false;
+    for (int k = 1; k <= extra; ++k) {
+      if ((p[i + k] & 0xC0) != 0x80) return false;
+      c = (c << 6) | (p[i + k] & 0x3F);
+    }
+    out.push_back(c);
+    i += 1 + (size_t)extra;
+  }
+  return true;
+}
+
+void utf8_append(std::string& out, const uint32_t* s, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t cp = s[i];
+    if (cp < 0x80) {
+      out.push_back((char)cp);
+    } else if (cp < 0x800) {
+      out.push_back((char)(0xC0 | (cp >> 6)));
+      out.push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+      out.push_back((char)(0xE0 | (cp >> 12)));
+      out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      out.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      out.push_back((char)(0xF0 | (cp >> 18)));
+      out.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      out.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+  }
+}
+
+// ------------------------------------------------------------ string table --
+constexpr uint8_t F_VERB = 1, F_ADJ = 2, F_EOMI = 4;
+
+struct Info {
+  uint64_t tags = 0;         // bit t: the string is a morph of dictionary tag t
+  uint8_t flags = 0;         // F_VERB | F_ADJ | F_EOMI
+  int32_t rule_lo = 0, rule_n = 0;
+};
+
+struct Span {
+  uint32_t off = 0, len = 0;
+};
+
+inline uint64_t seq_hash(const uint32_t* s, uint32_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xC2B2AE3D27D4EB4Full);
+  for (uint32_t i = 0; i < n; ++i) {
+    h ^= s[i];
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 29;
+  }
+  return h ^ (h >> 32);
+}
+
+class Table {
+ public:
+  std::vector<uint32_t> pool;                 // key code points (+ rule strings)
+  std::vector<Span> keys;
+  std::vector<Info> infos;
+
+  void reserve(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 16) cap <<= 1;
+    slots_.assign(cap, -1);
+    mask_ = cap - 1;
+  }
+
+  Info& get_or_add(const uint32_t* s, uint32_t n) {
+    const uint64_t h = seq_hash(s, n);
+    size_t i = (size_t)h & mask_;
+    while (slots_[i] >= 0) {
+      const Span& k = keys[(size_t)slots_[i]];
+      if (k.len == n && std::equal(s, s + n, pool.data() + k.off)) return infos[(size_t)slots_[i]];
+      i = (i + 1) & mask_;
+    }
+    if (2 * (keys.size() + 1) > slots_.size()) {      // grow and re-place
+      grow();
+      return get_or_add(s, n);
+    }
+    slots_[i] = (int32_t)keys.size();
+    keys.push_back(Span{(uint32_t)pool.size(), n});
+    pool.insert(pool.end(), s, s + n);
+    infos.emplace_back();
+    return infos.back();
+  }
+
+  const Info* find(const uint32_t* s, uint32_t n) const {
+    const uint64_t h = seq_hash(s, n);
+    size_t i = (size_t)h & mask_;
+    while (slots_[i] >= 0) {
+      const Span& k = keys[(size_t)slots_[i]];
+      if (k.len == n && std::equal(s, s + n, pool.data() + k.off)) return &infos[(size_t)slots_[i]];
+      i = (i + 1) & mask_;
+    }
+    return nullptr;
+  }
+
+ private:
+  std::vector<int32_t> slots_;
+  size_t mask_ = 0;
+
+  void grow() {
+    std::vector<int32_t> old;
+    old.swap(slots_);
+    slots_.assign(old.size() * 2, -1);
+    mask_ = slots_.size() - 1;
+    for (size_t x = 0; x < keys.size(); ++x) {
+      const Span& k = keys[x];
+      size_t i = (size_t)seq_hash(pool.data() + k.off, k.len) & mask_;
+      while (slots_[i] >= 0) i = (i + 1) & mask_;
+      slots_[i] = (int32_t)x;
+    }
+  }
+};
+
+struct RulePair {
+  Span stem, eomi;            // in Table::pool
+};
+
+struct Standalone {
+  int32_t dict_tag;           // index into the dictionary's tags, -1: not a dictionary tag
+  int32_t name;               // index into names
+  bool is_noun;
+};
+
+// One lattice node while building (strings by reference).
+struct WordRec {
+  uint32_t w_off, w_len;      // surface: text[w_off .. +w_len)
+  int32_t m0_off, m0_len;     // morph0 in the thread pool; m0_off < 0: the surface
+  int32_t m1_off, m1_len;     // morph1 in the thread pool; m1_off < 0: None
+  int32_t tag0, tag1;         // name indices; tag1 < 0: None
+  int32_t len, b, e;
+  bool is_l;
+};
+
+}  // namespace
+
+struct lt_lexicon {
+  Table table;
+  std::vector<RulePair> rules;
+  std::vector<std::string> names;     // UTF-8 tag names: dictionary tags, then literals
+  int32_t n_dict_tags = 0;
+  int32_t dict_noun = -1, dict_josa = -1;       // dictionary tag indices of 'Noun' / 'Josa'
+  int32_t name_noun = 0, name_josa = 0, name_adj = 0, name_verb = 0, name_eomi = 0;
+  std::vector<Standalone> standalones;
+  int32_t max_len = 0;
+  bool prefer_exact = true;
+  uint64_t k0 = 0, k1 = 0;
+};
+
+struct lt_lattices {
+  std::vector<uint32_t> chars;
+  std::vector<int64_t> char_off, slot_off, sent_words;
+  std::string wb, mb, m1b, tb, t1b;
+  std::vector<int64_t> woff, moff, m1off, toff, t1off;
+  std::vector<uint8_t> m1null, t1null;
+  std::vector<int64_t> len, e, b, is_l;
+};
+
+namespace {
+
+// ------------------------------------------------------------ the lookup --
+struct Worker {
+  const lt_lexicon& lx;
+  const uint32_t* text;
+  std::vector<uint32_t> pool;         // lemma strings of this worker
+  std::vector<uint32_t> sbuf, ebuf;   // candidate stem / eomi
+  std::vector<WordRec> tl, tr;        // lr_lookup's lset / rset
+
+  Worker(const lt_lexicon& l, const uint32_t* t) : lx(l), text(t) {}
+
+  const Info* find(const uint32_t* s, uint32_t n) const { return lx.table.find(s, n); }
+
+  static bool has(const Info* in, int32_t tag) { return tag >= 0 && in && ((in->tags >> tag) & 1u); }
+
+  int32_t keep(const std::vector<uint32_t>& s) {
+    const int32_t off = (int32_t)pool.size();
+    pool.insert(pool.end(), s.begin(), s.end());
+    return off;
+  }
+
+  // analyze_morphology (lemmatizer.py:43-51) of the candidate in sbuf/ebuf
+  void consider(uint32_t w_off, uint32_t m, int32_t len, int32_t b, int32_t e, bool is_l,
+                std::vector<WordRec>& out) {
+    const Info* ei = find(ebuf.data(), (uint32_t)ebuf.size());
+    if (!ei || !(ei->flags & F_EOMI)) return;
+    const Info* si = find(sbuf.data(), (uint32_t)sbuf.size());
+    if (!si || !(si->flags & (F_ADJ | F_VERB))) return;
+    const int32_t so = keep(sbuf), eo = keep(ebuf);
+    const int32_t sl = (int32_t)sbuf.size(), el = (int32_t)ebuf.size();
+    if (si->flags & F_ADJ)
+      out.push_back(WordRec{w_off, m, so, sl, eo, el, lx.name_adj, lx.name_eomi, len, b, e, is_l});
+    if (si->flags & F_VERB)
+      out.push_back(WordRec{w_off, m, so, sl, eo, el, lx.name_verb, lx.name_eomi, len, b, e, is_l});
+  }
+
+  void set_cand(const uint32_t* s1, size_t n1, const uint32_t* s2, size_t n2,
+                const uint32_t* e1, size_t m1, const uint32_t* e2, size_t m2) {
+    sbuf.assign(s1, s1 + n1);
+    sbuf.insert(sbuf.end(), s2, s2 + n2);
+    ebuf.assign(e1, e1 + m1);
+    ebuf.insert(ebuf.end(), e2, e2 + m2);
+  }
+
+  // MorphemeDictionary.lemmatize(word) words (dictionary.py:304-309) for the
+  // surface text[w_off .. +m): get_lemma_candidates (lemmatizer.py:90-112)
+  // filtered by analyze_morphology, in candidate order.
+  void lemmatize(uint32_t w_off, uint32_t m, int32_t len, int32_t b, int32_t e, bool is_l,
+                 std::vector<WordRec>& out) {
+    const uint32_t* w = text + w_off;
+    const std::vector<RulePair>& R = lx.rules;
+    const uint32_t* P = lx.table.pool.data();
+    for (uint32_t i = 0; i < m; ++i) {
+      // (l, r) = (word[:i+1], word[i+1:]), while i < max_i
+      if (i + 1 < m) {
+        set_cand(w, i + 1, nullptr, 0, w + i + 1, m - i - 1, nullptr, 0);
+        consider(w_off, m, len, b, e, is_l, out);
+      }
+      // 1 syllable conjugation: the pairs of rules[c], |rules[c]| times over
+      // (the nested loop of lemmatizer.py:100-101)
+      if (const Info* ci = find(w + i, 1)) {
+        for (int32_t rep = 0; rep < ci->rule_n; ++rep)
+          for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
+            const RulePair& rp = R[(size_t)q];
+            set_cand(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, w + i + 1, m - i - 1);
+            consider(w_off, m, len, b, e, is_l, out);
+          }
+      }
+      // 2 or 3 syllables conjugation: for conj in {word[i:i+2], word[i:i+3]}
+      // (set iteration order, lemmatizer.py:107); eomi + r[1:]
+      const uint32_t n2 = std::min<uint32_t>(2, m - i), n3 = std::min<uint32_t>(3, m - i);
+      const uint32_t* rest = w + std::min<uint32_t>(m, i + 2);
+      const uint32_t nrest = m - std::min<uint32_t>(m, i + 2);
+      uint32_t conj[2] = {n2, n3};
+      int nconj = 2;
+      if (n2 == n3) {
+        nconj = 1;
+      } else if (set2_second_first(py_str_hash(w + i, n2, lx.k0, lx.k1), py_str_hash(w + i, n3, lx.k0, lx.k1))) {
+        std::swap(conj[0], conj[1]);
+      }
+      for (int c = 0; c < nconj; ++c) {
+        const Info* ci = find(w + i, conj[c]);
+        if (!ci) continue;
+        for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
+          const RulePair& rp = R[(size_t)q];
+          set_cand(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, rest, nrest);
+          consider(w_off, m, len, b, e, is_l, out);
+        }
+      }
+    }
+  }
+
+  // MorphemeDictionary.lookup(word, b, is_l) (dictionary.py:304-315)
+  void dict_lookup(uint32_t w_off, uint32_t n, int32_t b, bool is_l, std::vector<WordRec>& out) {
+    if (const Info* in = find(text + w_off, n)) {
+      for (int32_t t = 0; t < lx.n_dict_tags; ++t)
+        if ((in->tags >> t) & 1u)
+          out.push_back(WordRec{w_off, n, -1, 0, -1, 0, t, -1, (int32_t)n, b, b + (int32_t)n, is_l});
+    }
+    lemmatize(w_off, n, (int32_t)n, b, b + (int32_t)n, is_l, out);
+  }
+
+  void noun_josa(uint32_t e_off, uint32_t n, uint32_t i, int32_t offset, int32_t len, std::vector<WordRec>& out) {
+    out.push_back(WordRec{e_off, i, -1, 0, -1, 0, lx.name_noun, -1, len, offset, offset + (int32_t)i, true});
+    out.push_back(WordRec{e_off + i, n - i, -1, 0, -1, 0, lx.name_josa, -1, len, offset + (int32_t)i,
+                          offset + (int32_t)n, false});
+  }
+
+  bool is_noun_josa(uint32_t e_off, uint32_t n, uint32_t i) {
+    return has(find(text + e_off, i), lx.dict_noun) && has(find(text + e_off + i, n - i), lx.dict_josa);
+  }
+
+  // lr_lookup (lookup.py:171-210)
+  void lr_lookup(uint32_t e_off, uint32_t n, int32_t offset, bool prefer, std::vector<WordRec>& out) {
+    const size_t start = out.size();
+    dict_lookup(e_off, n, offset, true, out);
+    if (prefer && out.size() > start) return;
+    for (uint32_t i = 1; i < n; ++i) {
+      if (is_noun_josa(e_off, n, i)) {
+        noun_josa(e_off, n, i, offset, (int32_t)n, out);
+        continue;
+      }
+      tl.clear();
+      dict_lookup(e_off, i, offset, true, tl);
+      if (tl.empty()) continue;
+      tr.clear();
+      dict_lookup(e_off + i, n - i, offset + (int32_t)i, false, tr);
+      if (tr.empty()) continue;
+      out.insert(out.end(), tl.begin(), tl.end());
+      out.insert(out.end(), tr.begin(), tr.end());
+    }
+  }
+
+  // morpheme_lookup (lookup.py:212-279)
+  void morpheme_lookup(uint32_t e_off, uint32_t n, int32_t offset, std::vector<WordRec>& out) {
+    const size_t start = out.size();
+    lr_lookup(e_off, n, offset, false, out);
+    if (lx.prefer_exact && out.size() > start) return;
+    const uint32_t max_len = lx.max_len <= 0 ? n : (uint32_t)lx.max_len;
+    std::vector<uint8_t> noun_end(n + 1, 0);
+    for (uint32_t i = 1; i < n; ++i)
+      if (is_noun_josa(e_off, n, i)) noun_josa(e_off, n, i, offset, (int32_t)i, out);
+    for (uint32_t b = 1; b < n; ++b) {
+      const uint32_t e_hi = std::min(b + max_len, n);
+      for (uint32_t e = b + 1; e <= e_hi; ++e) {
+        const uint32_t so = e_off + b, sl = e - b;
+        const Info* in = find(text + so, sl);
+        const int32_t B = offset + (int32_t)b, E = offset + (int32_t)e;
+        for (const Standalone& st : lx.standalones)
+          if (has(in, st.dict_tag)) {
+            out.push_back(WordRec{so, sl, -1, 0, -1, 0, st.name, -1, (int32_t)sl, B, E, false});
+            if (st.is_noun) noun_end[e] = 1;
+          }
+        if (noun_end[b] && has(in, lx.dict_josa))
+          out.push_back(WordRec{so, sl, -1, 0, -1, 0, lx.name_josa, -1, (int32_t)sl, B, E, false});
+        lemmatize(so, sl, (int32_t)sl, B, E, false, out);
+      }
+    }
+  }
+};
+
+// Columns of a range of sentences (one worker's share).
+struct Chunk {
+  std::string wb, mb, m1b, tb, t1b;
+  std::vector<int64_t> woff{0}, moff{0}, m1off{0}, toff{0}, t1off{0};
+  std::vector<uint8_t> m1null, t1null;
+  std::vector<int64_t> len, e, b, is_l;
+  std::vector<int64_t> slot_n;      // words per begin slot, sentence-major
+  std::vector<int64_t> sent_n;      // words per sentence
+  std::string err;
+};
+
+void run_chunk(const lt_lexicon& lx, const lt_text_desc& td, int32_t s0, int32_t s1, Chunk& ck) {
+  Worker wk(lx, td.text);
+  std::vector<WordRec> words, grouped;
+  std::vector<int64_t> cnt;
+  for (int32_t s = s0; s < s1; ++s) {
+    const int64_t n = td.char_off[s + 1] - td.char_off[s];
+    words.clear();
+    int32_t offset = 0;
+    for (int64_t j = td.sent_eoj[s]; j < td.sent_eoj[s + 1]; ++j) {
+      const uint32_t eo = (uint32_t)td.eoj_off[j], el = (uint32_t)(td.eoj_off[j + 1] - td.eoj_off[j]);
+      wk.morpheme_lookup(eo, el, offset, words);
+      offset += (int32_t)el;
+    }
+    // bindex[word.b].append(word) (lookup.py:365-367): stable by begin
+    cnt.assign((size_t)n + 1, 0);
+    for (const WordRec& w : words) {
+      if (w.b < 0 || w.b >= n) {
+        ck.err = "word begins outside its sentence (eojeols longer than the sentence's characters)";
+        return;
+      }
+      ++cnt[(size_t)w.b + 1];
+    }
+    for (int64_t x = 0; x < n; ++x) ck.slot_n.push_back(cnt[(size_t)x + 1]);
+    for (int64_t x = 0; x < n; ++x) cnt[(size_t)x + 1] += cnt[(size_t)x];
+    grouped.resize(words.size());
+    for (const WordRec& w : words) grouped[(size_t)cnt[(size_t)w.b]++] = w;
+    ck.sent_n.push_back((int64_t)words.size());
+    for (const WordRec& w : grouped) {
+      utf8_append(ck.wb, td.text + w.w_off, w.w_len);
+      ck.woff.push_back((int64_t)ck.wb.size());
+      if (w.m0_off < 0) utf8_append(ck.mb, td.text + w.w_off, w.w_len);
+      else utf8_append(ck.mb, wk.pool.data() + w.m0_off, (size_t)w.m0_len);
+      ck.moff.push_back((int64_t)ck.mb.size());
+      if (w.m1_off >= 0) utf8_append(ck.m1b, wk.pool.data() + w.m1_off, (size_t)w.m1_len);
+      ck.m1off.push_back((int64_t)ck.m1b.size());
+      ck.m1null.push_back(w.m1_off < 0);
+      ck.tb += lx.names[(size_t)w.tag0];
+      ck.toff.push_back((int64_t)ck.tb.size());
+      if (w.tag1 >= 0) ck.t1b += lx.names[(size_t)w.tag1];
+      ck.t1off.push_back((int64_t)ck.t1b.size());
+      ck.t1null.push_back(w.tag1 < 0);
+      ck.len.push_back(w.len);
+      ck.e.push_back(w.e);
+      ck.b.push_back(w.b);
+      ck.is_l.push_back(w.is_l ? 1 : 0);
+    }
+    wk.pool.clear();
+  }
+}
+
+void append_offsets(std::vector<int64_t>& dst, const std::vector<int64_t>& src, int64_t base) {
+  for (size_t i = 1; i < src.size(); ++i) dst.push_back(src[i] + base);
+}
+
+lt_strings view_of(const std::string& blob, const std::vector<int64_t>& off, const std::vector<uint8_t>* null) {
+  lt_strings s;
+  s.data = blob.data();
+  s.off = off.data();
+  s.null = null ? null->data() : nullptr;
+  s.n = (int64_t)off.size() - 1;
+  return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t lt_py_str_hash(const uint32_t* cps, int64_t n, uint64_t k0, uint64_t k1) {
+  if (n < 0 || (n > 0 && !cps)) return 0;
+  return py_str_hash(cps, (size_t)n, k0, k1);
+}
+
+int lt_py_set2_second_first(int64_t hash_a, int64_t hash_b) {
+  return set2_second_first(hash_a, hash_b) ? 1 : 0;
+}
+
+lt_status lt_lexicon_create(const lt_lexicon_desc* d, lt_lexicon** out) {
+  if (!d || !out) return lt::set_error(LT_EINVAL, "lt_lexicon_create: NULL argument");
+  *out = nullptr;
+  const int64_t T = d->tag.n;
+  if (T < 0 || T > LT_LEXICON_MAX_TAGS)
+    return lt::set_error(LT_EUNSUPPORTED, "lt_lexicon_create: %lld tags (at most %d)", (long long)T,
+                         LT_LEXICON_MAX_TAGS);
+  if (T > 0 && !d->morph_off) return lt::set_error(LT_EINVAL, "lt_lexicon_create: morph_off is NULL");
+  if (d->rule_surface.n > 0 && !d->rule_off) return lt::set_error(LT_EINVAL, "lt_lexicon_create: rule_off is NULL");
+  std::unique_ptr<lt_lexicon> lx(new (std::nothrow) lt_lexicon);
+  if (!lx) return lt::set_error(LT_ENOMEM, "lt_lexicon_create: out of host memory");
+  auto str = [](const lt_strings& t, int64_t i) {
+    return std::string(t.data + t.off[i], (size_t)(t.off[i + 1] - t.off[i]));
+  };
+  std::vector<uint32_t> cp;
+  auto decode = [&](const lt_strings& t, int64_t i) {
+    return utf8_decode(t.data + t.off[i], (size_t)(t.off[i + 1] - t.off[i]), cp);
+  };
+  Table& tab = lx->table;
+  tab.reserve((size_t)(d->morph.n + d->verbs.n + d->adjectives.n + d->eomis.n + d->rule_surface.n));
+  // tags and their morphs (get_tags order = the dictionary's tag order)
+  auto name_index = [&](const std::string& s) {
+    for (size_t i = 0; i < lx->names.size(); ++i)
+      if (lx->names[i] == s) return (int32_t)i;
+    lx->names.push_back(s);
+    return (int32_t)lx->names.size() - 1;
+  };
+  for (int64_t t = 0; t < T; ++t) {
+    const std::string name = str(d->tag, t);
+    for (size_t i = 0; i < lx->names.size(); ++i)
+      if (lx->names[i] == name) return lt::set_error(LT_EINVAL, "lt_lexicon_create: duplicate tag");
+    lx->names.push_back(name);
+  }
+  lx->n_dict_tags = (int32_t)T;
+  for (int64_t t = 0; t < T; ++t)
+    for (int64_t i = d->morph_off[t]; i < d->morph_off[t + 1]; ++i) {
+      if (i < 0 || i >= d->morph.n) return lt::set_error(LT_EINVAL, "lt_lexicon_create: morph_off out of range");
+      if (!decode(d->morph, i)) return lt::set_error(LT_EINVAL, "lt_lexicon_create: bad UTF-8");
+      tab.get_or_add(cp.data(), (uint32_t)cp.size()).tags |= (uint64_t)1 << t;
+    }
+  const std::pair<const lt_strings*, uint8_t> sets[] = {
+      {&d->verbs, F_VERB}, {&d->adjectives, F_ADJ}, {&d->eomis, F_EOMI}};
+  for (const auto& st : sets)
+    for (int64_t i = 0; i < st.first->n; ++i) {
+      if (!decode(*st.first, i)) return lt::set_error(LT_EINVAL, "lt_lexicon_create: bad UTF-8");
+      tab.get_or_add(cp.data(), (uint32_t)cp.size()).flags |= st.second;
+    }
+  // rules (surface -> pairs); the pair strings live in the table's pool
+  for (int64_t r = 0; r < d->rule_surface.n; ++r) {
+    if (d->rule_off[r] > d->rule_off[r + 1] || d->rule_off[r + 1] > d->rule_stem.n ||
+        d->rule_stem.n != d->rule_eomi.n)
+      return lt::set_error(LT_EINVAL, "lt_lexicon_create: rule_off out of range");
+    const int32_t lo = (int32_t)lx->rules.size();
+    for (int64_t q = d->rule_off[r]; q < d->rule_off[r + 1]; ++q) {
+      RulePair rp;
+      if (!decode(d->rule_stem, q)) return lt::set_error(LT_EINVAL, "lt_lexicon_create: bad UTF-8");
+      rp.stem = Span{(uint32_t)tab.pool.size(), (uint32_t)cp.size()};
+      tab.pool.insert(tab.pool.end(), cp.begin(), cp.end());
+      if (!decode(d->rule_eomi, q)) return lt::set_error(LT_EINVAL, "lt_lexicon_create: bad UTF-8");
+      rp.eomi = Span{(uint32_t)tab.pool.size(), (uint32_t)cp.size()};
+      tab.pool.insert(tab.pool.end(), cp.begin(), cp.end());
+      lx->rules.push_back(rp);
+    }
+    if (!decode(d->rule_surface, r)) return lt::set_error(LT_EINVAL, "lt_lexicon_create: bad UTF-8");
+    Info& in = tab.get_or_add(cp.data(), (uint32_t)cp.size());
+    if (in.rule_n == 0) {                      // first entry wins (dict keys are unique anyway)
+      in.rule_lo = lo;
+      in.rule_n = (int32_t)lx->rules.size() - lo;
+    }
+  }
+  // the tagset literals the lookup writes (tagset.py)
+  auto dict_tag = [&](const char* s) {
+    for (int32_t t = 0; t < (int32_t)T; ++t)
+      if (lx->names[(size_t)t] == s) return t;
+    return (int32_t)-1;
+  };
+  lx->dict_noun = dict_tag("Noun");
+  lx->dict_josa = dict_tag("Josa");
+  lx->name_noun = name_index("Noun");
+  lx->name_josa = name_index("Josa");
+  lx->name_adj = name_index("Adjective");
+  lx->name_verb = name_index("Verb");
+  lx->name_eomi = name_index("Eomi");
+  for (int64_t i = 0; i < d->standalones.n; ++i) {
+    const std::string s = str(d->standalones, i);
+    Standalone st;
+    st.dict_tag = -1;
+    for (int32_t t = 0; t < (int32_t)T; ++t)
+      if (lx->names[(size_t)t] == s) st.dict_tag = t;
+    st.name = name_index(s);
+    st.is_noun = s == "Noun";
+    lx->standalones.push_back(st);
+  }
+  lx->max_len = d->max_len;
+  lx->prefer_exact = d->prefer_exact_match != 0;
+  lx->k0 = d->hash_k0;
+  lx->k1 = d->hash_k1;
+  *out = lx.release();
+  return LT_OK;
+}
+
+lt_status lt_lexicon_destroy(lt_lexicon* lx) {
+  delete lx;
+  return LT_OK;
+}
+
+lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_threads, lt_lattices** out) {
+  if (!lx || !td || !out) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: NULL argument");
+  *out = nullptr;
+  const int32_t S = td->n_sent;
+  if (S < 0) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: negative sentence count");
+  if (S > 0 && (!td->sent_eoj || !td->char_off || !td->eoj_off))
+    return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: NULL arrays");
+  for (int32_t s = 0; s < S; ++s) {
+    if (td->sent_eoj[s + 1] < td->sent_eoj[s] || td->char_off[s + 1] < td->char_off[s])
+      return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: offsets decrease at sentence %d", s);
+    int64_t total = 0;
+    for (int64_t j = td->sent_eoj[s]; j < td->sent_eoj[s + 1]; ++j) {
+      if (td->eoj_off[j + 1] < td->eoj_off[j]) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: eojeol offsets decrease");
+      total += td->eoj_off[j + 1] - td->eoj_off[j];
+    }
+    if (total > td->char_off[s + 1] - td->char_off[s])
+      return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: sentence %d has more eojeol characters than characters", s);
+    if (td->char_off[s + 1] - td->char_off[s] > (int64_t)1 << 30)
+      return lt::set_error(LT_EUNSUPPORTED, "lt_lexicon_lookup: sentence %d too long", s);
+  }
+  if (S > 0 && td->char_off[0] != 0) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: char_off[0] != 0");
+  if (S > 0 && (td->eoj_off[td->sent_eoj[S]] >= ((int64_t)1 << 32) || td->sent_eoj[0] < 0))
+    return lt::set_error(LT_EUNSUPPORTED, "lt_lexicon_lookup: text too long for one call");
+  int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = std::max(1, std::min(nt, std::max(1, S / 16)));
+  std::vector<Chunk> ck((size_t)nt);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) {
+      const int32_t s0 = (int32_t)((int64_t)S * t / nt), s1 = (int32_t)((int64_t)S * (t + 1) / nt);
+      if (t + 1 == nt) run_chunk(*lx, *td, s0, s1, ck[(size_t)t]);
+      else th.emplace_back([&, s0, s1, t] { run_chunk(*lx, *td, s0, s1, ck[(size_t)t]); });
+    }
+    for (std::thread& x : th) x.join();
+  }
+  for (const Chunk& c : ck)
+    if (!c.err.empty()) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: %s", c.err.c_str());
+  std::unique_ptr<lt_lattices> L(new (std::nothrow) lt_lattices);
+  if (!L) return lt::set_error(LT_ENOMEM, "lt_lexicon_lookup: out of host memory");
+  const int64_t C = S > 0 ? td->char_off[S] : 0;
+  L->chars.assign(td->chars, td->chars + C);
+  L->char_off.assign(td->char_off, td->char_off + S + 1);
+  if (S == 0) L->char_off.assign(1, 0);
+  L->slot_off.push_back(0);
+  L->sent_words.push_back(0);
+  for (auto* v : {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off}) v->push_back(0);
+  for (const Chunk& c : ck) {
+    for (int64_t x : c.slot_n) L->slot_off.push_back(L->slot_off.back() + x);
+    for (int64_t x : c.sent_n) L->sent_words.push_back(L->sent_words.back() + x);
+    append_offsets(L->woff, c.woff, (int64_t)L->wb.size());
+    append_offsets(L->moff, c.moff, (int64_t)L->mb.size());
+    append_offsets(L->m1off, c.m1off, (int64_t)L->m1b.size());
+    append_offsets(L->toff, c.toff, (int64_t)L->tb.size());
+    append_offsets(L->t1off, c.t1off, (int64_t)L->t1b.size());
+    L->wb += c.wb;
+    L->mb += c.mb;
+    L->m1b += c.m1b;
+    L->tb += c.tb;
+    L->t1b += c.t1b;
+    L->m1null.insert(L->m1null.end(), c.m1null.begin(), c.m1null.end());
+    L->t1null.insert(L->t1null.end(), c.t1null.begin(), c.t1null.end());
+    L->len.insert(L->len.end(), c.len.begin(), c.len.end());
+    L->e.insert(L->e.end(), c.e.begin(), c.e.end());
+    L->b.insert(L->b.end(), c.b.begin(), c.b.end());
+    L->is_l.insert(L->is_l.end(), c.is_l.begin(), c.is_l.end());
+  }
+  if ((int64_t)L->slot_off.size() != C + 1) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: slot count mismatch");
+  // non-null data pointers for empty columns
+  for (std::string* bl : {&L->wb, &L->mb, &L->m1b, &L->tb, &L->t1b}) bl->reserve(1);
+  if (L->chars.empty()) L->chars.reserve(1);
+  *out = L.release();
+  return LT_OK;
+}
+
+lt_status lt_lattices_view(const lt_lattices* L, lt_lattice_view* v) {
+  if (!L || !v) return lt::set_error(LT_EINVAL, "lt_lattices_view: NULL argument");
+  lt_lattice_desc& d = v->lattice;
+  d.n_sent = (int32_t)L->char_off.size() - 1;
+  d.chars = L->chars.data();
+  d.char_off = L->char_off.data();
+  d.slot_off = L->slot_off.data();
+  d.n_words = (int64_t)L->len.size();
+  d.word = view_of(L->wb, L->woff, nullptr);
+  d.morph0 = view_of(L->mb, L->moff, nullptr);
+  d.tag0 = view_of(L->tb, L->toff, nullptr);
+  d.morph1 = view_of(L->m1b, L->m1off, &L->m1null);
+  d.tag1 = view_of(L->t1b, L->t1off, &L->t1null);
+  d.len = L->len.data();
+  d.e = L->e.data();
+  d.is_l = L->is_l.data();
+  v->b = L->b.data();
+  v->sent_words = L->sent_words.data();
+  return LT_OK;
+}
+
+lt_status lt_lattices_destroy(lt_lattices* L) {
+  delete L;
+  return LT_OK;
+}
+
+}  // extern "C"

@@ -242,6 +242,12 @@ class NativePacker:
         slot_off = np.asarray(slot_off, dtype=np.int64)
         desc = LatticeDesc(len(chars_l), _ptr(cps), _ptr(char_off), _ptr(slot_off), len(words),
                            tw.c(), tm.c(), tt.c(), tm1.c(), tt1.c(), _ptr(lens), _ptr(ends), _ptr(isl))
+        return self.pack_desc(desc, words, chars_l, max_len)
+
+    def pack_desc(self, desc, words, chars_l, max_len=8):
+        """Pack columnar lattices (an lt_lattice_desc, e.g. the native lattice
+        builder's); ``words[i]`` materialises global node i, ``chars_l`` are
+        the sentences' characters.  -> (PackedBatch, node views)."""
         out = Packed()
         _capi.check(self.lib.lt_packer_pack(self.handle, C.byref(desc), int(max_len), C.byref(out)))
         b = out.batch

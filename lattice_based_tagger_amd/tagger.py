@@ -4,18 +4,20 @@ Mirrors `lattice_tagger/tagger/tagger.py:10-78`:
 ``Tagger(dictionary, lookup, encoder, score_funcs).tag(sent, beam_size=5,
 ensure_normalize=True, debug=False) -> Sequence``.
 
-Lattice construction (dictionary lookup) is outside the accelerated path:
-the tagger drives whatever eojeol lookup it is given -- normally the
-reference's own ``MorphemeLookup`` (`dictionary/lookup.py:99-132`), which it
-builds from a reference ``MorphemeDictionary`` exactly as the reference
-``Tagger.__init__`` does (`tagger.py:60`).  The sentence-level grouping into a
-begin index restates `lookup.py:7-62` and `:344-369`.  Decoding runs through
-``beam_search_batch`` on the device.
+Lattice construction: with a reference ``MorphemeDictionary`` (the
+reference ``Tagger.__init__`` builds ``MorphemeLookup(dictionary)``,
+`tagger.py:60`) the lattices of a whole batch come from the native lattice
+builder (``lookup.NativeLexicon``, C++), which restates
+``morpheme_lookup`` and the lemmatizer node for node; a custom ``lookup``
+callable (or a dictionary subclass overriding the lookup methods) runs in
+Python, grouped into a begin index as `lookup.py:7-62, 344-369` do.
+Decoding runs on the device.
 """
 
 import sys
 
 from .beam import beam_search_batch
+from .tagset import Adjective, Adverb, Determiner, Exclamation, Noun, Number, Verb
 from .word import bos_word, eos_word
 
 
@@ -46,6 +48,40 @@ def sentence_lookup_as_begin_index(sent, eojeol_lookup):
     return nodes, bindex
 
 
+# MorphemeLookup defaults (lookup.py:104-105) -- the lookup Tagger builds
+# (tagger.py:60)
+STANDALONES = (Noun, Adverb, Exclamation, Determiner, Number)
+
+# the reference MorphemeDictionary methods the native lattice builder restates
+_REF_METHODS = {'lookup': 'MorphemeDictionary.lookup', 'check': 'WordDictionary.check',
+                'get_tags': 'WordDictionary.get_tags', 'lemmatize': 'MorphemeDictionary.lemmatize'}
+
+
+def find_max_len(dictionary, standalones):
+    """MorphemeLookup._find_max_len (`lookup.py:123-132`)."""
+    keep = set(standalones)
+    keep.add(Verb)
+    keep.add(Adjective)
+    max_len = 0
+    for tag, morphs in dictionary.tag_to_morphs.items():
+        if tag not in keep:
+            continue
+        max_len = max(max_len, max(len(m) for m in morphs))
+    return max_len
+
+
+def plain_morpheme_dictionary(dictionary):
+    """True when ``dictionary`` answers lookups with the reference
+    MorphemeDictionary's own methods (no subclass overrides), so the native
+    lattice builder restates it exactly."""
+    for name, qual in _REF_METHODS.items():
+        f = getattr(type(dictionary), name, None)
+        if f is None or getattr(f, '__qualname__', None) != qual or \
+                not str(getattr(f, '__module__', '')).endswith('dictionary.dictionary'):
+            return False
+    return True
+
+
 def _default_lookup(dictionary):
     ref = sys.modules.get('lattice_tagger.dictionary')
     if ref is None:
@@ -64,31 +100,76 @@ class Tagger:
     ``dictionary``  a reference ``MorphemeDictionary`` (or the string
                     'base', which builds the reference BaseMorphemeDictionary)
     ``lookup``      optional callable ``(eojeol, offset) -> [Word]``; when not
-                    callable the reference MorphemeLookup over ``dictionary``
-                    is used, as the reference does
+                    callable the tagger uses MorphemeLookup over
+                    ``dictionary`` with its defaults, as the reference does
+                    (`tagger.py:60`)
     ``score_funcs`` a ``BeamScoreFunctions`` composite (reference or mirror)
     ``device``      HIP device ordinal of the decoder
+    ``lexicon``     a prebuilt ``lookup.NativeLexicon`` (optional; used as
+                    given -- the caller rebuilds it after changing the
+                    dictionary)
+    ``native_lookup`` build lattices with the native lattice builder
+                    (``lookup.NativeLexicon``, C++) when the dictionary is a
+                    plain reference MorphemeDictionary; otherwise (or when
+                    False) the Python MorphemeLookup runs
     """
 
     def __init__(self, dictionary='base', lookup='subword_lookup', encoder=None,
-                 score_funcs=None, device=0):
+                 score_funcs=None, device=0, lexicon=None, native_lookup=True, lookup_threads=0):
+        self._lexicon = lexicon
+        self._lexicon_given = lexicon is not None     # used as given, never rebuilt
+        self._eojeol_lookup = None
+        self.lookup_threads = lookup_threads
         if callable(lookup):
             self.dictionary = dictionary
-            self.eojeol_lookup = lookup
+            self._eojeol_lookup = lookup
+            self.native = lexicon is not None
         else:
             if isinstance(dictionary, str):
                 ref = sys.modules.get('lattice_tagger.dictionary')
                 if ref is None:
                     import lattice_tagger.dictionary as ref
                 dictionary = ref.BaseMorphemeDictionary()
+            if lexicon is None and not hasattr(dictionary, 'rules'):
+                raise ValueError('dictionary must be MorphemeDictionary')      # lookup.py:101-102
             self.dictionary = dictionary
-            self.eojeol_lookup = _default_lookup(dictionary)
+            self.native = lexicon is not None or (native_lookup and plain_morpheme_dictionary(dictionary))
         self.encoder = encoder
         self.score_funcs = score_funcs
         self.device = device
 
+    @property
+    def eojeol_lookup(self):
+        if self._eojeol_lookup is None:
+            self._eojeol_lookup = _default_lookup(self.dictionary)
+        return self._eojeol_lookup
+
+    def native_lexicon(self):
+        """The NativeLexicon in use (rebuilt when the dictionary changed), or
+        None when lattices are built in Python."""
+        if not self.native:
+            return None
+        from .lookup import NativeLexicon, dictionary_fingerprint
+        from .native_packer import Unsupported
+        lex = self._lexicon
+        if lex is not None and (self._lexicon_given or
+                                dictionary_fingerprint(self.dictionary) == lex.fingerprint):
+            return lex
+        try:
+            standalones = list(STANDALONES)
+            lex = NativeLexicon(self.dictionary, standalones, find_max_len(self.dictionary, standalones),
+                                prefer_exact_match=True)
+        except Unsupported:
+            self.native = False
+            return None
+        self._lexicon = lex
+        return lex
+
     def lattice(self, sent):
         chars = sent.replace(' ', '')
+        lex = self.native_lexicon()
+        if lex is not None:
+            return lex.lookup([sent], n_threads=1).bindex(0), chars
         _, bindex = sentence_lookup_as_begin_index(sent, self.eojeol_lookup)
         return bindex, chars
 
@@ -101,7 +182,26 @@ class Tagger:
         """Best ``Sequence`` per sentence, decoded in one device launch.
         Raises IndexError like ``tag`` when a non-empty sentence has no
         dictionary node at all (`beam.py:32`)."""
-        lattices = [self.lattice(s) for s in sents]
-        matures = beam_search_batch(lattices, self.score_funcs, beam_size=beam_size,
-                                    device=self.device)
+        sents = list(sents)
+        lex = self.native_lexicon()
+        if lex is None:
+            lattices = [self.lattice(s) for s in sents]
+            matures = beam_search_batch(lattices, self.score_funcs, beam_size=beam_size,
+                                        device=self.device)
+            return [m[0] for m in matures]
+        from .beam import _check_beam, decode_batch, lowered_model
+        from .native_packer import packer_for
+        k = _check_beam(beam_size)
+        lat = lex.lookup(sents, n_threads=self.lookup_threads)
+        for s in range(len(sents)):
+            if lat.empty(s):
+                raise IndexError('list index out of range')            # beam.py:32 on bindex == []
+        model = lowered_model(self.score_funcs)
+        npk = packer_for(model)
+        if npk is None:
+            lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(sents))]
+            matures = beam_search_batch(lattices, self.score_funcs, beam_size=k, device=self.device)
+        else:
+            packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+            matures = decode_batch(packed, views, lat.chars, model, k, self.device)
         return [m[0] for m in matures]

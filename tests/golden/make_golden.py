@@ -176,7 +176,7 @@ def make_sentences(dic, n_sent, n_eojeol, seed):
 
 
 def main():
-    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense']
+    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'lookup']
 
     if 'base' in sets:
         d = BaseMorphemeDictionary()
@@ -255,6 +255,9 @@ def main():
 
     if 'dense' in sets:
         dump_dense()
+
+    if 'lookup' in sets:
+        dump_lookup()
 
 
 def W(word, tag, b, e, length=None, is_l=False, morph0=None, morph1=None, tag1=None):
@@ -366,6 +369,94 @@ def dump_dense():
     models = {'dense_tri': [spec_of(f) for f in funcs.funcs]}
     cases = [case(b, c, 'dense_tri', funcs, tag='dense') for b, c in lats]
     dump('dense', models, cases)
+
+
+# ------------------------------------------------------- lattice build set --
+class RecSet(set):
+    """A dictionary morph set that records its positive membership tests."""
+
+    def __init__(self, items):
+        super().__init__(items)
+        self.hits = set()
+
+    def __contains__(self, x):
+        r = set.__contains__(self, x)
+        if r:
+            self.hits.add(x)
+        return r
+
+
+class RecRules(dict):
+    """The lemmatisation rules, recording the surfaces that yielded pairs."""
+
+    def __init__(self, items):
+        super().__init__(items)
+        self.hits = set()
+
+    def get(self, k, default=None):
+        r = dict.get(self, k, default)
+        if r:
+            self.hits.add(k)
+        return r
+
+
+# eojeols whose lemma candidates depend on the {word[i:i+2], word[i:i+3]}
+# set order (lemmatizer.py:107), found by comparing both orders on the base
+# dictionary; plus edge strings
+ORDER_SENSITIVE = ['지겨우나 흥겨우나 기우고', '누우라고 드러누우라고 돌아누우라고',
+                   '눈물겨우나 짜기우고 힘겨우나 정겨우나', '파랬다 추운데 차가우니까 시작했으니까']
+EDGE_SENTS = ['', 'ㅋㅋㅋ', ' ', '  spaced   out  ', 'abc 가나다 123', '아이오아이의 노래 입니다',
+              '너무너무너무는 아이오아이의 노래 입니다', '했다 했 다', 'tab\tseparated 노래\t를', '가',
+              '\U0001F600웃음 😀', '가' * 40]
+
+
+def dump_lookup():
+    """Lattices of the reference's MorphemeLookup (what Tagger.tag builds,
+    tagger.py:60,73) for the base and demo dictionaries, with the part of
+    each dictionary the lookups consulted: every morph / verb / adjective /
+    eomi a membership test found, every rule surface that yielded pairs
+    (its whole tuple, in order).  A lookup against that restriction answers
+    every query of these sentences as the full dictionary does."""
+    out = {}
+    for name, D in (('base', BaseMorphemeDictionary), ('demo', DemoMorphemeDictionary)):
+        d = D()
+        lk = MorphemeLookup(d, flatten=False)          # max_len from the full dictionary
+        rec = {t: RecSet(ms) for t, ms in d.tag_to_morphs.items()}
+        d.tag_to_morphs = rec
+        d.verbs = rec.get('Verb', {})
+        d.adjectives = rec.get('Adjective', {})
+        d.eomis = rec.get('Eomi', {})
+        d.rules = RecRules(d.rules)
+        if name == 'base':
+            sents = make_sentences(d, 101, 20, seed=11)
+            sents = [make_sentences(d, 1, 10, seed=5)[0]] + sents[1:]        # = the 'base' set
+            rng = random.Random(7)
+            t2m = {t: sorted(ms) for t, ms in d.tag_to_morphs.items()}
+            for _ in range(60):       # random concatenations of morphs of any tag
+                eo = [''.join(rng.choice(t2m[rng.choice(list(t2m))][:300])
+                              for _ in range(rng.randint(1, 3))) for _ in range(rng.randint(1, 12))]
+                sents.append(' '.join(eo))
+        else:
+            sents = ['너무너무너무는 아이오아이의 노래 입니다', '아이오아이의 노래를 했다',
+                     '노래 연습을 합니다 아이오아이'] + make_sentences(d, 40, 8, seed=3)
+        sents += ORDER_SENSITIVE + EDGE_SENTS
+        lats = []
+        for s in sents:
+            _, bindex = sentence_lookup_as_begin_index(s, lk)
+            lats.append([[enc_word(w) for w in ws] for ws in bindex])
+        lex = {'tags': list(d.tag_to_morphs),
+               'morphs': {t: sorted(ms.hits) for t, ms in d.tag_to_morphs.items()},
+               'verbs': sorted(getattr(d.verbs, 'hits', ())),
+               'adjectives': sorted(getattr(d.adjectives, 'hits', ())),
+               'eomis': sorted(getattr(d.eomis, 'hits', ())),
+               'rules': [[k, [list(p) for p in dict.__getitem__(d.rules, k)]] for k in sorted(d.rules.hits)],
+               'standalones': list(lk.standalones), 'max_len': lk.max_len,
+               'prefer_exact_match': lk.prefer_exact_match}
+        out[name] = {'lexicon': lex, 'sentences': sents, 'lattices': lats}
+    path = os.path.join(HERE, 'lookup.json.gz')
+    with gzip.open(path, 'wt', encoding='utf-8') as f:
+        json.dump(out, f, ensure_ascii=False, separators=(',', ':'))
+    print('wrote', path, os.path.getsize(path), 'bytes')
 
 
 if __name__ == '__main__':

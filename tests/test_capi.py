@@ -60,3 +60,21 @@ def test_kernel_name_without_gpu():
     assert lib.lt_kernel_name(32) == b'lt_beam_pk'
     assert lib.lt_kernel_name(33) is None
     assert lib.lt_kernel_name(0) is None or lib.lt_kernel_name(0) == b'lt_viterbi_pk'
+
+
+@pytest.mark.parametrize('header', ['lattice_pack.h', 'lattice_lookup.h'])
+def test_host_side_headers_are_exported(header):
+    """The packer and lattice-builder entry points (include/lattice_pack.h,
+    include/lattice_lookup.h) are exported and load through ctypes."""
+    lib = _build.build(verbose=False)
+    text = open(os.path.join(os.path.dirname(HEADER), header)).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    declared = sorted(set(re.findall(r'\b(lt_[a-z_0-9]+)\s*\(', text)))
+    assert declared
+    out = subprocess.run(['nm', '-D', '--defined-only', lib], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r'\bT (lt_\w+)', out))
+    assert [s for s in declared if s not in exported] == []
+    loaded = _capi.load()
+    for s in declared:
+        getattr(loaded, s)

@@ -1,0 +1,142 @@
+"""Native lattice builder (include/lattice_lookup.h, lookup.NativeLexicon)
+against the reference's own lattices.
+
+* tests/golden/lookup.json.gz (made by make_golden.py with the reference's
+  MorphemeLookup, PYTHONHASHSEED=0): sentences of the base and demo
+  dictionaries, incl. eojeols whose lemma candidates depend on the
+  {word[i:i+2], word[i:i+3]} set order (lemmatizer.py:107) and edge strings;
+  the lattice must equal the reference's field for field, in node order;
+* the str-hash / set-order reproduction against this interpreter's hash()
+  and real sets (any hash seed);
+* threads and batching do not change the lattices.
+"""
+
+import gzip
+import json
+import os
+import random
+from types import SimpleNamespace
+
+import pytest
+
+from lattice_based_tagger_amd import lookup as LK
+from lattice_based_tagger_amd.native_packer import Unsupported
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ZERO_KEY = (0, 0)                      # PYTHONHASHSEED=0 (the fixture's)
+
+
+def _fixture():
+    with gzip.open(os.path.join(HERE, 'golden', 'lookup.json.gz'), 'rt', encoding='utf-8') as f:
+        return json.load(f)
+
+
+def fixture_dictionary(lex):
+    """A MorphemeDictionary-shaped object from the fixture's restriction."""
+    t2m = {t: set(lex['morphs'][t]) for t in lex['tags']}
+    return SimpleNamespace(tag_to_morphs=t2m, verbs=set(lex['verbs']), adjectives=set(lex['adjectives']),
+                           eomis=set(lex['eomis']),
+                           rules={k: tuple(tuple(p) for p in v) for k, v in lex['rules']})
+
+
+def fixture_lexicon(entry, key=ZERO_KEY):
+    lex = entry['lexicon']
+    return LK.NativeLexicon(fixture_dictionary(lex), lex['standalones'], lex['max_len'],
+                            lex['prefer_exact_match'], hash_key=key)
+
+
+@pytest.fixture(scope='module')
+def fix():
+    return _fixture()
+
+
+@pytest.mark.parametrize('name', ['base', 'demo'])
+def test_lattices_equal_reference(fix, name):
+    entry = fix[name]
+    lex = fixture_lexicon(entry)
+    sents = entry['sentences']
+    lat = lex.lookup(sents, n_threads=3)
+    for s, (sent, exp) in enumerate(zip(sents, entry['lattices'])):
+        got = [[list(w) for w in ws] for ws in lat.bindex(s)]
+        assert got == exp, (name, sent)
+        for ws in lat.bindex(s):
+            for w in ws:
+                assert type(w.is_l) is bool and type(w.len) is int
+    assert any(lat.empty(s) for s in range(len(sents)))          # 'ㅋㅋㅋ': bindex == []
+
+
+def test_set_order_matters_and_is_reproduced(fix):
+    """The order-sensitive eojeols change lattices under another hash key."""
+    entry = fix['base']
+    sents = entry['sentences']
+    idx = [i for i, s in enumerate(sents) if '겨우나' in s or '누우라고' in s]
+    assert idx
+    wrong = fixture_lexicon(entry, key=(1, 2)).lookup([sents[i] for i in idx])
+    right = fixture_lexicon(entry).lookup([sents[i] for i in idx])
+    diff = 0
+    for j, i in enumerate(idx):
+        assert [[list(w) for w in ws] for ws in right.bindex(j)] == entry['lattices'][i]
+        diff += [[list(w) for w in ws] for ws in wrong.bindex(j)] != entry['lattices'][i]
+    assert diff > 0
+
+
+def test_str_hash_and_set_order_match_interpreter():
+    key = LK.process_hash_key()
+    rng = random.Random(3)
+    alph = 'ab\xe9\xff가나했랬우니\U0001F600\U00010000'
+    for _ in range(3000):
+        a = ''.join(rng.choice(alph) for _ in range(rng.randint(0, 4)))
+        b = a + ''.join(rng.choice(alph) for _ in range(rng.randint(0, 2)))
+        assert LK.py_str_hash(a, key) == hash(a)
+        assert LK.set2_order(a, b, key) == list({a, b})
+    LK.self_check()
+
+
+def test_zero_key_is_hash_seed_zero():
+    # CPython with PYTHONHASHSEED=0: hash('a') is fixed
+    assert LK.py_str_hash('', ZERO_KEY) == 0
+    assert LK.py_str_hash('a', ZERO_KEY) == -7583489610679606711
+    assert LK.py_str_hash('가나', ZERO_KEY) == LK.py_str_hash('가나', (0, 0))
+
+
+def test_threads_and_batching_do_not_change_lattices(fix):
+    entry = fix['base']
+    lex = fixture_lexicon(entry)
+    sents = entry['sentences'] * 3
+    one = lex.lookup(sents, n_threads=1)
+    many = lex.lookup(sents, n_threads=8)
+    for s in range(len(sents)):
+        assert one.bindex(s) == many.bindex(s)
+    single = lex.lookup([sents[5]])
+    assert single.bindex(0) == one.bindex(5)
+
+
+def test_rejects_what_it_cannot_represent(fix):
+    lex = fixture_lexicon(fix['demo'])
+    with pytest.raises(Unsupported):
+        lex.lookup([b'bytes'])
+    d = fixture_dictionary(fix['demo']['lexicon'])
+    d.tag_to_morphs['Noun'] = {1, 2}
+    with pytest.raises(Unsupported):
+        LK.NativeLexicon(d, ['Noun'], 0, hash_key=ZERO_KEY)
+
+
+def test_tagger_native_lattice_matches_fixture(fix):
+    """Tagger.lattice goes through the native builder for a supplied lexicon."""
+    from lattice_based_tagger_amd import Tagger
+    entry = fix['demo']
+    t = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=fixture_lexicon(entry))
+    for sent, exp in list(zip(entry['sentences'], entry['lattices']))[:10]:
+        bindex, chars = t.lattice(sent)
+        assert chars == sent.replace(' ', '')
+        assert [[list(w) for w in ws] for ws in bindex] == exp
+
+
+def test_tagger_raises_index_error_on_empty_lattice(fix):
+    """'ㅋㅋㅋ' has no dictionary node: bindex == [] and Tagger.tag raises
+    IndexError (lookup.py:362-363, beam.py:32) before any device work."""
+    from lattice_based_tagger_amd import Tagger
+    entry = fix['base']
+    t = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=fixture_lexicon(entry))
+    with pytest.raises(IndexError):
+        t.tag_batch(['ㅋㅋㅋ'])
