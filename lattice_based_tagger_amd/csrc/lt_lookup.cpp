@@ -278,13 +278,29 @@ struct lt_lexicon {
   uint64_t k0 = 0, k1 = 0;
 };
 
+namespace {
+// An uninitialised array (filled in parallel by lt_lexicon_lookup).
+template <class T>
+struct Arr {
+  std::unique_ptr<T[]> p;
+  int64_t n = 0;
+  bool alloc(int64_t k) {
+    p.reset(new (std::nothrow) T[(size_t)std::max<int64_t>(k, 1)]);
+    n = k;
+    return p != nullptr;
+  }
+  T* data() const { return p.get(); }
+};
+}  // namespace
+
 struct lt_lattices {
-  std::vector<uint32_t> chars;
-  std::vector<int64_t> char_off, slot_off, sent_words;
-  std::string wb, mb, m1b, tb, t1b;
-  std::vector<int64_t> woff, moff, m1off, toff, t1off;
-  std::vector<uint8_t> m1null, t1null;
-  std::vector<int64_t> len, e, b, is_l;
+  int64_t n_sent = 0, n_words = 0;
+  Arr<uint32_t> chars;
+  Arr<int64_t> char_off, slot_off, sent_words;
+  Arr<char> wb, mb, m1b, tb, t1b;
+  Arr<int64_t> woff, moff, m1off, toff, t1off;
+  Arr<uint8_t> m1null, t1null;
+  Arr<int64_t> len, e, b, is_l;
 };
 
 namespace {
@@ -347,29 +363,33 @@ struct Worker {
         consider(w_off, m, len, b, e, is_l, out);
       }
       // 1 syllable conjugation: the pairs of rules[c], |rules[c]| times over
-      // (the nested loop of lemmatizer.py:100-101)
-      if (const Info* ci = find(w + i, 1)) {
-        for (int32_t rep = 0; rep < ci->rule_n; ++rep)
-          for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
-            const RulePair& rp = R[(size_t)q];
-            set_cand(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, w + i + 1, m - i - 1);
-            consider(w_off, m, len, b, e, is_l, out);
-          }
+      // (the nested loop of lemmatizer.py:100-101) -- every repetition emits
+      // the same words, so one pass is scored and its words repeated
+      if (const Info* ci = find(w + i, 1); ci && ci->rule_n > 0) {
+        const size_t first = out.size();
+        for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
+          const RulePair& rp = R[(size_t)q];
+          set_cand(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, w + i + 1, m - i - 1);
+          consider(w_off, m, len, b, e, is_l, out);
+        }
+        const size_t pass = out.size() - first;
+        if (pass) out.reserve(out.size() + pass * (size_t)(ci->rule_n - 1));
+        for (int32_t rep = 1; rep < ci->rule_n && pass; ++rep)
+          for (size_t x = 0; x < pass; ++x) out.push_back(out[first + x]);
       }
       // 2 or 3 syllables conjugation: for conj in {word[i:i+2], word[i:i+3]}
-      // (set iteration order, lemmatizer.py:107); eomi + r[1:]
+      // (set iteration order, lemmatizer.py:107); eomi + r[1:].  The order
+      // only matters when both surfaces have rules.
       const uint32_t n2 = std::min<uint32_t>(2, m - i), n3 = std::min<uint32_t>(3, m - i);
       const uint32_t* rest = w + std::min<uint32_t>(m, i + 2);
       const uint32_t nrest = m - std::min<uint32_t>(m, i + 2);
-      uint32_t conj[2] = {n2, n3};
-      int nconj = 2;
-      if (n2 == n3) {
-        nconj = 1;
-      } else if (set2_second_first(py_str_hash(w + i, n2, lx.k0, lx.k1), py_str_hash(w + i, n3, lx.k0, lx.k1))) {
+      const Info* c2 = find(w + i, n2);
+      const Info* c3 = n3 != n2 ? find(w + i, n3) : nullptr;
+      const Info* conj[2] = {c2 && c2->rule_n ? c2 : nullptr, c3 && c3->rule_n ? c3 : nullptr};
+      if (conj[0] && conj[1] &&
+          set2_second_first(py_str_hash(w + i, n2, lx.k0, lx.k1), py_str_hash(w + i, n3, lx.k0, lx.k1)))
         std::swap(conj[0], conj[1]);
-      }
-      for (int c = 0; c < nconj; ++c) {
-        const Info* ci = find(w + i, conj[c]);
+      for (const Info* ci : conj) {
         if (!ci) continue;
         for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
           const RulePair& rp = R[(size_t)q];
@@ -397,6 +417,7 @@ struct Worker {
   }
 
   bool is_noun_josa(uint32_t e_off, uint32_t n, uint32_t i) {
+    if (lx.dict_noun < 0 || lx.dict_josa < 0) return false;
     return has(find(text + e_off, i), lx.dict_noun) && has(find(text + e_off + i, n - i), lx.dict_josa);
   }
 
@@ -510,17 +531,54 @@ void run_chunk(const lt_lexicon& lx, const lt_text_desc& td, int32_t s0, int32_t
   }
 }
 
-void append_offsets(std::vector<int64_t>& dst, const std::vector<int64_t>& src, int64_t base) {
-  for (size_t i = 1; i < src.size(); ++i) dst.push_back(src[i] + base);
-}
-
-lt_strings view_of(const std::string& blob, const std::vector<int64_t>& off, const std::vector<uint8_t>* null) {
+lt_strings view_of(const Arr<char>& blob, const Arr<int64_t>& off, const uint8_t* null, int64_t n) {
   lt_strings s;
   s.data = blob.data();
   s.off = off.data();
-  s.null = null ? null->data() : nullptr;
-  s.n = (int64_t)off.size() - 1;
+  s.null = null;
+  s.n = n;
   return s;
+}
+
+// Where chunk c's pieces go in the merged arrays.
+struct Base {
+  int64_t words = 0, slots = 0, sents = 0, wb = 0, mb = 0, m1b = 0, tb = 0, t1b = 0;
+};
+
+// Copy chunk c into the merged arrays at base; frees the chunk.
+void merge_chunk(Chunk& c, const Base& at, lt_lattices& L) {
+  const int64_t W = (int64_t)c.len.size();
+  auto blob = [](Arr<char>& dst, int64_t base, const std::string& src) {
+    if (!src.empty()) memcpy(dst.data() + base, src.data(), src.size());
+  };
+  blob(L.wb, at.wb, c.wb);
+  blob(L.mb, at.mb, c.mb);
+  blob(L.m1b, at.m1b, c.m1b);
+  blob(L.tb, at.tb, c.tb);
+  blob(L.t1b, at.t1b, c.t1b);
+  auto offs = [&](Arr<int64_t>& dst, const std::vector<int64_t>& src, int64_t base) {
+    int64_t* d = dst.data() + at.words + 1;
+    for (int64_t i = 0; i < W; ++i) d[i] = src[(size_t)i + 1] + base;
+  };
+  offs(L.woff, c.woff, at.wb);
+  offs(L.moff, c.moff, at.mb);
+  offs(L.m1off, c.m1off, at.m1b);
+  offs(L.toff, c.toff, at.tb);
+  offs(L.t1off, c.t1off, at.t1b);
+  auto cols = [&](auto& dst, const auto& src) {
+    if (W) memcpy(dst.data() + at.words, src.data(), (size_t)W * sizeof(src[0]));
+  };
+  cols(L.m1null, c.m1null);
+  cols(L.t1null, c.t1null);
+  cols(L.len, c.len);
+  cols(L.e, c.e);
+  cols(L.b, c.b);
+  cols(L.is_l, c.is_l);
+  int64_t run = at.words;
+  for (size_t x = 0; x < c.slot_n.size(); ++x) L.slot_off.data()[at.slots + (int64_t)x + 1] = (run += c.slot_n[x]);
+  run = at.words;
+  for (size_t x = 0; x < c.sent_n.size(); ++x) L.sent_words.data()[at.sents + (int64_t)x + 1] = (run += c.sent_n[x]);
+  c = Chunk();
 }
 
 }  // namespace
@@ -682,36 +740,46 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_
   std::unique_ptr<lt_lattices> L(new (std::nothrow) lt_lattices);
   if (!L) return lt::set_error(LT_ENOMEM, "lt_lexicon_lookup: out of host memory");
   const int64_t C = S > 0 ? td->char_off[S] : 0;
-  L->chars.assign(td->chars, td->chars + C);
-  L->char_off.assign(td->char_off, td->char_off + S + 1);
-  if (S == 0) L->char_off.assign(1, 0);
-  L->slot_off.push_back(0);
-  L->sent_words.push_back(0);
-  for (auto* v : {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off}) v->push_back(0);
-  for (const Chunk& c : ck) {
-    for (int64_t x : c.slot_n) L->slot_off.push_back(L->slot_off.back() + x);
-    for (int64_t x : c.sent_n) L->sent_words.push_back(L->sent_words.back() + x);
-    append_offsets(L->woff, c.woff, (int64_t)L->wb.size());
-    append_offsets(L->moff, c.moff, (int64_t)L->mb.size());
-    append_offsets(L->m1off, c.m1off, (int64_t)L->m1b.size());
-    append_offsets(L->toff, c.toff, (int64_t)L->tb.size());
-    append_offsets(L->t1off, c.t1off, (int64_t)L->t1b.size());
-    L->wb += c.wb;
-    L->mb += c.mb;
-    L->m1b += c.m1b;
-    L->tb += c.tb;
-    L->t1b += c.t1b;
-    L->m1null.insert(L->m1null.end(), c.m1null.begin(), c.m1null.end());
-    L->t1null.insert(L->t1null.end(), c.t1null.begin(), c.t1null.end());
-    L->len.insert(L->len.end(), c.len.begin(), c.len.end());
-    L->e.insert(L->e.end(), c.e.begin(), c.e.end());
-    L->b.insert(L->b.end(), c.b.begin(), c.b.end());
-    L->is_l.insert(L->is_l.end(), c.is_l.begin(), c.is_l.end());
+  // bases of the chunks in the merged arrays
+  std::vector<Base> at(ck.size() + 1);
+  for (size_t t = 0; t < ck.size(); ++t) {
+    const Chunk& c = ck[t];
+    Base& nx = at[t + 1];
+    nx = at[t];
+    nx.words += (int64_t)c.len.size();
+    nx.slots += (int64_t)c.slot_n.size();
+    nx.sents += (int64_t)c.sent_n.size();
+    nx.wb += (int64_t)c.wb.size();
+    nx.mb += (int64_t)c.mb.size();
+    nx.m1b += (int64_t)c.m1b.size();
+    nx.tb += (int64_t)c.tb.size();
+    nx.t1b += (int64_t)c.t1b.size();
   }
-  if ((int64_t)L->slot_off.size() != C + 1) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: slot count mismatch");
-  // non-null data pointers for empty columns
-  for (std::string* bl : {&L->wb, &L->mb, &L->m1b, &L->tb, &L->t1b}) bl->reserve(1);
-  if (L->chars.empty()) L->chars.reserve(1);
+  const Base& tot = at.back();
+  if (tot.slots != C || tot.sents != S) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: slot count mismatch");
+  const int64_t W = tot.words;
+  bool ok = L->chars.alloc(C) && L->char_off.alloc(S + 1) && L->slot_off.alloc(C + 1) &&
+            L->sent_words.alloc(S + 1) && L->wb.alloc(tot.wb) && L->mb.alloc(tot.mb) &&
+            L->m1b.alloc(tot.m1b) && L->tb.alloc(tot.tb) && L->t1b.alloc(tot.t1b);
+  for (Arr<int64_t>* a : {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off}) ok = ok && a->alloc(W + 1);
+  ok = ok && L->m1null.alloc(W) && L->t1null.alloc(W);
+  for (Arr<int64_t>* a : {&L->len, &L->e, &L->b, &L->is_l}) ok = ok && a->alloc(W);
+  if (!ok) return lt::set_error(LT_ENOMEM, "lt_lexicon_lookup: out of host memory");
+  L->n_sent = S;
+  L->n_words = W;
+  if (C) memcpy(L->chars.data(), td->chars, (size_t)C * 4);
+  if (S) memcpy(L->char_off.data(), td->char_off, (size_t)(S + 1) * 8);
+  else L->char_off.data()[0] = 0;
+  L->slot_off.data()[0] = 0;
+  L->sent_words.data()[0] = 0;
+  for (Arr<int64_t>* a : {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off}) a->data()[0] = 0;
+  {
+    std::vector<std::thread> th;
+    for (size_t t = 0; t + 1 < ck.size(); ++t)
+      th.emplace_back([&, t] { merge_chunk(ck[t], at[t], *L); });
+    merge_chunk(ck.back(), at[ck.size() - 1], *L);
+    for (std::thread& x : th) x.join();
+  }
   *out = L.release();
   return LT_OK;
 }
@@ -719,16 +787,17 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_
 lt_status lt_lattices_view(const lt_lattices* L, lt_lattice_view* v) {
   if (!L || !v) return lt::set_error(LT_EINVAL, "lt_lattices_view: NULL argument");
   lt_lattice_desc& d = v->lattice;
-  d.n_sent = (int32_t)L->char_off.size() - 1;
+  const int64_t W = L->n_words;
+  d.n_sent = (int32_t)L->n_sent;
   d.chars = L->chars.data();
   d.char_off = L->char_off.data();
   d.slot_off = L->slot_off.data();
-  d.n_words = (int64_t)L->len.size();
-  d.word = view_of(L->wb, L->woff, nullptr);
-  d.morph0 = view_of(L->mb, L->moff, nullptr);
-  d.tag0 = view_of(L->tb, L->toff, nullptr);
-  d.morph1 = view_of(L->m1b, L->m1off, &L->m1null);
-  d.tag1 = view_of(L->t1b, L->t1off, &L->t1null);
+  d.n_words = W;
+  d.word = view_of(L->wb, L->woff, nullptr, W);
+  d.morph0 = view_of(L->mb, L->moff, nullptr, W);
+  d.tag0 = view_of(L->tb, L->toff, nullptr, W);
+  d.morph1 = view_of(L->m1b, L->m1off, L->m1null.data(), W);
+  d.tag1 = view_of(L->t1b, L->t1off, L->t1null.data(), W);
   d.len = L->len.data();
   d.e = L->e.data();
   d.is_l = L->is_l.data();
