@@ -90,6 +90,13 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lexicon, const lt_text_desc* text,
                             lt_lattices** out);
 lt_status lt_lattices_view(const lt_lattices* lattices, lt_lattice_view* view);
 lt_status lt_lattices_destroy(lt_lattices* lattices);
+/* Bulk string extraction for re-materialising nodes: field 0..4 = word,
+ * morph0, morph1, tag0, tag1; the strings of nodes idx[0..n) are written to
+ * out back to back, each followed by a NUL byte (a None value writes just
+ * the NUL).  cap: bytes available; *used receives the bytes written (or
+ * needed, with LT_EINVAL, when cap is too small). */
+lt_status lt_lattices_strings(const lt_lattices* lattices, int field, const int64_t* idx, int64_t n,
+                              char* out, int64_t cap, int64_t* used);
 
 /* CPython 3.10 hash() of the str with these code points under SipHash key
  * (k0, k1) -- test hook for the set-order reproduction. */

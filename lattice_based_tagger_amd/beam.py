@@ -12,6 +12,7 @@ GPU by the HIP kernel (``csrc/lt_decode.hip``).
 high-throughput entry point.
 """
 
+import gc
 import weakref
 
 import os
@@ -21,7 +22,8 @@ import numpy as np
 from . import _capi
 from .lowering import LoweredModel
 from .packer import pack
-from .word import bos_word, eos_word
+from .tagset import Unk
+from .word import Word, bos_word, eos_word
 
 __all__ = ['beam_search', 'beam_search_batch', 'Beam', 'Sequence', 'Decoder']
 
@@ -131,15 +133,28 @@ class Decoder:
             model._device_models[self.device] = dm
         return dm
 
+    # node records per launch (lt_batch_create takes < 2^31 B of 48 B records)
+    MAX_NODES = 40_000_000
+
     def decode_packed(self, model, packed, k):
-        """Decode a PackedBatch; returns (count, length, score, codes, cum_n)."""
+        """Decode a PackedBatch (in launches of at most MAX_NODES nodes);
+        returns (count, length, score, codes, cum_n)."""
         dm = self.device_model(model)
-        db = _capi.DeviceBatch(self.ctx, packed, max_k=k)
-        try:
-            count, length, score, codes = db.decode(dm, k)
-            return count, length, score, codes, db.cum_n
-        finally:
-            db.close()
+        parts = []
+        for s0, s1 in packed.split(self.MAX_NODES):
+            piece = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
+            db = _capi.DeviceBatch(self.ctx, piece, max_k=k)
+            try:
+                parts.append(db.decode(dm, k))
+            finally:
+                db.close()
+        if len(parts) == 1:
+            count, length, score, codes = parts[0]
+        else:
+            count, length, score, codes = (np.concatenate([p[i] for p in parts]) for i in range(4))
+        cum_n = np.zeros(packed.n_sent + 1, dtype=np.int64)
+        np.cumsum(packed.sent_n, out=cum_n[1:])
+        return count, length, score, codes, cum_n
 
 
 def pack_lattices(sentences, model, max_len):
@@ -175,26 +190,88 @@ def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device
     return decode_batch(packed, objs, [ch for _, ch in sentences], model, k, device)
 
 
-def decode_batch(packed, objs, chars_list, model, k, device=0):
+def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False):
     """Decode a packed batch and re-materialise the matures: ``objs[s][i]`` is
-    the Word of sentence s's local node i, ``chars_list[s]`` its characters."""
+    the Word of sentence s's local node i, ``chars_list[s]`` its characters.
+    ``best_only``: only the best mature of each sentence (what Tagger.tag
+    returns, tagger.py:78)."""
     if k == 0:
         # beam_size=0 keeps no hypothesis past BOS (beam.py:85 slices to [])
         return [[Sequence([bos_word(), eos_word(0)], 0)] if len(ch) == 0 else []
                 for ch in chars_list]
     count, length, score, codes, cum_n = Decoder.get(device).decode_packed(model, packed, k)
+    T = 1 if best_only else k
+    if objs and hasattr(getattr(objs[0], 'words', None), 'words_bulk'):
+        return _materialise_bulk(packed, objs, chars_list, k, T, count, length, score, codes, cum_n)
     out = []
     for s, chars in enumerate(chars_list):
         n = len(chars)
         nodes = objs[s]
         base = k * int(cum_n[s])
         matures = []
-        for t in range(int(count[s])):
+        for t in range(min(int(count[s]), T)):
             L = int(length[s, t])
             off = base + t * n
             path = [nodes[0]] + [nodes[c] for c in codes[off:off + L]] + [eos_word(n)]
             sc = float(score[s, t]) if n > 0 else 0
             matures.append(Sequence(path, sc, 0))
+        out.append(matures)
+    return out
+
+
+def _materialise_bulk(*args):
+    """decode_batch's result for lattices built natively: every path node's
+    Word is built in bulk (lookup.NativeLattices.words_bulk).  The cyclic GC
+    is paused meanwhile: millions of fresh tuples would otherwise trigger
+    repeated full collections (4x the construction time)."""
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        return _materialise_bulk_body(*args)
+    finally:
+        if enabled:
+            gc.enable()
+
+
+def _materialise_bulk_body(packed, objs, chars_list, k, T, count, length, score, codes, cum_n):
+    S = len(chars_list)
+    n = np.asarray(packed.sent_n, dtype=np.int64)
+    t = np.arange(T, dtype=np.int64)
+    valid = t[None, :] < np.minimum(count, T)[:, None]                     # S x T
+    L = np.where(valid, length[:, :T], 0).astype(np.int64)
+    starts = k * cum_n[:-1, None] + t[None, :] * n[:, None]
+    Lf = L.ravel()
+    total = int(Lf.sum())
+    seg = np.repeat(np.arange(Lf.size), Lf)
+    first = np.zeros(Lf.size, dtype=np.int64)
+    np.cumsum(Lf[:-1], out=first[1:])
+    within = np.arange(total, dtype=np.int64) - first[seg]
+    local = codes[starts.ravel()[seg] + within].astype(np.int64)
+    glob = packed.sent_node_off[seg // T] + local
+    src = objs[0].src[glob]
+    lat = objs[0].words
+    flat = [None] * total
+    dic = np.flatnonzero(src >= 0)
+    for j, w in zip(dic.tolist(), lat.words_bulk(src[dic])):
+        flat[j] = w
+    for j in np.flatnonzero(src < 0).tolist():          # synthesised Unknown nodes (BOS never on a path)
+        code = -2 - int(src[j])
+        b, d = code // 8, code % 8 + 1
+        sub = chars_list[int(seg[j]) // T][b:b + d]
+        flat[j] = Word(sub, sub, None, Unk, None, d, b, b + d, False)
+    out = []
+    pos = 0
+    cnt = np.minimum(count, T).tolist()
+    Ll = L.tolist()
+    sc = score.tolist()
+    for s in range(S):
+        nch = len(chars_list[s])
+        matures = []
+        for tt in range(cnt[s]):
+            ln = Ll[s][tt]
+            matures.append(Sequence([bos_word()] + flat[pos:pos + ln] + [eos_word(nch)],
+                                    sc[s][tt] if nch > 0 else 0, 0))
+            pos += ln
         out.append(matures)
     return out
 

@@ -806,6 +806,32 @@ lt_status lt_lattices_view(const lt_lattices* L, lt_lattice_view* v) {
   return LT_OK;
 }
 
+lt_status lt_lattices_strings(const lt_lattices* L, int field, const int64_t* idx, int64_t n, char* out,
+                              int64_t cap, int64_t* used) {
+  if (!L || (n > 0 && !idx) || field < 0 || field > 4)
+    return lt::set_error(LT_EINVAL, "lt_lattices_strings: bad argument");
+  const Arr<char>* blobs[] = {&L->wb, &L->mb, &L->m1b, &L->tb, &L->t1b};
+  const Arr<int64_t>* offs[] = {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off};
+  const char* blob = blobs[field]->data();
+  const int64_t* off = offs[field]->data();
+  int64_t need = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = idx[i];
+    if (v < 0 || v >= L->n_words) return lt::set_error(LT_EINVAL, "lt_lattices_strings: index %lld", (long long)v);
+    need += off[v + 1] - off[v] + 1;
+  }
+  if (used) *used = need;
+  if (need > cap || (need > 0 && !out)) return lt::set_error(LT_EINVAL, "lt_lattices_strings: %lld bytes needed", (long long)need);
+  char* p = out;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = idx[i], len = off[v + 1] - off[v];
+    memcpy(p, blob + off[v], (size_t)len);
+    p += len;
+    *p++ = '\0';
+  }
+  return LT_OK;
+}
+
 lt_status lt_lattices_destroy(lt_lattices* L) {
   delete L;
   return LT_OK;

@@ -22,6 +22,7 @@ fall back to the Python lookup.
 """
 
 import ctypes as C
+import functools
 import random
 import sys
 
@@ -58,6 +59,8 @@ _SIGS = {
     'lt_lattices_destroy': (C.c_int32, [C.c_void_p]),
     'lt_py_str_hash': (C.c_int64, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]),
     'lt_py_set2_second_first': (C.c_int, [C.c_int64, C.c_int64]),
+    'lt_lattices_strings': (C.c_int32, [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
+                                        C.c_int64, C.POINTER(C.c_int64)]),
 }
 
 
@@ -265,6 +268,32 @@ def dictionary_fingerprint(dictionary):
     return tuple(parts)
 
 
+_new_word = functools.partial(tuple.__new__, Word)      # Word from a 9-tuple, one C call
+
+
+def _gather_strings(blob, off, idx):
+    """Strings blob[off[i]:off[i+1]] for i in idx (UTF-8), via one gather and
+    one decode: the selected byte ranges are joined with NUL separators
+    (falling back to per-string slicing when the blob itself holds NULs)."""
+    if b'\0' in blob:
+        return [blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()]
+    starts = off[idx]
+    lens = off[idx + 1] - starts
+    n = idx.size
+    total = int(lens.sum())
+    src = np.frombuffer(blob, dtype=np.uint8)
+    out = np.zeros(total + n, dtype=np.uint8)              # NUL after every string
+    dst_start = np.zeros(n, dtype=np.int64)
+    np.cumsum(lens[:-1] + 1, out=dst_start[1:])
+    if total:
+        seg = np.repeat(np.arange(n), lens)
+        cum = np.zeros(n, dtype=np.int64)
+        np.cumsum(lens[:-1], out=cum[1:])
+        within = np.arange(total, dtype=np.int64) - cum[seg]
+        out[dst_start[seg] + within] = src[starts[seg] + within]
+    return out.tobytes().decode('utf-8').split('\0')[:n]
+
+
 class NativeLattices:
     """Lattices built by the library: columnar (``desc`` for lt_packer_pack)
     plus lazy ``Word`` materialisation and the reference-shaped ``bindex``."""
@@ -324,6 +353,34 @@ class NativeLattices:
 
     def __getitem__(self, i):
         return self.word(int(i))
+
+    def words_bulk(self, idx):
+        """[Word] of global node indices ``idx`` (int array), built with one
+        ragged gather + one UTF-8 decode per field instead of per node."""
+        idx = np.asarray(idx, dtype=np.int64)
+        if idx.size == 0:
+            return []
+        c = self._columns()
+        fields = []
+        idx = np.ascontiguousarray(idx)
+        for f, name in enumerate(('word', 'morph0', 'morph1', 'tag0', 'tag1')):
+            (blob, off), null = c[name]
+            need = int((off[idx + 1] - off[idx]).sum()) + idx.size
+            buf = C.create_string_buffer(need)
+            used = C.c_int64()
+            _capi.check(self.lib.lt_lattices_strings(self.handle, f, idx.ctypes.data, idx.size, buf,
+                                                     need, C.byref(used)))
+            vals = buf.raw[:need].decode('utf-8').split('\0')[:idx.size] if b'\0' not in blob else \
+                [blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()]
+            if null is not None:
+                for j in np.flatnonzero(null[idx]).tolist():
+                    vals[j] = None
+            fields.append(vals)
+        lens = c['len'][idx].tolist()
+        bs = c['b'][idx].tolist()
+        es = c['e'][idx].tolist()
+        isl = (c['is_l'][idx] != 0).tolist()
+        return list(map(_new_word, zip(*fields, lens, bs, es, isl)))
 
     def empty(self, s):
         """True when sentence s has characters but no node: the reference's

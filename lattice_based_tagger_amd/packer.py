@@ -45,6 +45,38 @@ class PackedBatch:
     def n_nodes(self):
         return int(self.node_word.shape[0])
 
+    NODE_FIELDS = ('node_word', 'node_morph0', 'node_tag', 'node_mask', 'node_pre', 'node_f4',
+                   'node_f5', 'node_f6')
+
+    def slice(self, s0, s1):
+        """Sentences [s0, s1) as a batch of their own (views; offsets rebased)."""
+        n0, n1 = int(self.sent_node_off[s0]), int(self.sent_node_off[s1])
+        p0, p1 = int(self.sent_span_off[s0]), int(self.sent_span_off[s1])
+        out = dict(max_len=self.max_len, n_post=self.n_post, has_trigram=self.has_trigram,
+                   sent_n=self.sent_n[s0:s1],
+                   sent_node_off=self.sent_node_off[s0:s1 + 1] - n0,
+                   sent_span_off=self.sent_span_off[s0:s1 + 1] - p0,
+                   span_start=self.span_start[p0:p1],
+                   node_post=self.node_post[:, n0:n1] if self.n_post else np.zeros((0, n1 - n0)))
+        for f in self.NODE_FIELDS:
+            out[f] = getattr(self, f)[n0:n1]
+        return PackedBatch(**out)
+
+    def split(self, max_nodes):
+        """[(s0, s1)] sentence ranges of at most max_nodes nodes each (a single
+        larger sentence gets a range of its own)."""
+        S = self.n_sent
+        if S == 0:
+            return [(0, 0)]
+        cuts, s0 = [], 0
+        off = self.sent_node_off
+        while s0 < S:
+            s1 = int(np.searchsorted(off, off[s0] + max_nodes, side='right')) - 1
+            s1 = min(max(s1, s0 + 1), S)
+            cuts.append((s0, s1))
+            s0 = s1
+        return cuts
+
 
 def _span_candidates(bindex_b, b, n, max_len):
     """Dict e -> candidates of bindex[b] ending at e, in bindex order."""

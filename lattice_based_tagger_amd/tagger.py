@@ -203,5 +203,5 @@ class Tagger:
             matures = beam_search_batch(lattices, self.score_funcs, beam_size=k, device=self.device)
         else:
             packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
-            matures = decode_batch(packed, views, lat.chars, model, k, self.device)
+            matures = decode_batch(packed, views, lat.chars, model, k, self.device, best_only=True)
         return [m[0] for m in matures]

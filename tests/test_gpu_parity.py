@@ -155,3 +155,17 @@ def test_ragged_and_empty_batch(gpu_decoder):
         alone = beam_search_batch([(b, ch)], funcs, beam_size=5)[0]
         assert [float(x.score).hex() for x in m] == [float(x.score).hex() for x in alone]
     assert beam_search_batch([], funcs, beam_size=3) == []
+
+
+def test_decode_in_several_launches(gpu_decoder, monkeypatch):
+    """A batch above the per-launch node budget is decoded in sentence-range
+    launches with the same results (Decoder.decode_packed)."""
+    from lattice_based_tagger_amd.beam import Decoder
+    cases = [c for c in load('base') if c.bindex]
+    lats = [(c.bindex, c.chars) for c in cases]
+    whole = beam_search_batch(lats, cases[0].funcs, beam_size=5)
+    monkeypatch.setattr(Decoder, 'MAX_NODES', 3000)
+    pieces = beam_search_batch(lats, cases[0].funcs, beam_size=5)
+    for a, b in zip(whole, pieces):
+        assert [float(x.score).hex() for x in a] == [float(x.score).hex() for x in b]
+        assert [[tuple(w) for w in x.sequences] for x in a] == [[tuple(w) for w in x.sequences] for x in b]

@@ -140,3 +140,14 @@ def test_tagger_raises_index_error_on_empty_lattice(fix):
     t = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=fixture_lexicon(entry))
     with pytest.raises(IndexError):
         t.tag_batch(['ㅋㅋㅋ'])
+
+
+def test_words_bulk_equals_word(fix):
+    import numpy as np
+    entry = fix['demo']
+    lat = fixture_lexicon(entry).lookup(entry['sentences'])
+    idx = np.random.default_rng(1).integers(0, lat.n_words, 500)
+    bulk = lat.words_bulk(idx)
+    assert [tuple(w) for w in bulk] == [tuple(lat.word(int(i))) for i in idx]
+    assert all(type(w.is_l) is bool for w in bulk)
+    assert lat.words_bulk(np.zeros(0, dtype=np.int64)) == []

@@ -105,3 +105,20 @@ def test_unsupported_scorer_raises():
             return 1.0
     with pytest.raises(NotImplementedError):
         lowering.LoweredModel(SF.BeamScoreFunctions(Custom()))
+
+
+def test_batch_split_and_slice_preserve_results():
+    """Decoding a batch in sentence-range pieces (Decoder.decode_packed over
+    PackedBatch.split/slice) gives the whole batch's results."""
+    raw = synth.make_lattices(300, seed=5, eojeols=7)
+    sm = synth.make_model(raw, seed=5, n_features=5000)
+    packed, keys, coefs = synth.pack_fast(raw, sm)
+    full = lt_oracle.decode(packed, keys, coefs, 3)
+    cuts = packed.split(packed.n_nodes // 7)
+    assert len(cuts) >= 7 and cuts[0][0] == 0 and cuts[-1][1] == packed.n_sent
+    assert all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
+    parts = [lt_oracle.decode(packed.slice(s0, s1), keys, coefs, 3) for s0, s1 in cuts]
+    for i in range(4):
+        got = np.concatenate([p[i] for p in parts])
+        assert np.array_equal(got.view(np.uint8), np.asarray(full[i]).view(np.uint8))
+    assert packed.split(1) == [(s, s + 1) for s in range(packed.n_sent)]

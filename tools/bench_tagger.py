@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""End-to-end Tagger throughput: text -> native lattices -> native packer ->
+HIP decode -> best Sequence objects, per phase.
+
+The base-dictionary sentences of tests/golden/lookup.json.gz (the golden
+'base' set's 101 sentences of 10-20 eojeols and 60 random ones, with the
+restricted reference dictionary that answers their lookups exactly) are
+replicated to --sentences; the model is the golden 'base' set's
+(RegularizationScore + SimpleTrigramFeatureScore).  One JSON line.
+
+    python tools/bench_tagger.py [--sentences 65536] [--k 1] [--threads 0] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
+
+from lattice_based_tagger_amd import _capi  # noqa: E402
+
+_capi.load()
+from golden_io import load  # noqa: E402
+from test_lookup import _fixture, fixture_dictionary, fixture_lexicon  # noqa: E402
+from lattice_based_tagger_amd import Tagger  # noqa: E402
+from lattice_based_tagger_amd.beam import decode_batch, lowered_model  # noqa: E402
+from lattice_based_tagger_amd.native_packer import packer_for  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--sentences', type=int, default=65536)
+    ap.add_argument('--k', type=int, default=1)
+    ap.add_argument('--threads', type=int, default=0)
+    ap.add_argument('--reps', type=int, default=3)
+    a = ap.parse_args()
+    entry = _fixture()['base']
+    funcs = load('base')[0].funcs
+    base = [s for s in entry['sentences'] if len(s.split()) >= 10]
+    sents = (base * (a.sentences // len(base) + 1))[:a.sentences]
+    lex = fixture_lexicon(entry)
+    tagger = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=lex, score_funcs=funcs)
+    tagger.tag_batch(sents[:256], beam_size=a.k)                   # warm: model lowering, device model
+    model = lowered_model(funcs)
+    npk = packer_for(model)
+    best = {}
+    for _ in range(a.reps):
+        t = {}
+        t0 = time.perf_counter()
+        lat = lex.lookup(sents, n_threads=a.threads)
+        t['lookup'] = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+        t['pack'] = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        matures = decode_batch(packed, views, lat.chars, model, a.k, 0)
+        t['decode_and_materialise'] = time.perf_counter() - t0
+        t['total'] = sum(t.values())
+        if not best or t['total'] < best['total']:
+            best = t
+            n_words = lat.n_words
+    t0 = time.perf_counter()
+    out = tagger.tag_batch(sents, beam_size=a.k)
+    api = time.perf_counter() - t0
+    assert len(out) == len(sents) and all(o.score == m[0].score for o, m in zip(out, matures))
+    line = {'metric': 'end-to-end Tagger.tag_batch sentences/s (text -> best Sequence)',
+            'sentences': len(sents), 'k': a.k, 'lattice_nodes': n_words,
+            'phase_s': best, 'sentences_per_s': {p: len(sents) / v for p, v in best.items()},
+            'tag_batch_api_sentences_per_s': len(sents) / api,
+            'lookup_threads': a.threads or os.cpu_count(), 'nproc': os.cpu_count()}
+    print(json.dumps(line))
+
+
+if __name__ == '__main__':
+    main()
