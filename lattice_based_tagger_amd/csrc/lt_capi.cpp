@@ -13,6 +13,7 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lattice_decode.h"
@@ -429,6 +430,33 @@ lt_status lt_model_destroy(lt_model* m) {
 int64_t lt_model_slots(const lt_model* m) { return m ? m->slots : 0; }
 
 // ---------------------------------------------------------------- batch --
+extern "C++" {
+// Host-side batch preparation runs over millions of nodes: split [0, n)
+// into contiguous ranges on up to 32 threads (one range below 64K items).
+template <class F>
+static void parallel_ranges(int64_t n, F fn) {
+  const int64_t per = 1 << 16;
+  int nt = (int)std::min<int64_t>((n + per - 1) / per, 32);
+  nt = std::max(1, std::min(nt, (int)std::max(1u, std::thread::hardware_concurrency())));
+  if (nt == 1) {
+    fn(0, (int64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(fn, t, n * t / nt, n * (t + 1) / nt);
+  fn(0, (int64_t)0, n / nt);
+  for (std::thread& x : th) x.join();
+}
+
+static bool hot_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("LT_HOT");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+}  // extern "C++"
+
 static lt_status validate(const lt_batch_desc* d) {
   if (d->n_sent < 0 || d->n_nodes < 0 || d->n_span < 0 || d->n_post < 0)
     return fail(LT_EINVAL, "batch: negative size");
@@ -448,41 +476,65 @@ static lt_status validate(const lt_batch_desc* d) {
     return fail(LT_EINVAL, "batch: offsets must start at 0");
   if (d->sent_node_off[d->n_sent] != d->n_nodes || d->sent_span_off[d->n_sent] != d->n_span)
     return fail(LT_EINVAL, "batch: offsets do not end at n_nodes / n_span");
-  for (int32_t s = 0; s < d->n_sent; ++s) {
-    const int64_t n = d->sent_n[s];
-    const int64_t nodes = d->sent_node_off[s + 1] - d->sent_node_off[s];
-    const int64_t spans = d->sent_span_off[s + 1] - d->sent_span_off[s];
-    if (n < 0 || spans != LT_MAX_SPAN * n + 1)
-      return fail(LT_EINVAL, "batch: sentence %d has %lld span entries for %lld chars", s,
-                  (long long)spans, (long long)n);
-    if (nodes < 1 || nodes >= MAX_LOCAL_NODES)
-      return fail(LT_EINVAL, "batch: sentence %d has %lld nodes", s, (long long)nodes);
-    const int32_t* ss = d->span_start + d->sent_span_off[s];
-    if (ss[0] != 1 || ss[spans - 1] != nodes)
-      return fail(LT_EINVAL, "batch: sentence %d span table does not cover its nodes", s);
-    for (int64_t e = 1; e <= n; ++e) {
-      const int64_t dmax = std::min<int64_t>(e, d->max_len);
-      for (int j = 0; j < LT_MAX_SPAN; ++j) {
-        const int64_t idx = (e - 1) * LT_MAX_SPAN + j;
-        const int32_t cnt = ss[idx + 1] - ss[idx];
-        const int dd = LT_MAX_SPAN - j;
-        if (cnt < 0) return fail(LT_EINVAL, "batch: sentence %d span table not monotone", s);
-        if (dd <= dmax && cnt == 0)
-          return fail(LT_EINVAL, "batch: sentence %d span (e=%lld,d=%d) has no candidate", s,
-                      (long long)e, dd);
-        if (dd > dmax && cnt != 0)
-          return fail(LT_EINVAL, "batch: sentence %d span (e=%lld,d=%d) is out of range", s,
-                      (long long)e, dd);
+  // per-sentence and per-node checks on threads; the first failure (lowest
+  // index) is reported
+  struct Bad {
+    int64_t at = -1;
+    lt_status st = LT_OK;
+    std::string msg;
+  };
+  auto first_bad = [](std::vector<Bad>& bad) -> const Bad* {
+    for (const Bad& x : bad)
+      if (x.at >= 0) return &x;
+    return nullptr;
+  };
+  std::vector<Bad> bad(32);
+  auto note = [](Bad& b, int64_t at, lt_status st, const char* fmt, long long a, long long c, long long e) {
+    char buf[256];
+    snprintf(buf, sizeof buf, fmt, a, c, e);
+    b.at = at;
+    b.st = st;
+    b.msg = buf;
+  };
+  parallel_ranges(d->n_sent, [&](int t, int64_t lo, int64_t hi) {
+    for (int64_t s = lo; s < hi; ++s) {
+      const int64_t n = d->sent_n[s];
+      const int64_t nodes = d->sent_node_off[s + 1] - d->sent_node_off[s];
+      const int64_t spans = d->sent_span_off[s + 1] - d->sent_span_off[s];
+      if (n < 0 || spans != LT_MAX_SPAN * n + 1)
+        return note(bad[t], s, LT_EINVAL, "batch: sentence %lld has %lld span entries for %lld chars", s, spans, n);
+      if (nodes < 1 || nodes >= MAX_LOCAL_NODES)
+        return note(bad[t], s, LT_EINVAL, "batch: sentence %lld has %lld nodes%.0lld", s, nodes, 0);
+      const int32_t* ss = d->span_start + d->sent_span_off[s];
+      if (ss[0] != 1 || ss[spans - 1] != nodes)
+        return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span table does not cover its nodes%.0lld%.0lld", s, 0, 0);
+      for (int64_t e = 1; e <= n; ++e) {
+        const int64_t dmax = std::min<int64_t>(e, d->max_len);
+        for (int j = 0; j < LT_MAX_SPAN; ++j) {
+          const int64_t idx = (e - 1) * LT_MAX_SPAN + j;
+          const int32_t cnt = ss[idx + 1] - ss[idx];
+          const int dd = LT_MAX_SPAN - j;
+          if (cnt < 0)
+            return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span table not monotone%.0lld%.0lld", s, 0, 0);
+          if (dd <= dmax && cnt == 0)
+            return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span (e=%lld,d=%lld) has no candidate", s, e, dd);
+          if (dd > dmax && cnt != 0)
+            return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span (e=%lld,d=%lld) is out of range", s, e, dd);
+        }
       }
     }
-  }
-  for (int64_t i = 0; i < d->n_nodes; ++i) {
-    if (d->node_word[i] < 0 || d->node_morph0[i] < 0 || d->node_tag[i] < 0)
-      return fail(LT_EINVAL, "batch: node %lld has a negative id", (long long)i);
-    if (!std::isfinite(d->node_pre[i]) || !std::isfinite(d->node_f4[i]) ||
-        !std::isfinite(d->node_f5[i]) || !std::isfinite(d->node_f6[i]))
-      return fail(LT_EUNSUPPORTED, "batch: node %lld has a non-finite score term", (long long)i);
-  }
+  });
+  if (const Bad* x = first_bad(bad)) return fail(x->st, "%s", x->msg.c_str());
+  parallel_ranges(d->n_nodes, [&](int t, int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      if (d->node_word[i] < 0 || d->node_morph0[i] < 0 || d->node_tag[i] < 0)
+        return note(bad[t], i, LT_EINVAL, "batch: node %lld has a negative id%.0lld%.0lld", i, 0, 0);
+      if (!std::isfinite(d->node_pre[i]) || !std::isfinite(d->node_f4[i]) ||
+          !std::isfinite(d->node_f5[i]) || !std::isfinite(d->node_f6[i]))
+        return note(bad[t], i, LT_EUNSUPPORTED, "batch: node %lld has a non-finite score term%.0lld%.0lld", i, 0, 0);
+    }
+  });
+  if (const Bad* x = first_bad(bad)) return fail(x->st, "%s", x->msg.c_str());
   for (int64_t i = 0; i < (int64_t)d->n_post * d->n_nodes; ++i)
     if (!std::isfinite(d->node_post[i]))
       return fail(LT_EUNSUPPORTED, "batch: non-finite post term %lld", (long long)i);
@@ -549,28 +601,36 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   up(&b->d_cum_n, cum_n.data(), (size_t)S + 1);
   up(&b->d_span_start, d->span_start, (size_t)d->n_span);
   // device node records: AoS, mask + each node's span length d-1 (bits 24-26)
-  std::vector<NodeRec> recs((size_t)d->n_nodes);
-  for (int64_t i = 0; i < d->n_nodes; ++i) {
-    NodeRec& r = recs[(size_t)i];
-    r.word = (uint32_t)d->node_word[i];
-    r.morph = (uint32_t)d->node_morph0[i];
-    r.tag = (uint32_t)d->node_tag[i];
-    r.mask = d->node_mask[i] & ~(D_MASK | F_WI);
-    r.pre = d->node_pre[i];
-    r.f4 = d->node_f4[i];
-    r.f5 = d->node_f5[i];
-    r.f6 = d->node_f6[i];
+  std::unique_ptr<NodeRec[]> recs(new (std::nothrow) NodeRec[(size_t)std::max<int64_t>(d->n_nodes, 1)]);
+  if (!recs) {
+    batch_free(b);
+    return fail(LT_ENOMEM, "lt_batch_create: out of host memory");
   }
-  for (int32_t s = 0; s < S; ++s) {
-    const int32_t* ss = d->span_start + d->sent_span_off[s];
-    const int64_t base = d->sent_node_off[s];
-    for (int64_t x = 0; x < (int64_t)LT_MAX_SPAN * d->sent_n[s]; ++x) {
-      const uint32_t dd = (uint32_t)(LT_MAX_SPAN - (x % LT_MAX_SPAN));
-      for (int32_t v = ss[x]; v < ss[x + 1]; ++v) recs[(size_t)(base + v)].mask |= (dd - 1u) << D_SHIFT;
+  // sentence by sentence on threads: the records, then each node's span
+  // length d-1 (bits 24-26) from the span table
+  parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
+    for (int64_t s = lo; s < hi; ++s) {
+      const int64_t base = d->sent_node_off[s];
+      for (int64_t i = base; i < d->sent_node_off[s + 1]; ++i) {
+        NodeRec& r = recs[(size_t)i];
+        r.word = (uint32_t)d->node_word[i];
+        r.morph = (uint32_t)d->node_morph0[i];
+        r.tag = (uint32_t)d->node_tag[i];
+        r.mask = d->node_mask[i] & ~(D_MASK | F_WI);
+        r.pre = d->node_pre[i];
+        r.f4 = d->node_f4[i];
+        r.f5 = d->node_f5[i];
+        r.f6 = d->node_f6[i];
+      }
+      const int32_t* ss = d->span_start + d->sent_span_off[s];
+      for (int64_t x = 0; x < (int64_t)LT_MAX_SPAN * d->sent_n[s]; ++x) {
+        const uint32_t dd = (uint32_t)(LT_MAX_SPAN - (x % LT_MAX_SPAN));
+        for (int32_t v = ss[x]; v < ss[x + 1]; ++v) recs[(size_t)(base + v)].mask |= (dd - 1u) << D_SHIFT;
+      }
     }
-  }
-  up(&b->d_nodes, recs.data(), recs.size());
-  {
+  });
+  up(&b->d_nodes, recs.get(), (size_t)d->n_nodes);
+  if (hot_enabled()) {
     const uint32_t lim = 1u << NARROW_ID_BITS;
     b->f_word.assign(lim, 0u);
     b->f_tag.assign(lim, 0u);
@@ -627,11 +687,7 @@ static lt_status build_hot(lt_ctx* c, const lt_model* m, lt_batch* b) {
   if (!m->narrow) return LT_OK;
   // opt-in (LT_HOT=1) until it pays: it trades global probe traffic for LDS
   // reads and VALU, and the k=1 kernel is currently VALU/latency bound
-  static const bool enabled = [] {
-    const char* v = std::getenv("LT_HOT");
-    return v && v[0] == '1';
-  }();
-  if (!enabled) return LT_OK;
+  if (!hot_enabled() || b->f_word.empty()) return LT_OK;
   const double inv = b->n_nodes ? 1.0 / (double)b->n_nodes : 0.0;
   auto fw = [&](uint32_t x) { return b->f_word[x] * inv; };
   auto ft = [&](uint32_t x) { return b->f_tag[x] * inv; };
