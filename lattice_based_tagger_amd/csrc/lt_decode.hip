@@ -1229,7 +1229,7 @@ lt_beam_pk(DecodeParams p) {
   constexpr int STAGE = 64;                     // candidate records staged per position
   __shared__ Entry ring[WPB][RING][KT];
   __shared__ int32_t cntl[WPB][RING];
-  __shared__ uint4 stg[2][WPB][3 * 64];         // [position parity][wave]
+  __shared__ uint4 stg[WPB][3 * 64];            // records of the current position
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][LN];
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][LN];
   __shared__ unsigned long long tkey[WPB][KT];
@@ -1249,6 +1249,10 @@ lt_beam_pk(DecodeParams p) {
   const uint32_t nbase = (uint32_t)p.node_off[s];
   const int32_t* __restrict__ ssp = p.span_start + p.span_off[s];
   uint32_t* __restrict__ bp = p.bp + p.bp_off[s];
+  // the sentence's backpointers as a buffer: every position issues exactly one
+  // store instruction (non-writer lanes: out-of-range offset, dropped), so the
+  // wait at the top of the next position can leave that store in flight
+  const rsrc_t bpr = make_rsrc(bp, (uint64_t)(n + 1) * (uint64_t)p.bp_stride * 4u);
   const int k = p.k;
   const int bstride = p.bp_stride;
   const uint32_t slots = p.slots, seed = p.seed;
@@ -1268,15 +1272,36 @@ lt_beam_pk(DecodeParams p) {
     R[0][0] = e0;
     cnt9[0] = 1;
   }
-  int ss[MAX_SPAN + 1];
+  // The next position's first 64 records (lane t holds 16 B chunks t,
+  // 64 + t, 128 + t of the block: consecutive lanes read consecutive bytes)
+  // and span starts (lane j <= 8) are loaded into registers one position
+  // ahead and written to LDS at the top of the position: ordinary loads, so
+  // the compiler's waits count them exactly (an LDS-DMA in flight would make
+  // it drain every memory operation before each LDS access).
+  u32x4 pf[3];
+  int pfs = 0;
+  auto prefetch = [&](int e1, int first, bool valid) {
+    const uint32_t base = (nbase + (uint32_t)first) * (uint32_t)sizeof(NodeRec);
 #pragma unroll
-  for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = n >= 1 ? ssp[j] : 0;
-  dma_block<64>(B, nbase + (uint32_t)ss[0], n >= 1, stg[1][wv], lane);
+    for (int pl = 0; pl < 3; ++pl) pf[pl] = ld128(B.node, valid ? base + (uint32_t)(pl * 64 + lane) * 16u : OOB);
+    pfs = (valid && lane <= MAX_SPAN) ? ssp[(e1 - 1) * MAX_SPAN + lane] : 0;
+  };
+  int ss[MAX_SPAN + 1];
+  prefetch(1, n >= 1 ? ssp[0] : 0, n >= 1);
+  __builtin_amdgcn_raw_buffer_store_b32(0u, bpr, OOB, 0, 0);      // the invariant's first store
   __builtin_amdgcn_wave_barrier();
 
   for (int e = 1; e <= n; ++e) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): this position's records landed
-    const uint4* const cst = stg[e & 1][wv];
+    // vmcnt(1): the prefetched records and span starts landed (VMEM
+    // operations retire in order on gfx9; the one younger operation is the
+    // previous position's backpointer store)
+    __builtin_amdgcn_s_waitcnt(0x0F71);
+    uint4* const cst = stg[wv];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = __builtin_amdgcn_readlane(pfs, j);
+    __builtin_amdgcn_wave_barrier();
     const int dmax = min(e, p.max_len);
     const int em9 = e % RING;
     const int A0 = ss[0];
@@ -1289,10 +1314,6 @@ lt_beam_pk(DecodeParams p) {
       pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
     }
     const int M = pre[MAX_SPAN];
-    int ssn[MAX_SPAN + 1];
-    const int en = min(e + 1, n);
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = ssp[(en - 1) * MAX_SPAN + j];
 
     // expansion g -> span slot j (d = 8 - j), hypothesis rank r, candidate i
     auto decode = [&](int g, int& j, int& r, int& i) {
@@ -1312,7 +1333,6 @@ lt_beam_pk(DecodeParams p) {
     };
 
     int nrun = 0;
-    const int last0 = min(RPC, (M + 63) >> 6) - 1;   // DMA of e+1 after this round of chunk 0
     for (int base = 0; base < M; base += CH) {
       unsigned long long myk[RPC];
       uint32_t myg[RPC];
@@ -1343,14 +1363,6 @@ lt_beam_pk(DecodeParams p) {
         const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));
         Probe<NARROW> P;
         probe_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
-        if (base == 0 && t == last0) {
-          // next position's records, into the other parity buffer (an LDS
-          // read behind this DMA waits for it: issued after the reads of
-          // the scoring rounds of chunk 0)
-          __builtin_amdgcn_sched_barrier(0);
-          dma_block<64>(B, nbase + (uint32_t)ss[MAX_SPAN], e < n, stg[(e + 1) & 1][wv], lane);
-          __builtin_amdgcn_sched_barrier(0);
-        }
         asm volatile("" ::: "memory");
         const Hyp h1 = read_entry(R[hb][hr]);
         if (!skip) {
@@ -1455,37 +1467,46 @@ lt_beam_pk(DecodeParams p) {
       }
     }
 
-    // beam[e] = the running top-k (Sequence.add, beam.py:112-116)
+    // the next position's records and span starts: issued after this
+    // position's last load wait (VMEM operations retire in order, so any wait
+    // for a younger load would also wait for these)
+    prefetch(e + 1, ss[MAX_SPAN], e < n);
+
+    // beam[e] = the running top-k (Sequence.add, beam.py:112-116).  Winners
+    // among the staged records read them from LDS; a winner past the staged
+    // block (a position with more than STAGE candidates) takes a separate,
+    // uniform path with global loads, so the common path has no load to wait
+    // for (and does not wait for the prefetch above).
     Entry ne;
     uint32_t bpv = 0;
     const bool writer = lane < nrun;
-    if (writer) {
-      const unsigned long long key = LK[KTP - nrun + lane];
-      int j, r, i;
-      decode((int)LG[KTP - nrun + lane], j, r, i);
-      const int d = MAX_SPAN - j;
-      const int node = ss[j] + i;
-      const int so = node - A0;
-      const Cand c = so < STAGE ? read_block<64>(cst, 0, so) : load_cand(B, nbase + (uint32_t)node);
-      const Entry& h = R[(e - d) % RING][r];
-      ne.score = ord_score(key); ne.f6 = c.f6;
+    int wj = 0, wr = 0, wi = 0;
+    if (writer) decode((int)LG[KTP - nrun + lane], wj, wr, wi);
+    const int wnode = ss[wj] + wi;
+    const bool far = writer && wnode - A0 >= STAGE;
+    auto build = [&](const Cand& c) {
+      const int d = MAX_SPAN - wj;
+      const Entry& h = R[(e - d) % RING][wr];
+      ne.score = ord_score(LK[KTP - nrun + lane]); ne.f6 = c.f6;
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
       ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
       ne.depth = h.depth + 1;
-      bpv = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+      bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
+    };
+    if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
+      if (writer) build(read_block<64>(cst, 0, min(wnode - A0, STAGE - 1)));
+    } else if (writer) {
+      build(far ? load_cand(B, nbase + (uint32_t)wnode) : read_block<64>(cst, 0, min(wnode - A0, STAGE - 1)));
     }
     __builtin_amdgcn_wave_barrier();
-    if (writer) {
-      R[em9][lane] = ne;
-      bp[(int64_t)e * bstride + lane] = bpv;
-    }
+    if (writer) R[em9][lane] = ne;
+    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + lane) * 4u : OOB, 0, 0);
     if (lane == 0) cnt9[em9] = nrun;
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = ssn[j];
     __builtin_amdgcn_wave_barrier();
   }
 
   // matures = beam[n] + EOS (beam.py:59-61); backtrace per mature rank
+  __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): the backpointer stores are done
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const int nm = cnt9[n % RING];
   if (lane == 0) p.out_count[s] = nm;
@@ -1524,6 +1545,354 @@ hipError_t launch_bp(const DecodeParams& p, hipStream_t st) {
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((lt_beam_pk<KT, WPB, NARROW, COUNT>), dim3(blocks), dim3(64 * WPB), 0, st, p);
   return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// beam_size 2..8, BW_W sentences per wave.  With one sentence per wave a
+// position's expansions (about 27 at k = 5) leave most of the 64 lanes idle;
+// here the expansions of the wave's sentences at their common end position e
+// form one list (sentence order, generation order within, as lt_viterbi_pk
+// packs candidates) scored in rounds of 64 lanes.  Each sentence's entries go
+// to its own LDS list; top-k is the same exact rank counting as lt_beam_pk
+// (rank = entries with a larger key, or an equal key and a smaller
+// generation index), one lane per entry, the lanes of all sentences in the
+// same rounds.  A position with more than CHW expansions in a sentence is
+// taken in passes of CHW that carry the running top-k.
+// ---------------------------------------------------------------------------
+constexpr int BW_W = 2;                 // sentences per wave
+constexpr int BW_WPB = 4;               // waves per block
+
+// a[w] for a per-lane sentence index w (selects over uniform values)
+template <class T, int N>
+__device__ __forceinline__ T sel(const T (&a)[N], int w) {
+  T v = a[0];
+#pragma unroll
+  for (int u = 1; u < N; ++u)
+    if (w == u) v = a[u];
+  return v;
+}
+
+template <int KT, bool NARROW>
+__global__ void __launch_bounds__(64 * BW_WPB)
+lt_beam_pw(DecodeParams p) {
+  constexpr int W = BW_W, WPB = BW_WPB;
+  constexpr int KTP = KT < 4 ? 4 : KT;          // running-list room (multiple of 4)
+  constexpr int CHW = 128;                      // expansions per sentence per pass
+  constexpr int LN = KTP + CHW;
+  static_assert(W * KT <= 64, "one lane per (sentence, rank)");
+  __shared__ Entry ring[WPB][W][RING][KT];
+  __shared__ int32_t cntl[WPB][W][RING];
+  __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][W][LN];
+  __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][W][LN];
+  __shared__ unsigned long long tkey[WPB][W][KT];
+  __shared__ uint32_t tgen[WPB][W][KT];
+  constexpr bool USE_D3 = KT <= 8;              // dense class-3 table in LDS (3 blocks per CU still fit)
+  __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
+  Aux aux{nullptr, nullptr, 0u, p.hk};
+  if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
+
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = (int)(threadIdx.x & 63);
+  const int slot0 = (blockIdx.x * WPB + wv) * W;
+  if (slot0 >= p.n_sent) return;                // whole wave
+  const Bufs B = make_bufs(p);
+  const int k = p.k;
+  const int bstride = p.bp_stride;
+  const uint32_t slots = p.slots, seed = p.seed;
+  const int has_tri = p.has_tri;
+  Counts cnt;
+
+  // lane w < W owns sentence w of the wave
+  const bool own = lane < W && slot0 + lane < p.n_sent;
+  const int ol = lane < W ? lane : 0;           // owner index (in-bounds for every lane)
+  const int sid = own ? p.order[slot0 + lane] : 0;
+  const int nw = own ? p.sent_n[sid] : 0;
+  const uint32_t nbo = own ? (uint32_t)p.node_off[sid] : 0u;
+  const int32_t* const ssp = p.span_start + (own ? p.span_off[sid] : 0);
+  const int64_t bpo = own ? p.bp_off[sid] : 0;
+  int nS[W], sidS[W];
+  uint32_t nbS[W];
+  int64_t bpS[W];
+  int nmax = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    nS[w] = __builtin_amdgcn_readlane(nw, w);
+    sidS[w] = __builtin_amdgcn_readlane(sid, w);
+    nbS[w] = (uint32_t)__builtin_amdgcn_readlane((int)nbo, w);
+    bpS[w] = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(bpo >> 32), w) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bpo, w);
+    nmax = max(nmax, nS[w]);
+  }
+  if (own) {                                    // beam[0] = [BOS] (beam.py:21-23)
+    const Cand b0 = load_cand(B, nbo);
+    Entry e0;
+    e0.score = 0.0; e0.f6 = b0.f6;
+    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
+    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+    ring[wv][lane][0][0] = e0;
+    cntl[wv][lane][0] = 1;
+  }
+  // owner lanes: span starts of the current and the next position
+  int ssn[MAX_SPAN + 1];
+#pragma unroll
+  for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = (own && nw >= 1) ? ssp[j] : 0;
+  __builtin_amdgcn_wave_barrier();
+
+  for (int e = 1; e <= nmax; ++e) {
+    const int dmax = min(e, p.max_len);
+    const int em9 = e % RING;
+    // owner lanes: expansion prefix of the 8 span slots (beam.py:27-33):
+    // spans j (d = 8 - j) x hypotheses of beam[e - d] x candidates
+    int ss[MAX_SPAN + 1], pre[MAX_SPAN + 1];
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = ssn[j];
+    const bool live = own && e <= nw;
+    pre[0] = 0;
+#pragma unroll
+    for (int j = 0; j < MAX_SPAN; ++j) {
+      const int d = MAX_SPAN - j;
+      const int c = (live && d <= dmax) ? cntl[wv][ol][(e - d) % RING] : 0;
+      pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
+    }
+    const int en = min(e + 1, max(nw, 1));
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = (own && nw >= 1) ? ssp[(en - 1) * MAX_SPAN + j] : 0;
+    int ssS[W][MAX_SPAN + 1], preS[W][MAX_SPAN + 1], MS[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+#pragma unroll
+      for (int j = 0; j <= MAX_SPAN; ++j) {
+        ssS[w][j] = __builtin_amdgcn_readlane(ss[j], w);
+        preS[w][j] = __builtin_amdgcn_readlane(pre[j], w);
+      }
+      MS[w] = preS[w][MAX_SPAN];
+    }
+    // expansion g of sentence w -> span slot j (d = 8 - j), hypothesis rank
+    // r, candidate (local node) index; per-lane sentence selects
+    auto decode = [&](int w, int g, int& j, int& r, int& node) {
+      int pl[MAX_SPAN + 1], sl[MAX_SPAN + 1];
+#pragma unroll
+      for (int q = 0; q <= MAX_SPAN; ++q) {
+        pl[q] = preS[0][q];
+        sl[q] = ssS[0][q];
+#pragma unroll
+        for (int v = 1; v < W; ++v)
+          if (w == v) { pl[q] = preS[v][q]; sl[q] = ssS[v][q]; }
+      }
+      j = 0;
+#pragma unroll
+      for (int q = 1; q < MAX_SPAN; ++q) j += (g >= pl[q]) ? 1 : 0;
+      int pj = pl[0], m = sl[1] - sl[0], sj = sl[0];
+#pragma unroll
+      for (int q = 1; q < MAX_SPAN; ++q)
+        if (j == q) { pj = pl[q]; m = sl[q + 1] - sl[q]; sj = sl[q]; }
+      const int local = g - pj;
+      m = max(m, 1);
+      r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
+      int i = local - r * m;
+      if (i < 0) { --r; i += m; }
+      else if (i >= m) { ++r; i -= m; }
+      node = sj + i;
+    };
+
+    int nrun[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) nrun[w] = 0;
+    if (lane < W * KTP) {                       // empty running lists
+      lkey[wv][lane / KTP][lane % KTP] = 0ull;
+      lgen[wv][lane / KTP][lane % KTP] = INV;
+    }
+    int npass = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) npass = max(npass, (MS[w] + CHW - 1) / CHW);
+    for (int pass = 0; pass < npass; ++pass) {
+      int P[W], T = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        P[w] = min(max(MS[w] - pass * CHW, 0), CHW);
+        T += P[w];
+      }
+      // ---- scoring rounds: lane f of the list -> (sentence, entry x)
+      for (int f0 = 0; f0 < T; f0 += 64) {
+        const int f = f0 + lane;
+        int ms = W, x = 0, run = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          if (f >= run && f < run + P[w]) { ms = w; x = f - run; }
+          run += P[w];
+        }
+        const bool act = ms < W;
+        const int msr = act ? ms : 0;
+        const int g = pass * CHW + x;
+        int j = 0, r = 0, node = 0;
+        if (act) decode(msr, g, j, r, node);
+        const int d = MAX_SPAN - j;
+        const uint32_t gn = act ? sel(nbS, msr) + (uint32_t)node : INV;
+        const Cand c = load_cand(B, gn);
+        const int hb = act ? (e - d) % RING : 0;
+        const int hr = act ? r : 0;
+        const Hyp h0 = read_entry(ring[wv][msr][hb][hr]);
+        // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
+        const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));
+        Probe<NARROW> Pr;
+        probe_issue<NARROW>(Pr, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
+        asm volatile("" ::: "memory");
+        const Hyp h1 = read_entry(ring[wv][msr][hb][hr]);
+        unsigned long long key = 0ull;
+        if (!skip) {
+          const double tri = has_tri ? probe_finish<NARROW, false>(Pr, h1, c, cnt) : 0.0;
+          key = ord_key(h1.score + increment(p, c, tri, gn));    // beam.py:115
+        }
+        if (act) {
+          lkey[wv][msr][KTP + x] = key;
+          lgen[wv][msr][KTP + x] = (uint32_t)g;
+        }
+      }
+      // zero entries up to a multiple of 4 behind each sentence's pass entries
+      if (lane < 4 * W) {
+        const int w = lane >> 2, t = lane & 3;
+        const int Pw = sel(P, w);
+        const int at = Pw + t;
+        if (at < ((Pw + 3) & ~3)) { lkey[wv][w][KTP + at] = 0ull; lgen[wv][w][KTP + at] = INV; }
+      }
+      // ---- rank counting: the running entries [0, nrun) and the pass
+      // entries [KTP, KTP + P) of each sentence, one lane per entry
+      int Lt = 0, L4max = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        Lt += nrun[w] + P[w];
+        L4max = max(L4max, KTP + ((P[w] + 3) & ~3));
+      }
+      int valid[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) valid[w] = 0;
+      for (int f0 = 0; f0 < Lt; f0 += 64) {
+        const int f = f0 + lane;
+        int ms = W, y = 0, run = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const int Lw = nrun[w] + P[w];
+          if (f >= run && f < run + Lw) { ms = w; y = f - run; }
+          run += Lw;
+        }
+        const bool act = ms < W;
+        const int msr = act ? ms : 0;
+        const int nr = sel(nrun, msr);
+        const int idx = y < nr ? y : KTP + (y - nr);
+        const unsigned long long ck = act ? lkey[wv][msr][idx] : 0ull;
+        const uint32_t cg = act ? lgen[wv][msr][idx] : INV;
+        const int lim = act ? KTP + ((sel(P, msr) + 3) & ~3) : 0;
+        const unsigned long long* LK = lkey[wv][msr];
+        const uint32_t* LG = lgen[wv][msr];
+        int rank = 0;
+        for (int q = 0; q < L4max; q += 4) {
+          if (q < lim) {
+            const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
+            const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
+            const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
+            const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
+            const uint32_t gq[4] = {gg.x, gg.y, gg.z, gg.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) rank += (kq[u] > ck || (kq[u] == ck && gq[u] < cg)) ? 1 : 0;
+          }
+        }
+        const bool ok = act && ck != 0ull;
+        if (ok && rank < k) { tkey[wv][msr][rank] = ck; tgen[wv][msr][rank] = cg; }
+#pragma unroll
+        for (int w = 0; w < W; ++w) valid[w] += __builtin_popcountll(__ballot(ok && ms == w));
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) nrun[w] = min(k, valid[w]);
+      // the new running lists (zero padded to KTP), in order behind the writes above
+      if (lane < W * KTP) {
+        const int w = lane / KTP, t = lane % KTP;
+        const bool has = t < sel(nrun, w);
+        lkey[wv][w][t] = has ? tkey[wv][w][t] : 0ull;
+        lgen[wv][w][t] = has ? tgen[wv][w][t] : INV;
+      }
+    }
+
+    // beam[e] = the running top-k of each sentence (Sequence.add, beam.py:112-116)
+    const int wm = lane / KT, tm = lane % KT;
+    const int wmr = wm < W ? wm : 0;
+    const bool writer = wm < W && tm < sel(nrun, wmr) && e <= sel(nS, wmr);
+    Entry ne;
+    uint32_t bpv = 0;
+    if (writer) {
+      const unsigned long long key = lkey[wv][wmr][tm];
+      int j, r, node;
+      decode(wmr, (int)lgen[wv][wmr][tm], j, r, node);
+      const int d = MAX_SPAN - j;
+      const Cand c = load_cand(B, sel(nbS, wmr) + (uint32_t)node);
+      const Entry& h = ring[wv][wmr][(e - d) % RING][r];
+      ne.score = ord_score(key); ne.f6 = c.f6;
+      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
+      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
+      ne.depth = h.depth + 1;
+      bpv = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (writer) {
+      ring[wv][wmr][em9][tm] = ne;
+      p.bp[sel(bpS, wmr) + (int64_t)e * bstride + tm] = bpv;
+    }
+    if (lane < W && e <= sel(nS, lane)) cntl[wv][lane][em9] = sel(nrun, lane);
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // matures = beam[n] + EOS (beam.py:59-61); backtrace per (sentence, rank)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const int wm = lane / KT, tm = lane % KT;
+  if (wm < W && slot0 + wm < p.n_sent && tm < k) {
+    const int n = sel(nS, wm);
+    const int s = sel(sidS, wm);
+    const int nm = cntl[wv][wm][n % RING];
+    if (tm == 0) p.out_count[s] = nm;
+    const int64_t o = (int64_t)s * k + tm;
+    if (tm >= nm) {                             // unused mature slots read as empty
+      p.out_score[o] = 0.0;
+      p.out_len[o] = 0;
+    } else {
+      const Entry& f = ring[wv][wm][n % RING][tm];
+      p.out_score[o] = f.score + 0.0;
+      p.out_len[o] = (int32_t)f.depth;
+      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)tm * n;
+      const uint32_t* bpg = p.bp + sel(bpS, wm);
+      int pos = n, rank = tm;
+      for (int step = (int)f.depth - 1; step >= 0; --step) {
+        const uint32_t v = bpg[(int64_t)pos * bstride + rank];
+        codes[step] = (int32_t)bp_node(v);
+        pos -= (int)bp_d(v);
+        rank = (int)bp_rank(v);
+      }
+    }
+  }
+}
+
+template <int KT, bool NARROW>
+hipError_t launch_pw(const DecodeParams& p, hipStream_t st) {
+  constexpr int SPB = BW_W * BW_WPB;
+  const int blocks = (p.n_sent + SPB - 1) / SPB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((lt_beam_pw<KT, NARROW>), dim3(blocks), dim3(64 * BW_WPB), 0, st, p);
+  return hipGetLastError();
+}
+
+static bool beam_packed_all() {
+  static const bool v = [] {
+    const char* e = std::getenv("LT_BEAM");
+    return e && std::strcmp(e, "pw") == 0;
+  }();
+  return v;
+}
+
+// LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
+static bool beam_one_per_wave() {
+  static const bool v = [] {
+    const char* e = std::getenv("LT_BEAM");
+    return e && std::strcmp(e, "pk") == 0;
+  }();
+  return v;
 }
 
 static bool beam_v1() {
@@ -1623,6 +1992,16 @@ hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
 
 template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
+  // two sentences per wave pays where a position has few expansions (k = 2);
+  // LT_BEAM=pw selects it for k <= 8, LT_BEAM=pk never
+  if (!COUNT && !beam_v1() && !beam_one_per_wave() && (kt == 2 || (kt <= 8 && beam_packed_all()))) {
+    switch (kt) {
+      case 2: return launch_pw<2, NARROW>(p, st);
+      case 4: return launch_pw<4, NARROW>(p, st);
+      case 8: return launch_pw<8, NARROW>(p, st);
+      default: break;
+    }
+  }
   if (kt > 1 && !beam_v1()) {
     switch (kt) {
       case 2: return launch_bp<2, 4, NARROW, COUNT>(p, st);
@@ -1666,7 +2045,10 @@ hipError_t launch_evaluate(const EvalParams& p, hipStream_t st) {
 const char* kernel_name_for(int k) {
   const int kt = beam_template_for(k);
   if (kt < 0) return nullptr;
-  if (kt > 1) return beam_v1() ? "lt_beam_k" : "lt_beam_pk";
+  if (kt > 1) {
+    if (beam_v1()) return "lt_beam_k";
+    return (!beam_one_per_wave() && (kt == 2 || (kt <= 8 && beam_packed_all()))) ? "lt_beam_pw" : "lt_beam_pk";
+  }
   return viterbi_variant() == 0 ? "lt_viterbi_k" : "lt_viterbi_pk";
 }
 
