@@ -587,6 +587,12 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   }
   b->total_chars = cum_n[S];
   b->bp_entries = bp_off[S];
+  if (b->bp_entries * 4 >= ((int64_t)1 << 31)) {
+    const long long slots = (long long)b->bp_entries;
+    delete b;
+    return fail(LT_EUNSUPPORTED, "lt_batch_create: %lld backpointer slots exceed one launch (2^31 B); split the batch",
+                slots);
+  }
 
   hipStream_t stm = c->stream;
   hipError_t e = hipSuccess;
@@ -764,6 +770,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.nodes = b->d_nodes;
   p.npost = b->d_post;
   p.bp = b->d_bp;
+  p.bp_bytes = b->bp_entries * 4;
   p.bp_off = b->d_bp_off;
   p.cum_n = b->d_cum_n;
   p.out_count = b->d_count;

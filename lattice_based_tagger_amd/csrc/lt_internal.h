@@ -33,6 +33,7 @@ struct DecodeParams {
   const double* npost;
   // scratch + results
   uint32_t* bp;
+  int64_t bp_bytes;             // bytes of bp (< 2^31: 32-bit buffer offsets)
   const int64_t* bp_off;
   const int64_t* cum_n;         // sum_{s2<s} n_s2 (codes of s start at k*cum_n[s])
   int32_t* out_count;
