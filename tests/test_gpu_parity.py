@@ -85,7 +85,7 @@ def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
     assert (ex, tu) == (o_ex, o_tu)
 
 
-@pytest.mark.parametrize('k', [1, 5])
+@pytest.mark.parametrize('k', [1, 2, 5])
 def test_dense_lattices_with_ties_match_c_oracle(gpu_decoder, k):
     """Dense lattices (about 30 candidates per end position, half of the extra
     ones exact duplicates of the span's first candidate, hence score ties):
@@ -169,3 +169,19 @@ def test_decode_in_several_launches(gpu_decoder, monkeypatch):
     for a, b in zip(whole, pieces):
         assert [float(x.score).hex() for x in a] == [float(x.score).hex() for x in b]
         assert [[tuple(w) for w in x.sequences] for x in a] == [[tuple(w) for w in x.sequences] for x in b]
+
+
+def test_two_sentence_beam_kernel_multi_pass(gpu_decoder):
+    """k=2 runs lt_beam_pw (two sentences per wave).  Very dense lattices
+    (about 75 candidates per end position) give positions with more than one
+    128-expansion pass per sentence and several scoring / ranking rounds per
+    pass, with ties; results bit-exact against the C restatement."""
+    from lattice_based_tagger_amd import _capi as C
+    assert C.load().lt_kernel_name(2) == b'lt_beam_pw'
+    packed, keys, coefs = _synthetic(257, seed=411, n_features=100_000, eojeols=5,
+                                     extra_lambda=45.0, dup_rate=0.4)
+    (count, length, score, codes), _ = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, 2)
+    o = lt_oracle.decode(packed, keys, coefs, 2, nthreads=16)
+    assert np.array_equal(count, o[0]) and np.array_equal(length, o[1])
+    assert np.array_equal(score.view(np.uint64), o[2].view(np.uint64))
+    assert np.array_equal(codes, o[3])
