@@ -1547,53 +1547,50 @@ hipError_t launch_bp(const DecodeParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// beam_size 2..8, BW_W sentences per wave.  With one sentence per wave a
-// position's expansions (about 27 at k = 5) leave most of the 64 lanes idle;
-// here the expansions of the wave's sentences at their common end position e
-// form one list (sentence order, generation order within, as lt_viterbi_pk
-// packs candidates) scored in rounds of 64 lanes.  Each sentence's entries go
-// to its own LDS list; top-k is the same exact rank counting as lt_beam_pk
-// (rank = entries with a larger key, or an equal key and a smaller
-// generation index), one lane per entry, the lanes of all sentences in the
-// same rounds.  A position with more than CHW expansions in a sentence is
-// taken in passes of CHW that carry the running top-k.
-// ---------------------------------------------------------------------------
-constexpr int BW_W = 2;                 // sentences per wave
-constexpr int BW_WPB = 4;               // waves per block
-
-// a[w] for a per-lane sentence index w (selects over uniform values)
-template <class T, int N>
-__device__ __forceinline__ T sel(const T (&a)[N], int w) {
-  T v = a[0];
-#pragma unroll
-  for (int u = 1; u < N; ++u)
-    if (w == u) v = a[u];
+// LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
+static bool beam_one_per_wave() {
+  static const bool v = [] {
+    const char* e = std::getenv("LT_BEAM");
+    return e && std::strcmp(e, "pk") == 0;
+  }();
   return v;
 }
 
-template <int KT, bool NARROW>
-__global__ void __launch_bounds__(64 * BW_WPB)
-lt_beam_pw(DecodeParams p) {
-  constexpr int W = BW_W, WPB = BW_WPB;
-  constexpr int KTP = KT < 4 ? 4 : KT;          // running-list room (multiple of 4)
-  constexpr int CHW = 128;                      // expansions per sentence per pass
-  constexpr int LN = KTP + CHW;
-  static_assert(W * KT <= 64, "one lane per (sentence, rank)");
-  __shared__ Entry ring[WPB][W][RING][KT];
-  __shared__ int32_t cntl[WPB][W][RING];
-  __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][W][LN];
-  __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][W][LN];
-  __shared__ unsigned long long tkey[WPB][W][KT];
-  __shared__ uint32_t tgen[WPB][W][KT];
-  constexpr bool USE_D3 = KT <= 8;              // dense class-3 table in LDS (3 blocks per CU still fit)
+// ---------------------------------------------------------------------------
+// beam_size 2..8, half waves: lanes 0-31 decode one sentence and lanes 32-63
+// another, in lockstep over end positions.  lt_beam_pk leaves about half of a
+// wave's lanes idle at k = 5 (about 27 expansions per position) and is
+// issue-bound; here each half scores its own sentence's expansions in rounds
+// of 32 lanes, so one instruction stream serves two sentences.  Everything
+// per sentence (span starts, expansion prefix, counts) lives in VGPRs that
+// are uniform within a half; top-k is lt_beam_pk's exact rank counting and
+// threshold pruning, per half.
+// ---------------------------------------------------------------------------
+template <int KT, int WPB, bool NARROW>
+__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(3, 3)))
+lt_beam_hw(DecodeParams p) {
+  constexpr int RPC = 2;                        // scoring rounds (of 32) per chunk
+  constexpr int CH = 32 * RPC;                  // expansions per chunk per half
+  constexpr int KTP = KT < 4 ? 4 : KT;
+  constexpr int LN = KTP + CH;
+  constexpr int STAGE = 32;                     // records staged per half and position
+  static_assert(KT <= 32, "one writer lane per rank in a half");
+  __shared__ Entry ring[WPB][2][RING][KT];
+  __shared__ int32_t cntl[WPB][2][RING];
+  __shared__ uint4 stg[WPB][3 * 64];            // half h's record r: chunks 96h + 3r .. +2
+  __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][2][LN];
+  __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][2][LN];
+  __shared__ unsigned long long tkey[WPB][2][KT];
+  __shared__ uint32_t tgen[WPB][2][KT];
+  constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   Aux aux{nullptr, nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
-  const int slot0 = (blockIdx.x * WPB + wv) * W;
+  const int hf = lane >> 5, hl = lane & 31;
+  const int slot0 = (blockIdx.x * WPB + wv) * 2;
   if (slot0 >= p.n_sent) return;                // whole wave
   const Bufs B = make_bufs(p);
   const int k = p.k;
@@ -1601,192 +1598,211 @@ lt_beam_pw(DecodeParams p) {
   const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
   Counts cnt;
+  // this half's sentence (values uniform within the half)
+  const bool hv = slot0 + hf < p.n_sent;
+  const int s = hv ? p.order[slot0 + hf] : 0;
+  const int n = hv ? p.sent_n[s] : 0;
+  const uint32_t nbase = hv ? (uint32_t)p.node_off[s] : 0u;
+  const int32_t* const ssp = p.span_start + (hv ? p.span_off[s] : 0);
+  const int64_t bpo = hv ? p.bp_off[s] : 0;
+  const int nmax = max(__builtin_amdgcn_readlane(n, 0), __builtin_amdgcn_readlane(n, 32));
+  const uint32_t nb0 = (uint32_t)__builtin_amdgcn_readlane((int)nbase, 0);
+  const uint32_t nb1 = (uint32_t)__builtin_amdgcn_readlane((int)nbase, 32);
+  const rsrc_t bpr = make_rsrc(p.bp, (uint64_t)p.bp_bytes);
+  Entry (*const R)[KT] = ring[wv][hf];
+  int32_t* const cnt9 = cntl[wv][hf];
+  unsigned long long* const LK = lkey[wv][hf];
+  uint32_t* const LG = lgen[wv][hf];
+  unsigned long long* const TK = tkey[wv][hf];
+  uint32_t* const TG = tgen[wv][hf];
+  const unsigned long long hmask = hf ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+  auto hcount = [&](unsigned long long bal) { return __builtin_popcountll(bal & hmask); };
 
-  // lane w < W owns sentence w of the wave
-  const bool own = lane < W && slot0 + lane < p.n_sent;
-  const int ol = lane < W ? lane : 0;           // owner index (in-bounds for every lane)
-  const int sid = own ? p.order[slot0 + lane] : 0;
-  const int nw = own ? p.sent_n[sid] : 0;
-  const uint32_t nbo = own ? (uint32_t)p.node_off[sid] : 0u;
-  const int32_t* const ssp = p.span_start + (own ? p.span_off[sid] : 0);
-  const int64_t bpo = own ? p.bp_off[sid] : 0;
-  int nS[W], sidS[W];
-  uint32_t nbS[W];
-  int64_t bpS[W];
-  int nmax = 0;
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    nS[w] = __builtin_amdgcn_readlane(nw, w);
-    sidS[w] = __builtin_amdgcn_readlane(sid, w);
-    nbS[w] = (uint32_t)__builtin_amdgcn_readlane((int)nbo, w);
-    bpS[w] = ((int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(bpo >> 32), w) << 32) |
-             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bpo, w);
-    nmax = max(nmax, nS[w]);
-  }
-  if (own) {                                    // beam[0] = [BOS] (beam.py:21-23)
-    const Cand b0 = load_cand(B, nbo);
+  if (hv && hl == 0) {                          // beam[0] = [BOS] (beam.py:21-23)
+    const Cand b0 = load_cand(B, nbase);
     Entry e0;
     e0.score = 0.0; e0.f6 = b0.f6;
     e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
     e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
-    ring[wv][lane][0][0] = e0;
-    cntl[wv][lane][0] = 1;
+    R[0][0] = e0;
+    cnt9[0] = 1;
   }
-  // owner lanes: span starts of the current and the next position
-  int ssn[MAX_SPAN + 1];
+  // next position's first STAGE records of both halves (chunk c = 64 pl + lane
+  // of the wave's stream: half c / 96, chunk c % 96 of that half's block) and
+  // span starts (lane 32h + j <= 8: span start j of half h), one position
+  // ahead, issued after the position's last load wait (lt_beam_pk)
+  u32x4 pf[3];
+  int pfs = 0;
+  auto prefetch = [&](int e1, int first_own) {
+    const int f0 = __builtin_amdgcn_readlane(first_own, 0), f1 = __builtin_amdgcn_readlane(first_own, 32);
+    const bool ok0 = e1 <= __builtin_amdgcn_readlane(n, 0), ok1 = e1 <= __builtin_amdgcn_readlane(n, 32);
 #pragma unroll
-  for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = (own && nw >= 1) ? ssp[j] : 0;
+    for (int pl = 0; pl < 3; ++pl) {
+      const int c = 64 * pl + lane;
+      const bool h1 = c >= 96;
+      const int cc = h1 ? c - 96 : c;
+      const bool ok = h1 ? ok1 : ok0;
+      const uint32_t o = ok ? ((h1 ? nb1 + (uint32_t)f1 : nb0 + (uint32_t)f0) * (uint32_t)sizeof(NodeRec) +
+                               (uint32_t)cc * 16u) : OOB;
+      pf[pl] = ld128(B.node, o);
+    }
+    pfs = (e1 <= n && hl <= MAX_SPAN) ? ssp[(e1 - 1) * MAX_SPAN + hl] : 0;
+  };
+  prefetch(1, n >= 1 ? ssp[0] : 0);
+  __builtin_amdgcn_raw_buffer_store_b32(0u, bpr, OOB, 0, 0);
   __builtin_amdgcn_wave_barrier();
 
   for (int e = 1; e <= nmax; ++e) {
+    __builtin_amdgcn_s_waitcnt(0x0F71);         // vmcnt(1): the prefetch (older than the store)
+    uint4* const cst = stg[wv];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
+    int ss[MAX_SPAN + 1];
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) {
+      const int a = __builtin_amdgcn_readlane(pfs, j), b = __builtin_amdgcn_readlane(pfs, 32 + j);
+      ss[j] = hf ? b : a;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const bool live = e <= n;
     const int dmax = min(e, p.max_len);
     const int em9 = e % RING;
-    // owner lanes: expansion prefix of the 8 span slots (beam.py:27-33):
-    // spans j (d = 8 - j) x hypotheses of beam[e - d] x candidates
-    int ss[MAX_SPAN + 1], pre[MAX_SPAN + 1];
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = ssn[j];
-    const bool live = own && e <= nw;
+    const int A0 = ss[0];
+    int pre[MAX_SPAN + 1];
     pre[0] = 0;
 #pragma unroll
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
-      const int c = (live && d <= dmax) ? cntl[wv][ol][(e - d) % RING] : 0;
+      const int c = (live && d <= dmax) ? cnt9[(e - d) % RING] : 0;
       pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
     }
-    const int en = min(e + 1, max(nw, 1));
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = (own && nw >= 1) ? ssp[(en - 1) * MAX_SPAN + j] : 0;
-    int ssS[W][MAX_SPAN + 1], preS[W][MAX_SPAN + 1], MS[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-#pragma unroll
-      for (int j = 0; j <= MAX_SPAN; ++j) {
-        ssS[w][j] = __builtin_amdgcn_readlane(ss[j], w);
-        preS[w][j] = __builtin_amdgcn_readlane(pre[j], w);
-      }
-      MS[w] = preS[w][MAX_SPAN];
-    }
-    // expansion g of sentence w -> span slot j (d = 8 - j), hypothesis rank
-    // r, candidate (local node) index; per-lane sentence selects
-    auto decode = [&](int w, int g, int& j, int& r, int& node) {
-      int pl[MAX_SPAN + 1], sl[MAX_SPAN + 1];
-#pragma unroll
-      for (int q = 0; q <= MAX_SPAN; ++q) {
-        pl[q] = preS[0][q];
-        sl[q] = ssS[0][q];
-#pragma unroll
-        for (int v = 1; v < W; ++v)
-          if (w == v) { pl[q] = preS[v][q]; sl[q] = ssS[v][q]; }
-      }
+    const int M = pre[MAX_SPAN];                // this half's expansions
+    const int Mmax = max(__builtin_amdgcn_readlane(M, 0), __builtin_amdgcn_readlane(M, 32));
+
+    auto decode = [&](int g, int& j, int& r, int& i) {
       j = 0;
 #pragma unroll
-      for (int q = 1; q < MAX_SPAN; ++q) j += (g >= pl[q]) ? 1 : 0;
-      int pj = pl[0], m = sl[1] - sl[0], sj = sl[0];
+      for (int q = 1; q < MAX_SPAN; ++q) j += (g >= pre[q]) ? 1 : 0;
+      int pj = pre[0], m = ss[1] - ss[0];
 #pragma unroll
       for (int q = 1; q < MAX_SPAN; ++q)
-        if (j == q) { pj = pl[q]; m = sl[q + 1] - sl[q]; sj = sl[q]; }
+        if (j == q) { pj = pre[q]; m = ss[q + 1] - ss[q]; }
       const int local = g - pj;
-      m = max(m, 1);
       r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
-      int i = local - r * m;
+      i = local - r * m;
       if (i < 0) { --r; i += m; }
       else if (i >= m) { ++r; i -= m; }
-      node = sj + i;
     };
 
-    int nrun[W];
+    int nrun = 0;                               // this half's running top-k size
+    for (int base = 0; base < Mmax; base += CH) {
+      unsigned long long myk[RPC];
+      uint32_t myg[RPC];
 #pragma unroll
-    for (int w = 0; w < W; ++w) nrun[w] = 0;
-    if (lane < W * KTP) {                       // empty running lists
-      lkey[wv][lane / KTP][lane % KTP] = 0ull;
-      lgen[wv][lane / KTP][lane % KTP] = INV;
-    }
-    int npass = 0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) npass = max(npass, (MS[w] + CHW - 1) / CHW);
-    for (int pass = 0; pass < npass; ++pass) {
-      int P[W], T = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        P[w] = min(max(MS[w] - pass * CHW, 0), CHW);
-        T += P[w];
-      }
-      // ---- scoring rounds: lane f of the list -> (sentence, entry x)
-      for (int f0 = 0; f0 < T; f0 += 64) {
-        const int f = f0 + lane;
-        int ms = W, x = 0, run = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          if (f >= run && f < run + P[w]) { ms = w; x = f - run; }
-          run += P[w];
-        }
-        const bool act = ms < W;
-        const int msr = act ? ms : 0;
-        const int g = pass * CHW + x;
-        int j = 0, r = 0, node = 0;
-        if (act) decode(msr, g, j, r, node);
+      for (int t = 0; t < RPC; ++t) {
+        myk[t] = 0ull;
+        myg[t] = INV;
+        if (base + 32 * t >= Mmax) continue;     // uniform
+        const int g = base + 32 * t + hl;
+        const bool act = g < M;
+        int j = 0, r = 0, i = 0;
+        if (act) decode(g, j, r, i);
         const int d = MAX_SPAN - j;
-        const uint32_t gn = act ? sel(nbS, msr) + (uint32_t)node : INV;
-        const Cand c = load_cand(B, gn);
+        const int node = ss[j] + i;
+        const int so = node - A0;
+        Cand c;
+        if (!act) {
+          c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
+        } else if (so < STAGE) {
+          const uint4* q = cst + 96 * hf + 3 * so;
+          const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
+          c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
+          c.pre = dbl(q1.x, q1.y); c.f4 = dbl(q1.z, q1.w);
+          c.f5 = dbl(q2.x, q2.y); c.f6 = dbl(q2.z, q2.w);
+        } else {
+          c = load_cand(B, nbase + (uint32_t)node);
+        }
         const int hb = act ? (e - d) % RING : 0;
         const int hr = act ? r : 0;
-        const Hyp h0 = read_entry(ring[wv][msr][hb][hr]);
-        // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
-        const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));
-        Probe<NARROW> Pr;
-        probe_issue<NARROW>(Pr, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
+        const Hyp h0 = read_entry(R[hb][hr]);
+        const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
+        Probe<NARROW> P;
+        probe_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
         asm volatile("" ::: "memory");
-        const Hyp h1 = read_entry(ring[wv][msr][hb][hr]);
-        unsigned long long key = 0ull;
+        const Hyp h1 = read_entry(R[hb][hr]);
         if (!skip) {
-          const double tri = has_tri ? probe_finish<NARROW, false>(Pr, h1, c, cnt) : 0.0;
-          key = ord_key(h1.score + increment(p, c, tri, gn));    // beam.py:115
+          const double tri = has_tri ? probe_finish<NARROW, false>(P, h1, c, cnt) : 0.0;
+          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
+          myk[t] = ord_key(sc);
+          myg[t] = (uint32_t)g;
         }
-        if (act) {
-          lkey[wv][msr][KTP + x] = key;
-          lgen[wv][msr][KTP + x] = (uint32_t)g;
-        }
+        LK[KTP + 32 * t + hl] = myk[t];
+        LG[KTP + 32 * t + hl] = myg[t];
       }
-      // zero entries up to a multiple of 4 behind each sentence's pass entries
-      if (lane < 4 * W) {
-        const int w = lane >> 2, t = lane & 3;
-        const int Pw = sel(P, w);
-        const int at = Pw + t;
-        if (at < ((Pw + 3) & ~3)) { lkey[wv][w][KTP + at] = 0ull; lgen[wv][w][KTP + at] = INV; }
-      }
-      // ---- rank counting: the running entries [0, nrun) and the pass
-      // entries [KTP, KTP + P) of each sentence, one lane per entry
-      int Lt = 0, L4max = 0;
+      // top-k of this half's chunk entries and its running top-k
+      const int R0 = max(0, min(RPC, (M - base + 31) >> 5));        // this half's rounds
+      const unsigned long long rk = hl < nrun ? LK[KTP - nrun + hl] : 0ull;
+      const uint32_t rg = hl < nrun ? LG[KTP - nrun + hl] : INV;
+      int valid = nrun;
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        Lt += nrun[w] + P[w];
-        L4max = max(L4max, KTP + ((P[w] + 3) & ~3));
-      }
-      int valid[W];
-#pragma unroll
-      for (int w = 0; w < W; ++w) valid[w] = 0;
-      for (int f0 = 0; f0 < Lt; f0 += 64) {
-        const int f = f0 + lane;
-        int ms = W, y = 0, run = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          const int Lw = nrun[w] + P[w];
-          if (f >= run && f < run + Lw) { ms = w; y = f - run; }
-          run += Lw;
-        }
-        const bool act = ms < W;
-        const int msr = act ? ms : 0;
-        const int nr = sel(nrun, msr);
-        const int idx = y < nr ? y : KTP + (y - nr);
-        const unsigned long long ck = act ? lkey[wv][msr][idx] : 0ull;
-        const uint32_t cg = act ? lgen[wv][msr][idx] : INV;
-        const int lim = act ? KTP + ((sel(P, msr) + 3) & ~3) : 0;
-        const unsigned long long* LK = lkey[wv][msr];
-        const uint32_t* LG = lgen[wv][msr];
+      for (int t = 0; t < RPC; ++t) valid += hcount(__ballot(myk[t] != 0ull));
+      const bool single = R0 <= 1 && nrun == 0;
+      if (__builtin_amdgcn_ballot_w64(!single) == 0ull) {
+        // one entry per lane in both halves: rank against the half's 32 list
+        // slots of round 0 (slots past M hold 0 keys)
+        const int qe = KTP + ((min(32, max(M - base, 0)) + 3) & ~3);
+        const int qmax = max(__builtin_amdgcn_readlane(qe, 0), __builtin_amdgcn_readlane(qe, 32));
         int rank = 0;
-        for (int q = 0; q < L4max; q += 4) {
-          if (q < lim) {
+#pragma unroll 2
+        for (int q = KTP; q < qmax; q += 4) {
+          const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
+          const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
+          const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
+          const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
+          const uint32_t gq[4] = {gg.x, gg.y, gg.z, gg.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) rank += (kq[u] > myk[0] || (kq[u] == myk[0] && gq[u] < myg[0])) ? 1 : 0;
+        }
+        if (myk[0] != 0ull && rank < k) { TK[rank] = myk[0]; TG[rank] = myg[0]; }
+      } else {
+        // threshold pruning (lt_beam_pk), per half: tau = the k-th largest of
+        // the half's lane maxima
+        unsigned long long mx = rk;
+#pragma unroll
+        for (int t = 0; t < RPC; ++t) mx = myk[t] > mx ? myk[t] : mx;
+        unsigned long long* const MX = LK + KTP;                 // chunk entries are in registers now
+        MX[hl] = mx;
+        if (hl == 0) TK[0] = ~0ull;
+        int gtc = 0;
+#pragma unroll 4
+        for (int q = 0; q < 32; q += 2) {
+          const ulonglong2 m2 = *reinterpret_cast<const ulonglong2*>(&MX[q]);
+          gtc += (m2.x > mx ? 1 : 0) + (m2.y > mx ? 1 : 0);
+        }
+        const int nz = hcount(__ballot(mx != 0ull));
+        if (mx != 0ull && gtc < k)
+          __hip_atomic_fetch_min(&TK[0], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned long long tau = nz >= k ? TK[0] : 1ull;
+        int nc = 0;
+        auto push = [&](unsigned long long key, uint32_t g) {
+          const bool c = key >= tau && key != 0ull;
+          const uint32_t bh = (uint32_t)((__ballot(c) & hmask) >> (32 * hf));
+          const int at = nc + __builtin_popcount(bh & ((1u << hl) - 1u));
+          if (c) { LK[at] = key; LG[at] = g; }
+          nc += __builtin_popcount(bh);
+        };
+        push(rk, rg);
+#pragma unroll
+        for (int t = 0; t < RPC; ++t) push(myk[t], myg[t]);
+        const int nc4 = (nc + 3) & ~3;
+        if (hl < nc4 - nc) { LK[nc + hl] = 0ull; LG[nc + hl] = INV; }
+        const int ncmax = max(__builtin_amdgcn_readlane(nc, 0), __builtin_amdgcn_readlane(nc, 32));
+        for (int c0 = 0; c0 < ncmax; c0 += 32) {
+          const int c = c0 + hl;
+          const unsigned long long ck = c < nc ? LK[c] : 0ull;
+          const uint32_t cg = c < nc ? LG[c] : INV;
+          int rank = 0;
+          for (int q = 0; q < nc4; q += 4) {
             const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
             const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
             const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
@@ -1795,70 +1811,76 @@ lt_beam_pw(DecodeParams p) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) rank += (kq[u] > ck || (kq[u] == ck && gq[u] < cg)) ? 1 : 0;
           }
+          if (c < nc && rank < k) { TK[rank] = ck; TG[rank] = cg; }
         }
-        const bool ok = act && ck != 0ull;
-        if (ok && rank < k) { tkey[wv][msr][rank] = ck; tgen[wv][msr][rank] = cg; }
-#pragma unroll
-        for (int w = 0; w < W; ++w) valid[w] += __builtin_popcountll(__ballot(ok && ms == w));
       }
-#pragma unroll
-      for (int w = 0; w < W; ++w) nrun[w] = min(k, valid[w]);
-      // the new running lists (zero padded to KTP), in order behind the writes above
-      if (lane < W * KTP) {
-        const int w = lane / KTP, t = lane % KTP;
-        const bool has = t < sel(nrun, w);
-        lkey[wv][w][t] = has ? tkey[wv][w][t] : 0ull;
-        lgen[wv][w][t] = has ? tgen[wv][w][t] : INV;
+      nrun = min(k, valid);
+      const int nrp2 = (nrun + 3) & ~3;
+      if (hl < nrp2) {
+        const int dst = KTP - nrp2 + hl, src = hl - (nrp2 - nrun);
+        LK[dst] = src >= 0 ? TK[src] : 0ull;
+        LG[dst] = src >= 0 ? TG[src] : INV;
       }
     }
 
-    // beam[e] = the running top-k of each sentence (Sequence.add, beam.py:112-116)
-    const int wm = lane / KT, tm = lane % KT;
-    const int wmr = wm < W ? wm : 0;
-    const bool writer = wm < W && tm < sel(nrun, wmr) && e <= sel(nS, wmr);
+    prefetch(e + 1, ss[MAX_SPAN]);              // after the position's last load wait
+
+    // beam[e] of each half (Sequence.add, beam.py:112-116)
     Entry ne;
     uint32_t bpv = 0;
-    if (writer) {
-      const unsigned long long key = lkey[wv][wmr][tm];
-      int j, r, node;
-      decode(wmr, (int)lgen[wv][wmr][tm], j, r, node);
-      const int d = MAX_SPAN - j;
-      const Cand c = load_cand(B, sel(nbS, wmr) + (uint32_t)node);
-      const Entry& h = ring[wv][wmr][(e - d) % RING][r];
-      ne.score = ord_score(key); ne.f6 = c.f6;
+    const bool writer = live && hl < nrun;
+    int wj = 0, wr = 0, wi = 0;
+    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi);
+    const int wnode = ss[wj] + wi;
+    const bool far = writer && wnode - A0 >= STAGE;
+    auto build = [&](const Cand& c) {
+      const int d = MAX_SPAN - wj;
+      const Entry& h = R[(e - d) % RING][wr];
+      ne.score = ord_score(LK[KTP - nrun + hl]); ne.f6 = c.f6;
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
       ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
       ne.depth = h.depth + 1;
-      bpv = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+      bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
+    };
+    auto staged = [&](int r) {
+      const uint4* q = cst + 96 * hf + 3 * r;
+      const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
+      Cand c;
+      c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
+      c.pre = dbl(q1.x, q1.y); c.f4 = dbl(q1.z, q1.w);
+      c.f5 = dbl(q2.x, q2.y); c.f6 = dbl(q2.z, q2.w);
+      return c;
+    };
+    if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
+      if (writer) build(staged(min(wnode - A0, STAGE - 1)));
+    } else if (writer) {
+      build(far ? load_cand(B, nbase + (uint32_t)wnode) : staged(min(wnode - A0, STAGE - 1)));
     }
     __builtin_amdgcn_wave_barrier();
-    if (writer) {
-      ring[wv][wmr][em9][tm] = ne;
-      p.bp[sel(bpS, wmr) + (int64_t)e * bstride + tm] = bpv;
-    }
-    if (lane < W && e <= sel(nS, lane)) cntl[wv][lane][em9] = sel(nrun, lane);
+    if (writer) R[em9][hl] = ne;
+    __builtin_amdgcn_raw_buffer_store_b32(
+        bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, 0);
+    if (live && hl == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
   }
 
-  // matures = beam[n] + EOS (beam.py:59-61); backtrace per (sentence, rank)
+  // matures = beam[n] + EOS (beam.py:59-61); backtrace per (half, rank)
+  __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): the backpointer stores are done
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const int wm = lane / KT, tm = lane % KT;
-  if (wm < W && slot0 + wm < p.n_sent && tm < k) {
-    const int n = sel(nS, wm);
-    const int s = sel(sidS, wm);
-    const int nm = cntl[wv][wm][n % RING];
-    if (tm == 0) p.out_count[s] = nm;
-    const int64_t o = (int64_t)s * k + tm;
-    if (tm >= nm) {                             // unused mature slots read as empty
+  if (hv && hl < k) {
+    const int nm = cnt9[n % RING];
+    if (hl == 0) p.out_count[s] = nm;
+    const int64_t o = (int64_t)s * k + hl;
+    if (hl >= nm) {
       p.out_score[o] = 0.0;
       p.out_len[o] = 0;
     } else {
-      const Entry& f = ring[wv][wm][n % RING][tm];
+      const Entry& f = R[n % RING][hl];
       p.out_score[o] = f.score + 0.0;
       p.out_len[o] = (int32_t)f.depth;
-      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)tm * n;
-      const uint32_t* bpg = p.bp + sel(bpS, wm);
-      int pos = n, rank = tm;
+      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
+      const uint32_t* bpg = p.bp + bpo;
+      int pos = n, rank = hl;
       for (int step = (int)f.depth - 1; step >= 0; --step) {
         const uint32_t v = bpg[(int64_t)pos * bstride + rank];
         codes[step] = (int32_t)bp_node(v);
@@ -1869,31 +1891,14 @@ lt_beam_pw(DecodeParams p) {
   }
 }
 
-template <int KT, bool NARROW>
-hipError_t launch_pw(const DecodeParams& p, hipStream_t st) {
-  constexpr int SPB = BW_W * BW_WPB;
-  const int blocks = (p.n_sent + SPB - 1) / SPB;
+template <int KT, int WPB, bool NARROW>
+hipError_t launch_hw(const DecodeParams& p, hipStream_t st) {
+  const int blocks = (p.n_sent + 2 * WPB - 1) / (2 * WPB);
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_beam_pw<KT, NARROW>), dim3(blocks), dim3(64 * BW_WPB), 0, st, p);
+  hipLaunchKernelGGL((lt_beam_hw<KT, WPB, NARROW>), dim3(blocks), dim3(64 * WPB), 0, st, p);
   return hipGetLastError();
 }
 
-static bool beam_packed_all() {
-  static const bool v = [] {
-    const char* e = std::getenv("LT_BEAM");
-    return e && std::strcmp(e, "pw") == 0;
-  }();
-  return v;
-}
-
-// LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
-static bool beam_one_per_wave() {
-  static const bool v = [] {
-    const char* e = std::getenv("LT_BEAM");
-    return e && std::strcmp(e, "pk") == 0;
-  }();
-  return v;
-}
 
 static bool beam_v1() {
   static const bool v = [] {
@@ -1992,13 +1997,13 @@ hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
 
 template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
-  // two sentences per wave pays where a position has few expansions (k = 2);
-  // LT_BEAM=pw selects it for k <= 8, LT_BEAM=pk never
-  if (!COUNT && !beam_v1() && !beam_one_per_wave() && (kt == 2 || (kt <= 8 && beam_packed_all()))) {
+  // half waves (two sentences per wave, 32 lanes each) for k = 2..8;
+  // LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
+  if (!COUNT && !beam_v1() && !beam_one_per_wave() && kt <= 8) {
     switch (kt) {
-      case 2: return launch_pw<2, NARROW>(p, st);
-      case 4: return launch_pw<4, NARROW>(p, st);
-      case 8: return launch_pw<8, NARROW>(p, st);
+      case 2: return launch_hw<2, 4, NARROW>(p, st);
+      case 4: return launch_hw<4, 4, NARROW>(p, st);
+      case 8: return launch_hw<8, 4, NARROW>(p, st);
       default: break;
     }
   }
@@ -2047,7 +2052,8 @@ const char* kernel_name_for(int k) {
   if (kt < 0) return nullptr;
   if (kt > 1) {
     if (beam_v1()) return "lt_beam_k";
-    return (!beam_one_per_wave() && (kt == 2 || (kt <= 8 && beam_packed_all()))) ? "lt_beam_pw" : "lt_beam_pk";
+    if (beam_one_per_wave()) return "lt_beam_pk";
+    return kt <= 8 ? "lt_beam_hw" : "lt_beam_pk";
   }
   return viterbi_variant() == 0 ? "lt_viterbi_k" : "lt_viterbi_pk";
 }

@@ -56,8 +56,9 @@ def test_kernel_name_without_gpu():
     """Host-only query: the kernel each beam width launches (profiling names)."""
     lib = _capi.load()
     assert lib.lt_kernel_name(1) == b'lt_viterbi_pk'
-    assert lib.lt_kernel_name(2) == b'lt_beam_pw'
-    assert lib.lt_kernel_name(5) == b'lt_beam_pk'
+    assert lib.lt_kernel_name(2) == b'lt_beam_hw'
+    assert lib.lt_kernel_name(5) == b'lt_beam_hw'
+    assert lib.lt_kernel_name(16) == b'lt_beam_pk'
     assert lib.lt_kernel_name(32) == b'lt_beam_pk'
     assert lib.lt_kernel_name(33) is None
     assert lib.lt_kernel_name(0) is None or lib.lt_kernel_name(0) == b'lt_viterbi_pk'

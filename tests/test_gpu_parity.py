@@ -72,7 +72,7 @@ def _gpu_decode(ctx, packed, keys, coefs, k):
         dm.close()
 
 
-@pytest.mark.parametrize('k,n_sent', [(1, 65536), (5, 8192), (16, 4096), (2, 2048), (32, 512)])
+@pytest.mark.parametrize('k,n_sent', [(1, 65536), (5, 8192), (16, 4096), (2, 2048), (3, 2048), (8, 2048), (32, 512)])
 def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
     packed, keys, coefs = _synthetic(n_sent, seed=100 + k, n_features=1_000_000)
     (count, length, score, codes), (ex, tu, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
@@ -171,13 +171,14 @@ def test_decode_in_several_launches(gpu_decoder, monkeypatch):
         assert [[tuple(w) for w in x.sequences] for x in a] == [[tuple(w) for w in x.sequences] for x in b]
 
 
-def test_two_sentence_beam_kernel_multi_pass(gpu_decoder):
-    """k=2 runs lt_beam_pw (two sentences per wave).  Very dense lattices
-    (about 75 candidates per end position) give positions with more than one
-    128-expansion pass per sentence and several scoring / ranking rounds per
-    pass, with ties; results bit-exact against the C restatement."""
+def test_half_wave_beam_kernel_multi_chunk(gpu_decoder):
+    """k=2 runs lt_beam_hw (two sentences per wave, 32 lanes each).  Very
+    dense lattices (about 64 candidates per end position) give positions with
+    several 64-expansion chunks per half, so the threshold-pruning path and
+    the carried running top-k run in both halves at once, with ties; results
+    bit-exact against the C restatement."""
     from lattice_based_tagger_amd import _capi as C
-    assert C.load().lt_kernel_name(2) == b'lt_beam_pw'
+    assert C.load().lt_kernel_name(2) == b'lt_beam_hw'
     packed, keys, coefs = _synthetic(257, seed=411, n_features=100_000, eojeols=5,
                                      extra_lambda=45.0, dup_rate=0.4)
     (count, length, score, codes), _ = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, 2)
