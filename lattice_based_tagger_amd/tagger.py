@@ -178,10 +178,16 @@ class Tagger:
             raise NotImplementedError('debug=True is not available from the device decoder')
         return self.tag_batch([sent], beam_size=beam_size)[0]
 
+    # sentences per pipeline chunk of tag_batch
+    CHUNK = 8192
+
     def tag_batch(self, sents, beam_size=5):
-        """Best ``Sequence`` per sentence, decoded in one device launch.
-        Raises IndexError like ``tag`` when a non-empty sentence has no
-        dictionary node at all (`beam.py:32`)."""
+        """Best ``Sequence`` per sentence.  Raises IndexError like ``tag``
+        when a non-empty sentence has no dictionary node at all
+        (`beam.py:32`).  With native lattices the batch runs as a two-stage
+        pipeline over chunks of CHUNK sentences: a worker thread builds and
+        packs chunk i+1 (C++, outside the GIL) while this thread uploads,
+        decodes and re-materialises chunk i."""
         sents = list(sents)
         lex = self.native_lexicon()
         if lex is None:
@@ -189,19 +195,43 @@ class Tagger:
             matures = beam_search_batch(lattices, self.score_funcs, beam_size=beam_size,
                                         device=self.device)
             return [m[0] for m in matures]
+        from concurrent.futures import ThreadPoolExecutor
         from .beam import _check_beam, decode_batch, lowered_model
         from .native_packer import packer_for
         k = _check_beam(beam_size)
-        lat = lex.lookup(sents, n_threads=self.lookup_threads)
-        for s in range(len(sents)):
-            if lat.empty(s):
-                raise IndexError('list index out of range')            # beam.py:32 on bindex == []
+        chunks = [sents[i:i + self.CHUNK] for i in range(0, len(sents), self.CHUNK)] or [[]]
+
+        def lookup(chunk):
+            lat = lex.lookup(chunk, n_threads=self.lookup_threads)
+            for s in range(len(chunk)):
+                if lat.empty(s):
+                    raise IndexError('list index out of range')        # beam.py:32 on bindex == []
+            return lat
+
+        lat0 = lookup(chunks[0])                   # (the reference raises before scoring)
         model = lowered_model(self.score_funcs)
         npk = packer_for(model)
-        if npk is None:
-            lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(sents))]
-            matures = beam_search_batch(lattices, self.score_funcs, beam_size=k, device=self.device)
-        else:
+
+        def front(chunk, lat=None):
+            lat = lat if lat is not None else lookup(chunk)
+            if npk is None:
+                return lat, None, None
             packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
-            matures = decode_batch(packed, views, lat.chars, model, k, self.device, best_only=True)
-        return [m[0] for m in matures]
+            return lat, packed, views
+
+        out = []
+        with ThreadPoolExecutor(max_workers=1) as pool:
+            fut = pool.submit(front, chunks[0], lat0)
+            for i in range(len(chunks)):
+                lat, packed, views = fut.result()
+                if i + 1 < len(chunks):
+                    fut = pool.submit(front, chunks[i + 1])
+                if packed is None:
+                    lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(chunks[i]))]
+                    matures = beam_search_batch(lattices, self.score_funcs, beam_size=k,
+                                                device=self.device)
+                else:
+                    matures = decode_batch(packed, views, lat.chars, model, k, self.device,
+                                           best_only=True)
+                out += [m[0] for m in matures]
+        return out

@@ -15,8 +15,10 @@ from test_lookup import _fixture, fixture_dictionary, fixture_lexicon
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('name', ['base', 'demo'])
-def test_tagger_native_lattices_match_reference(gpu_decoder, name):
+@pytest.mark.parametrize('name,chunk', [('base', None), ('demo', None), ('base', 16)])
+def test_tagger_native_lattices_match_reference(gpu_decoder, name, chunk, monkeypatch):
+    if chunk:                                   # several pipeline chunks (lookup/pack overlapped)
+        monkeypatch.setattr(Tagger, 'CHUNK', chunk)
     entry = _fixture()[name]
     cases = load(name)
     by_chars = {c.chars: c for c in cases}

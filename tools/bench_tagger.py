@@ -36,6 +36,7 @@ def main():
     ap.add_argument('--k', type=int, default=1)
     ap.add_argument('--threads', type=int, default=0)
     ap.add_argument('--reps', type=int, default=3)
+    ap.add_argument('--chunk', type=int, default=0, help='Tagger.tag_batch pipeline chunk (0: default)')
     a = ap.parse_args()
     entry = _fixture()['base']
     funcs = load('base')[0].funcs
@@ -44,6 +45,8 @@ def main():
     lex = fixture_lexicon(entry)
     tagger = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=lex, score_funcs=funcs)
     tagger.tag_batch(sents[:256], beam_size=a.k)                   # warm: model lowering, device model
+    if a.chunk:
+        Tagger.CHUNK = a.chunk
     model = lowered_model(funcs)
     npk = packer_for(model)
     best = {}
