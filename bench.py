@@ -156,6 +156,46 @@ def cpu_baseline(raw, sm, budget_s):
                       % (done, float(raw.sent_n[:done].mean()), dt)}
 
 
+_POOL = {}
+
+
+def _pool_worker(args):
+    """One process of cpu_baseline_pool: render and decode sentences lo..hi
+    step `step` with the pure-Python restatement; returns (count, decode s)."""
+    lo, hi, step = args
+    from oracle import ref_beam
+    raw, funcs = _POOL['raw'], _POOL['funcs']
+    idx = list(range(lo, hi, step))
+    sents = synth.render_sentences(raw, idx)
+    t0 = time.perf_counter()
+    for bindex, chars in sents:
+        ref_beam.beam_search(bindex, chars, funcs, beam_size=1)
+    return len(idx), time.perf_counter() - t0
+
+
+def cpu_baseline_pool(raw, sm, procs, budget_s):
+    """The pure-Python restatement (as cpu_baseline) on `procs` host cores at
+    once: multiprocessing (fork, before this process touches the GPU), each
+    worker a strided share of the batch prefix; rate = sentences / the
+    slowest worker's decode time."""
+    import multiprocessing as mp
+    from lattice_based_tagger_amd import score_funcs as SF, feature as FE
+    dic, coef = synth.render_model(raw, sm)
+    _POOL['raw'] = raw
+    _POOL['funcs'] = SF.BeamScoreFunctions(SF.RegularizationScore(),
+                                           SF.SimpleTrigramFeatureScore(FE.SimpleTrigramEncoder(dic), coef))
+    n = int(min(raw.S, 500 * procs * budget_s))
+    with mp.get_context('fork').Pool(procs) as pool:
+        res = pool.map(_pool_worker, [(r, n, procs) for r in range(procs)])
+    _POOL.clear()
+    done = sum(c for c, _ in res)
+    slow = max(t for _, t in res)
+    return {'value': done / slow, 'unit': 'sentences/s', 'cores': procs, 'kind': 'port',
+            'sample': 'first %d sentences of the batch, k=1, oracle/ref_beam.py pure-Python restatement '
+                      'of beam.py:5-61 in %d processes (one per host core of the job), slowest '
+                      'worker %.1f s' % (done, procs, slow)}
+
+
 def cpu_baseline_c(packed, keys, coefs, k, budget_s):
     """The C restatement (oracle/lt_oracle.c: sorted-key binary search, OpenMP
     over sentences) on the host cores available to this job, on a bounded
@@ -211,11 +251,16 @@ def main():
     a = parse()
     lib = _capi.load()          # liblt binds its HIP runtime before torch (gloo) is imported
     d = Dist(a.gpus)
-    if lib.lt_device_count() < 1:
-        raise SystemExit('bench.py: no HIP device visible')
     t_gen = time.perf_counter()
     raw, lay, sm, packed, keys, coefs = make_workload(a.sentences, a.seed + 1000 * d.rank, a.features)
     t_gen = time.perf_counter() - t_gen
+    host_cores = max(1, min(int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1)), 64))
+    pool_baseline = None
+    if not a.no_cpu_baseline and d.world == 1:
+        # forked workers: before this process initialises the GPU
+        pool_baseline = cpu_baseline_pool(raw, sm, host_cores, a.cpu_seconds / 2)
+    if lib.lt_device_count() < 1:
+        raise SystemExit('bench.py: no HIP device visible')
     ctx = _capi.Context(d.local)
     dm = _capi.DeviceModel(ctx, keys, coefs)
     t_up = time.perf_counter()
@@ -348,6 +393,7 @@ def main():
         if not a.no_cpu_baseline and d.world == 1:
             line['cpu_baseline'] = cpu_baseline(raw, sm, a.cpu_seconds)
             line['cpu_baseline_c'] = cpu_baseline_c(packed, keys, coefs, a.k, a.cpu_seconds / 2)
+            line['cpu_baseline_pool'] = pool_baseline
         else:
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)
