@@ -1566,22 +1566,24 @@ static bool beam_one_per_wave() {
 // are uniform within a half; top-k is lt_beam_pk's exact rank counting and
 // threshold pruning, per half.
 // ---------------------------------------------------------------------------
-template <int KT, int WPB, bool NARROW>
-__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(3, 3)))
+template <int KT, int G, int WPB, bool NARROW>
+__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu((G == 16 && KT > 2) ? 2 : 3, 3)))
 lt_beam_hw(DecodeParams p) {
-  constexpr int RPC = 2;                        // scoring rounds (of 32) per chunk
-  constexpr int CH = 32 * RPC;                  // expansions per chunk per half
+  constexpr int S = 64 / G;                     // sentences per wave, one per lane group
+  constexpr int RPC = 2;                        // scoring rounds (of G) per chunk
+  constexpr int CH = G * RPC;                   // expansions per chunk per group
   constexpr int KTP = KT < 4 ? 4 : KT;
   constexpr int LN = KTP + CH;
-  constexpr int STAGE = 32;                     // records staged per half and position
-  static_assert(KT <= 32, "one writer lane per rank in a half");
-  __shared__ Entry ring[WPB][2][RING][KT];
-  __shared__ int32_t cntl[WPB][2][RING];
-  __shared__ uint4 stg[WPB][3 * 64];            // half h's record r: chunks 96h + 3r .. +2
-  __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][2][LN];
-  __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][2][LN];
-  __shared__ unsigned long long tkey[WPB][2][KT];
-  __shared__ uint32_t tgen[WPB][2][KT];
+  constexpr int STAGE = 64 / S;                 // records staged per group and position
+  constexpr int CPG = 3 * STAGE;                // staged 16 B chunks per group
+  static_assert(KT <= G && G >= MAX_SPAN + 1, "one writer lane per rank in a group; span starts fit a group");
+  __shared__ Entry ring[WPB][S][RING][KT];
+  __shared__ int32_t cntl[WPB][S][RING];
+  __shared__ uint4 stg[WPB][3 * 64];            // group h's record r: chunks CPG h + 3r .. +2
+  __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][S][LN];
+  __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][S][LN];
+  __shared__ unsigned long long tkey[WPB][S][KT];
+  __shared__ uint32_t tgen[WPB][S][KT];
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   Aux aux{nullptr, nullptr, 0u, p.hk};
@@ -1589,8 +1591,8 @@ lt_beam_hw(DecodeParams p) {
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
-  const int hf = lane >> 5, hl = lane & 31;
-  const int slot0 = (blockIdx.x * WPB + wv) * 2;
+  const int hf = lane / G, hl = lane % G;       // lane group (sentence) and lane in the group
+  const int slot0 = (blockIdx.x * WPB + wv) * S;
   if (slot0 >= p.n_sent) return;                // whole wave
   const Bufs B = make_bufs(p);
   const int k = p.k;
@@ -1605,9 +1607,21 @@ lt_beam_hw(DecodeParams p) {
   const uint32_t nbase = hv ? (uint32_t)p.node_off[s] : 0u;
   const int32_t* const ssp = p.span_start + (hv ? p.span_off[s] : 0);
   const int64_t bpo = hv ? p.bp_off[s] : 0;
-  const int nmax = max(__builtin_amdgcn_readlane(n, 0), __builtin_amdgcn_readlane(n, 32));
-  const uint32_t nb0 = (uint32_t)__builtin_amdgcn_readlane((int)nbase, 0);
-  const uint32_t nb1 = (uint32_t)__builtin_amdgcn_readlane((int)nbase, 32);
+  // the maximum of a group-uniform value over the groups
+  auto gmax = [&](int v) {
+    int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+    for (int h = 1; h < S; ++h) m = max(m, __builtin_amdgcn_readlane(v, h * G));
+    return m;
+  };
+  const int nmax = gmax(n);
+  uint32_t nbS[S];
+  int nS[S];
+#pragma unroll
+  for (int h = 0; h < S; ++h) {
+    nbS[h] = (uint32_t)__builtin_amdgcn_readlane((int)nbase, h * G);
+    nS[h] = __builtin_amdgcn_readlane(n, h * G);
+  }
   const rsrc_t bpr = make_rsrc(p.bp, (uint64_t)p.bp_bytes);
   Entry (*const R)[KT] = ring[wv][hf];
   int32_t* const cnt9 = cntl[wv][hf];
@@ -1615,7 +1629,7 @@ lt_beam_hw(DecodeParams p) {
   uint32_t* const LG = lgen[wv][hf];
   unsigned long long* const TK = tkey[wv][hf];
   uint32_t* const TG = tgen[wv][hf];
-  const unsigned long long hmask = hf ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+  const unsigned long long hmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (G * hf);
   auto hcount = [&](unsigned long long bal) { return __builtin_popcountll(bal & hmask); };
 
   if (hv && hl == 0) {                          // beam[0] = [BOS] (beam.py:21-23)
@@ -1627,23 +1641,26 @@ lt_beam_hw(DecodeParams p) {
     R[0][0] = e0;
     cnt9[0] = 1;
   }
-  // next position's first STAGE records of both halves (chunk c = 64 pl + lane
-  // of the wave's stream: half c / 96, chunk c % 96 of that half's block) and
-  // span starts (lane 32h + j <= 8: span start j of half h), one position
-  // ahead, issued after the position's last load wait (lt_beam_pk)
+  // next position's first STAGE records of every group (chunk c = 64 pl +
+  // lane of the wave's stream: group c / CPG, chunk c % CPG of that group's
+  // block) and span starts (lane G h + j <= 8: span start j of group h), one
+  // position ahead, issued after the position's last load wait (lt_beam_pk)
   u32x4 pf[3];
   int pfs = 0;
   auto prefetch = [&](int e1, int first_own) {
-    const int f0 = __builtin_amdgcn_readlane(first_own, 0), f1 = __builtin_amdgcn_readlane(first_own, 32);
-    const bool ok0 = e1 <= __builtin_amdgcn_readlane(n, 0), ok1 = e1 <= __builtin_amdgcn_readlane(n, 32);
+    int fS[S];
+#pragma unroll
+    for (int h = 0; h < S; ++h) fS[h] = __builtin_amdgcn_readlane(first_own, h * G);
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) {
       const int c = 64 * pl + lane;
-      const bool h1 = c >= 96;
-      const int cc = h1 ? c - 96 : c;
-      const bool ok = h1 ? ok1 : ok0;
-      const uint32_t o = ok ? ((h1 ? nb1 + (uint32_t)f1 : nb0 + (uint32_t)f0) * (uint32_t)sizeof(NodeRec) +
-                               (uint32_t)cc * 16u) : OOB;
+      const int hc = c / CPG, cc = c - hc * CPG;
+      uint32_t nb = nbS[0], f = (uint32_t)fS[0];
+      bool ok = e1 <= nS[0];
+#pragma unroll
+      for (int h = 1; h < S; ++h)
+        if (hc == h) { nb = nbS[h]; f = (uint32_t)fS[h]; ok = e1 <= nS[h]; }
+      const uint32_t o = ok ? (nb + f) * (uint32_t)sizeof(NodeRec) + (uint32_t)cc * 16u : OOB;
       pf[pl] = ld128(B.node, o);
     }
     pfs = (e1 <= n && hl <= MAX_SPAN) ? ssp[(e1 - 1) * MAX_SPAN + hl] : 0;
@@ -1660,8 +1677,12 @@ lt_beam_hw(DecodeParams p) {
     int ss[MAX_SPAN + 1];
 #pragma unroll
     for (int j = 0; j <= MAX_SPAN; ++j) {
-      const int a = __builtin_amdgcn_readlane(pfs, j), b = __builtin_amdgcn_readlane(pfs, 32 + j);
-      ss[j] = hf ? b : a;
+      if constexpr (S == 2) {
+        const int a = __builtin_amdgcn_readlane(pfs, j), b = __builtin_amdgcn_readlane(pfs, 32 + j);
+        ss[j] = hf ? b : a;
+      } else {
+        ss[j] = __shfl(pfs, hf * G + j);
+      }
     }
     __builtin_amdgcn_wave_barrier();
     const bool live = e <= n;
@@ -1677,7 +1698,7 @@ lt_beam_hw(DecodeParams p) {
       pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
     }
     const int M = pre[MAX_SPAN];                // this half's expansions
-    const int Mmax = max(__builtin_amdgcn_readlane(M, 0), __builtin_amdgcn_readlane(M, 32));
+    const int Mmax = gmax(M);
 
     auto decode = [&](int g, int& j, int& r, int& i) {
       j = 0;
@@ -1702,8 +1723,8 @@ lt_beam_hw(DecodeParams p) {
       for (int t = 0; t < RPC; ++t) {
         myk[t] = 0ull;
         myg[t] = INV;
-        if (base + 32 * t >= Mmax) continue;     // uniform
-        const int g = base + 32 * t + hl;
+        if (base + G * t >= Mmax) continue;      // uniform
+        const int g = base + G * t + hl;
         const bool act = g < M;
         int j = 0, r = 0, i = 0;
         if (act) decode(g, j, r, i);
@@ -1714,7 +1735,7 @@ lt_beam_hw(DecodeParams p) {
         if (!act) {
           c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
         } else if (so < STAGE) {
-          const uint4* q = cst + 96 * hf + 3 * so;
+          const uint4* q = cst + CPG * hf + 3 * so;
           const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
           c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
           c.pre = dbl(q1.x, q1.y); c.f4 = dbl(q1.z, q1.w);
@@ -1736,11 +1757,11 @@ lt_beam_hw(DecodeParams p) {
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
         }
-        LK[KTP + 32 * t + hl] = myk[t];
-        LG[KTP + 32 * t + hl] = myg[t];
+        LK[KTP + G * t + hl] = myk[t];
+        LG[KTP + G * t + hl] = myg[t];
       }
       // top-k of this half's chunk entries and its running top-k
-      const int R0 = max(0, min(RPC, (M - base + 31) >> 5));        // this half's rounds
+      const int R0 = max(0, min(RPC, (M - base + G - 1) / G));      // this group's rounds
       const unsigned long long rk = hl < nrun ? LK[KTP - nrun + hl] : 0ull;
       const uint32_t rg = hl < nrun ? LG[KTP - nrun + hl] : INV;
       int valid = nrun;
@@ -1750,8 +1771,8 @@ lt_beam_hw(DecodeParams p) {
       if (__builtin_amdgcn_ballot_w64(!single) == 0ull) {
         // one entry per lane in both halves: rank against the half's 32 list
         // slots of round 0 (slots past M hold 0 keys)
-        const int qe = KTP + ((min(32, max(M - base, 0)) + 3) & ~3);
-        const int qmax = max(__builtin_amdgcn_readlane(qe, 0), __builtin_amdgcn_readlane(qe, 32));
+        const int qe = KTP + ((min(G, max(M - base, 0)) + 3) & ~3);
+        const int qmax = gmax(qe);
         int rank = 0;
 #pragma unroll 2
         for (int q = KTP; q < qmax; q += 4) {
@@ -1775,7 +1796,7 @@ lt_beam_hw(DecodeParams p) {
         if (hl == 0) TK[0] = ~0ull;
         int gtc = 0;
 #pragma unroll 4
-        for (int q = 0; q < 32; q += 2) {
+        for (int q = 0; q < G; q += 2) {
           const ulonglong2 m2 = *reinterpret_cast<const ulonglong2*>(&MX[q]);
           gtc += (m2.x > mx ? 1 : 0) + (m2.y > mx ? 1 : 0);
         }
@@ -1786,7 +1807,7 @@ lt_beam_hw(DecodeParams p) {
         int nc = 0;
         auto push = [&](unsigned long long key, uint32_t g) {
           const bool c = key >= tau && key != 0ull;
-          const uint32_t bh = (uint32_t)((__ballot(c) & hmask) >> (32 * hf));
+          const uint32_t bh = (uint32_t)((__ballot(c) & hmask) >> (G * hf));
           const int at = nc + __builtin_popcount(bh & ((1u << hl) - 1u));
           if (c) { LK[at] = key; LG[at] = g; }
           nc += __builtin_popcount(bh);
@@ -1796,8 +1817,8 @@ lt_beam_hw(DecodeParams p) {
         for (int t = 0; t < RPC; ++t) push(myk[t], myg[t]);
         const int nc4 = (nc + 3) & ~3;
         if (hl < nc4 - nc) { LK[nc + hl] = 0ull; LG[nc + hl] = INV; }
-        const int ncmax = max(__builtin_amdgcn_readlane(nc, 0), __builtin_amdgcn_readlane(nc, 32));
-        for (int c0 = 0; c0 < ncmax; c0 += 32) {
+        const int ncmax = gmax(nc);
+        for (int c0 = 0; c0 < ncmax; c0 += G) {
           const int c = c0 + hl;
           const unsigned long long ck = c < nc ? LK[c] : 0ull;
           const uint32_t cg = c < nc ? LG[c] : INV;
@@ -1843,7 +1864,7 @@ lt_beam_hw(DecodeParams p) {
       bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
     };
     auto staged = [&](int r) {
-      const uint4* q = cst + 96 * hf + 3 * r;
+      const uint4* q = cst + CPG * hf + 3 * r;
       const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
       Cand c;
       c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
@@ -1891,12 +1912,25 @@ lt_beam_hw(DecodeParams p) {
   }
 }
 
-template <int KT, int WPB, bool NARROW>
+template <int KT, int G, int WPB, bool NARROW>
 hipError_t launch_hw(const DecodeParams& p, hipStream_t st) {
-  const int blocks = (p.n_sent + 2 * WPB - 1) / (2 * WPB);
+  constexpr int SPB = (64 / G) * WPB;
+  const int blocks = (p.n_sent + SPB - 1) / SPB;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_beam_hw<KT, WPB, NARROW>), dim3(blocks), dim3(64 * WPB), 0, st, p);
+  hipLaunchKernelGGL((lt_beam_hw<KT, G, WPB, NARROW>), dim3(blocks), dim3(64 * WPB), 0, st, p);
   return hipGetLastError();
+}
+
+// lanes per sentence of lt_beam_hw: 16 (four sentences per wave) where a
+// position has few expansions (k <= 3), else 32; LT_BEAM_G=16 / 32 forces one
+static int beam_group_lanes(int k) {
+  static const int forced = [] {
+    const char* e = std::getenv("LT_BEAM_G");
+    if (e && std::strcmp(e, "16") == 0) return 16;
+    if (e && std::strcmp(e, "32") == 0) return 32;
+    return 0;
+  }();
+  return forced ? forced : (k <= 3 ? 16 : 32);
 }
 
 
@@ -2000,10 +2034,18 @@ hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
   // half waves (two sentences per wave, 32 lanes each) for k = 2..8;
   // LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
   if (!COUNT && !beam_v1() && !beam_one_per_wave() && kt <= 8) {
+    if (beam_group_lanes(p.k) == 16) {
+      switch (kt) {
+        case 2: return launch_hw<2, 16, 4, NARROW>(p, st);
+        case 4: return launch_hw<4, 16, 4, NARROW>(p, st);
+        case 8: return launch_hw<8, 16, 4, NARROW>(p, st);
+        default: break;
+      }
+    }
     switch (kt) {
-      case 2: return launch_hw<2, 4, NARROW>(p, st);
-      case 4: return launch_hw<4, 4, NARROW>(p, st);
-      case 8: return launch_hw<8, 4, NARROW>(p, st);
+      case 2: return launch_hw<2, 32, 4, NARROW>(p, st);
+      case 4: return launch_hw<4, 32, 4, NARROW>(p, st);
+      case 8: return launch_hw<8, 32, 4, NARROW>(p, st);
       default: break;
     }
   }

@@ -1,0 +1,11 @@
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_g32.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest_g32.log; exit 1; }
+tail -1 gpurun_out/pytest_g32.log
+LT_BEAM_G=16 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_g16.log 2>&1 || { echo PYTEST_FAIL_G16; tail -40 gpurun_out/pytest_g16.log; exit 1; }
+tail -1 gpurun_out/pytest_g16.log
+for V in "32 2" "16 2" "32 3" "16 3" "32 5" "16 5"; do set -- $V
+LT_BEAM_G=$1 timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 2 --k $2 --no-cpu-baseline > gpurun_out/bench_g$1_k$2.log 2>&1 || { echo BENCH_FAIL; tail -30 gpurun_out/bench_g$1_k$2.log; exit 1; }
+python3 -c "import json;d=json.loads(open('gpurun_out/bench_g$1_k$2.log').read().strip().splitlines()[-1]);print('G=$1 k=$2', round(d['value']), 'kernel_ms', round(d['roofline']['avg_kernel_ms'],3), 'frac', round(d['roofline']['frac'],4))"
+done
