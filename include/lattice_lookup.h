@@ -85,7 +85,7 @@ typedef struct lt_lattices lt_lattices;
 
 lt_status lt_lexicon_create(const lt_lexicon_desc* desc, lt_lexicon** out);
 lt_status lt_lexicon_destroy(lt_lexicon* lexicon);
-/* Host only.  n_threads <= 0: hardware concurrency. */
+/* Host only.  n_threads <= 0: OMP_NUM_THREADS, else the hardware concurrency. */
 lt_status lt_lexicon_lookup(const lt_lexicon* lexicon, const lt_text_desc* text, int n_threads,
                             lt_lattices** out);
 lt_status lt_lattices_view(const lt_lattices* lattices, lt_lattice_view* view);

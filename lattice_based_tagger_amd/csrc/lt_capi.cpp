@@ -40,6 +40,17 @@ lt_status fail(lt_status st, const char* fmt, ...) {
 
 }  // namespace
 
+int lt::host_threads() {
+  static const int n = [] {
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+      const int v = std::atoi(e);
+      if (v > 0) return v;
+    }
+    return (int)std::max(1u, std::thread::hardware_concurrency());
+  }();
+  return n;
+}
+
 lt_status lt::set_error(lt_status st, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -437,7 +448,7 @@ template <class F>
 static void parallel_ranges(int64_t n, F fn) {
   const int64_t per = 1 << 16;
   int nt = (int)std::min<int64_t>((n + per - 1) / per, 32);
-  nt = std::max(1, std::min(nt, (int)std::max(1u, std::thread::hardware_concurrency())));
+  nt = std::max(1, std::min(nt, lt::host_threads()));
   if (nt == 1) {
     fn(0, (int64_t)0, n);
     return;

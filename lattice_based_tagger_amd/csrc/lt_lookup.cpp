@@ -723,7 +723,7 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_
   if (S > 0 && td->char_off[0] != 0) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: char_off[0] != 0");
   if (S > 0 && (td->eoj_off[td->sent_eoj[S]] >= ((int64_t)1 << 32) || td->sent_eoj[0] < 0))
     return lt::set_error(LT_EUNSUPPORTED, "lt_lexicon_lookup: text too long for one call");
-  int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int nt = n_threads > 0 ? n_threads : lt::host_threads();
   nt = std::max(1, std::min(nt, std::max(1, S / 16)));
   std::vector<Chunk> ck((size_t)nt);
   {

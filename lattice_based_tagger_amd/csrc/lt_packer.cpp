@@ -323,7 +323,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       }
     };
     const int64_t work = (int64_t)N;
-    int nt = (int)std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+    int nt = std::min(lt::host_threads(), 16);
     if (work < 200000) nt = 1;
     if (const char* env = std::getenv("LT_PACK_THREADS")) nt = std::max(1, std::atoi(env));
     nt = std::min<int>(nt, std::max<int32_t>(S, 1));
