@@ -83,6 +83,14 @@ class Dist:
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
+    def min(self, v):
+        if not self.pg:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MIN)
+        return float(t.item())
+
     def sum(self, v):
         if not self.pg:
             return v
@@ -270,11 +278,21 @@ def main():
 
     # result gather to rank 0 over RCCL/xGMI (the path's one exchange step)
     gather = d.world > 1 if a.gather is None else bool(a.gather)
-    comm = None
+    comm, gather_error = None, None
     if gather:
-        uid = d.broadcast_bytes(_capi.comm_unique_id() if d.rank == 0 else None)
-        comm = _capi.Comm(ctx, d.world, d.rank, uid)
-        comm.prepare(db, a.k, root=0)
+        try:
+            uid = d.broadcast_bytes(_capi.comm_unique_id() if d.rank == 0 else None)
+            comm = _capi.Comm(ctx, d.world, d.rank, uid)
+            comm.prepare(db, a.k, root=0)
+        except (_capi.LTError, OSError) as exc:      # reported in the JSON line, never silent
+            gather_error = '%s: %s' % (type(exc).__name__, exc)
+            print('bench.py: result gather disabled on rank %d: %s' % (d.rank, gather_error),
+                  file=sys.stderr)
+        if d.min(0.0 if gather_error else 1.0) < 1.0:  # every rank gathers, or none does
+            if comm:
+                comm.close()
+            comm = None
+            gather_error = gather_error or 'failed on another rank'
 
     def step():
         db.launch(dm, a.k)
@@ -315,7 +333,7 @@ def main():
     pcie_rate = d.sum(float(a.sentences * pcie_steps)) / d.max(tp)
 
     count, length, score, codes = db.results(a.k)
-    gather_info = None
+    gather_info = {'error': gather_error} if gather_error else None
     if comm:
         # the last gather delivered every rank's results of the same batch
         step()
