@@ -76,12 +76,14 @@ typedef struct {
   const int64_t* is_l;
 } lt_lattice_desc;
 
-/* Packed batch (library-owned arrays, valid until the next pack or destroy).
- * node_src: >= 0 dictionary word index, -1 BOS, -2 - (8 b + d - 1) Unknown
- * node of span (b, b + d). */
+/* Packed batch.  The arrays belong to `owner`, one block per pack, valid
+ * until lt_packed_release (independent of the packer and of later packs, so
+ * a pipeline can hold several).  node_src: >= 0 dictionary word index, -1
+ * BOS, -2 - (8 b + d - 1) Unknown node of span (b, b + d). */
 typedef struct {
   lt_batch_desc batch;
   const int64_t* node_src;
+  void* owner;
 } lt_packed;
 
 typedef struct lt_packer lt_packer;
@@ -89,6 +91,9 @@ lt_status lt_packer_create(const lt_packer_desc* desc, lt_packer** out);
 lt_status lt_packer_destroy(lt_packer* packer);
 /* max_len as beam_search's (1..8).  Host only; no GPU needed. */
 lt_status lt_packer_pack(lt_packer* packer, const lt_lattice_desc* lattices, int max_len, lt_packed* out);
+/* Frees one pack's arrays and zeroes *out (NULL or an already released
+ * lt_packed: no-op). */
+lt_status lt_packed_release(lt_packed* out);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,7 @@
 #include "lt_internal.h"
 #include "lt_error.h"
 #include "lt_handles.h"
+#include "lt_host.h"
 
 using namespace lt;
 
@@ -442,23 +443,6 @@ int64_t lt_model_slots(const lt_model* m) { return m ? m->slots : 0; }
 
 // ---------------------------------------------------------------- batch --
 extern "C++" {
-// Host-side batch preparation runs over millions of nodes: split [0, n)
-// into contiguous ranges on up to 32 threads (one range below 64K items).
-template <class F>
-static void parallel_ranges(int64_t n, F fn) {
-  const int64_t per = 1 << 16;
-  int nt = (int)std::min<int64_t>((n + per - 1) / per, 32);
-  nt = std::max(1, std::min(nt, lt::host_threads()));
-  if (nt == 1) {
-    fn(0, (int64_t)0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (int t = 1; t < nt; ++t) th.emplace_back(fn, t, n * t / nt, n * (t + 1) / nt);
-  fn(0, (int64_t)0, n / nt);
-  for (std::thread& x : th) x.join();
-}
-
 static bool hot_enabled() {
   static const bool on = [] {
     const char* v = std::getenv("LT_HOT");
@@ -507,6 +491,7 @@ static lt_status validate(const lt_batch_desc* d) {
     b.st = st;
     b.msg = buf;
   };
+  // sentence ranges: a sentence is hundreds of nodes, so split at 256 sentences
   parallel_ranges(d->n_sent, [&](int t, int64_t lo, int64_t hi) {
     for (int64_t s = lo; s < hi; ++s) {
       const int64_t n = d->sent_n[s];
@@ -534,7 +519,7 @@ static lt_status validate(const lt_batch_desc* d) {
         }
       }
     }
-  });
+  }, 256);
   if (const Bad* x = first_bad(bad)) return fail(x->st, "%s", x->msg.c_str());
   parallel_ranges(d->n_nodes, [&](int t, int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
@@ -645,7 +630,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
         for (int32_t v = ss[x]; v < ss[x + 1]; ++v) recs[(size_t)(base + v)].mask |= (dd - 1u) << D_SHIFT;
       }
     }
-  });
+  }, 256);
   up(&b->d_nodes, recs.get(), (size_t)d->n_nodes);
   if (hot_enabled()) {
     const uint32_t lim = 1u << NARROW_ID_BITS;

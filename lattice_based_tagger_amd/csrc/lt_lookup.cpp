@@ -27,6 +27,9 @@
 
 #include "../../include/lattice_lookup.h"
 #include "lt_error.h"
+#include "lt_host.h"
+
+using lt::Arr;
 
 namespace {
 
@@ -277,21 +280,6 @@ struct lt_lexicon {
   bool prefer_exact = true;
   uint64_t k0 = 0, k1 = 0;
 };
-
-namespace {
-// An uninitialised array (filled in parallel by lt_lexicon_lookup).
-template <class T>
-struct Arr {
-  std::unique_ptr<T[]> p;
-  int64_t n = 0;
-  bool alloc(int64_t k) {
-    p.reset(new (std::nothrow) T[(size_t)std::max<int64_t>(k, 1)]);
-    n = k;
-    return p != nullptr;
-  }
-  T* data() const { return p.get(); }
-};
-}  // namespace
 
 struct lt_lattices {
   int64_t n_sent = 0, n_words = 0;

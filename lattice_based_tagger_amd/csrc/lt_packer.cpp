@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <string_view>
@@ -22,6 +23,7 @@
 #include "../../include/lattice_pack.h"
 #include "lt_common.h"
 #include "lt_error.h"
+#include "lt_host.h"
 
 using namespace lt;
 
@@ -44,9 +46,8 @@ uint32_t node_mask(uint32_t vw, uint32_t vmo, uint32_t vt) {
          bit(vw, S71) * J7B | bit(vmo, S80) * J8A | bit(vw, S70) * I7A | bit(vmo, S80) * I8A;
 }
 
-// Key of a (string, string[, int]) tuple written into a reused buffer: a, b,
-// then a's length (strings with any byte, NUL included, split unambiguously),
-// then the optional integer.
+// Key of a (string, string) tuple written into a reused buffer: a, b, then
+// a's length (strings with any byte, NUL included, split unambiguously).
 std::string_view tuple_key(std::string& buf, std::string_view a, std::string_view b) {
   buf.clear();
   buf.append(a);
@@ -55,26 +56,90 @@ std::string_view tuple_key(std::string& buf, std::string_view a, std::string_vie
   buf.append(reinterpret_cast<const char*>(&la), sizeof la);
   return buf;
 }
-std::string_view tuple_key(std::string& buf, std::string_view a, std::string_view b, int64_t x) {
-  tuple_key(buf, a, b);
-  buf.append(reinterpret_cast<const char*>(&x), sizeof x);
-  return buf;
-}
 
-// string_view-keyed map over strings the packer owns (no allocation per lookup)
+// string_view-keyed map over strings the packer owns: open addressing over
+// (hash, pointer, length, value) records, so a lookup is one probe sequence
+// in one array (no allocation, no node chasing) -- the packer does several
+// per lattice node.
 template <typename V>
 struct ViewMap {
+  struct E {
+    uint64_t h;                                  // 0: empty
+    const char* s;
+    uint64_t n;
+    V v;
+  };
   std::vector<std::unique_ptr<std::string>> store;
-  std::unordered_map<std::string_view, V> map;
+  std::vector<E> tab = std::vector<E>(16, E{0, nullptr, 0, V()});
+  uint64_t mask = 15, count = 0;
+
+  static uint64_t hash(std::string_view k) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)k.size();
+    const char* s = k.data();
+    size_t n = k.size();
+    auto mix = [&](uint64_t x) {
+      h = (h ^ x) * 0xBF58476D1CE4E5B9ull;
+      h ^= h >> 31;
+    };
+    for (; n >= 8; n -= 8, s += 8) {
+      uint64_t x;
+      std::memcpy(&x, s, 8);
+      mix(x);
+    }
+    if (n) {
+      uint64_t x = 0;
+      std::memcpy(&x, s, n);
+      mix(x);
+    }
+    h ^= h >> 29;
+    h *= 0x94D049BB133111EBull;
+    h ^= h >> 32;
+    return h ? h : 1;
+  }
+  const E* find(std::string_view k, uint64_t h) const {
+    for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+      const E& e = tab[i];
+      if (e.h == 0) return nullptr;
+      if (e.h == h && e.n == k.size() && std::memcmp(e.s, k.data(), k.size()) == 0) return &e;
+    }
+  }
+  void insert(const E& x) {
+    uint64_t i = x.h & mask;
+    while (tab[i].h) i = (i + 1) & mask;
+    tab[i] = x;
+  }
   void put(std::string_view k, V v) {
-    if (map.count(k)) return;                    // first entry wins (Python dict semantics)
+    const uint64_t h = hash(k);
+    if (find(k, h)) return;                      // first entry wins (Python dict semantics)
+    if (2 * (count + 1) > tab.size()) {
+      std::vector<E> old(tab.size() * 2, E{0, nullptr, 0, V()});
+      old.swap(tab);
+      mask = tab.size() - 1;
+      for (const E& e : old)
+        if (e.h) insert(e);
+    }
     store.emplace_back(new std::string(k));
-    map.emplace(std::string_view(*store.back()), v);
+    insert(E{h, store.back()->data(), (uint64_t)k.size(), v});
+    ++count;
   }
   const V* get(std::string_view k) const {
-    auto it = map.find(k);
-    return it == map.end() ? nullptr : &it->second;
+    const E* e = find(k, hash(k));
+    return e ? &e->v : nullptr;
   }
+  V* get_mut(std::string_view k) { return const_cast<V*>(get(k)); }
+};
+
+// A vocabulary string's id (0: absent) and its class-5 coefficients
+// (word, tag0, is_l) -> coef as entries [c5_lo, c5_lo + c5_n) of
+// lt_packer::c5e: one probe answers both per node (the tables are far larger
+// than the caches, so each probe is a memory round trip).
+struct WordInfo {
+  int32_t id = 0, c5_lo = 0, c5_n = 0;
+};
+struct C5Entry {
+  std::string tag;
+  int64_t is_l;
+  double coef;
 };
 
 const std::string_view kUnk = "Unknown", kNoun = "Noun", kBOS = "BOS";
@@ -102,25 +167,63 @@ void utf8_append(std::string& out, uint32_t cp) {
 
 }  // namespace
 
+// One pack's output arrays, handed to the caller through lt_packed.owner
+// (uninitialised: every element is written by the thread that packs its
+// sentence, which also first-touches the pages).  A released block goes back
+// to its packer's pool (at most two, up to 2 GiB each), so a pipeline of packs
+// reuses mapped memory instead of faulting in fresh pages every call.
+struct PackPool;
+struct PackOut {
+  Arr<int32_t> sent_n, span_start, node_word, node_morph0, node_tag;
+  Arr<int64_t> sent_node_off, sent_span_off, node_src;
+  Arr<uint32_t> node_mask;
+  Arr<double> node_pre, node_f4, node_f5, node_f6, node_post;
+  std::shared_ptr<PackPool> pool;             // while handed out
+  size_t bytes() const {
+    return sent_n.bytes() + span_start.bytes() + node_word.bytes() + node_morph0.bytes() +
+           node_tag.bytes() + sent_node_off.bytes() + sent_span_off.bytes() + node_src.bytes() +
+           node_mask.bytes() + node_pre.bytes() + node_f4.bytes() + node_f5.bytes() + node_f6.bytes() +
+           node_post.bytes();
+  }
+};
+struct PackPool {
+  std::mutex mu;
+  std::vector<std::unique_ptr<PackOut>> free;
+  std::unique_ptr<PackOut> take() {
+    std::lock_guard<std::mutex> g(mu);
+    if (free.empty()) return std::unique_ptr<PackOut>(new (std::nothrow) PackOut);
+    std::unique_ptr<PackOut> o = std::move(free.back());
+    free.pop_back();
+    return o;
+  }
+};
+static void release_block(PackOut* o) {
+  std::shared_ptr<PackPool> pool = std::move(o->pool);
+  if (pool && o->bytes() <= ((size_t)2 << 30)) {
+    std::lock_guard<std::mutex> g(pool->mu);
+    if (pool->free.size() < 2) {
+      pool->free.emplace_back(o);
+      return;
+    }
+  }
+  delete o;
+}
+
 struct lt_packer {
-  ViewMap<int32_t> vocab;
+  std::shared_ptr<PackPool> pool = std::make_shared<PackPool>();
+  ViewMap<WordInfo> vocab;                          // vocabulary strings and class-5 words
   std::vector<uint32_t> vmask;
   std::unordered_map<int64_t, double> c4, c6;
-  ViewMap<double> c5;                               // (word, tag0, is_l)
+  std::vector<C5Entry> c5e;                         // grouped by word (WordInfo::c5_lo)
   int32_t n_local = 0, n_pre = 0;
   std::vector<int32_t> kind;
   std::vector<double> reg;                          // 3 per scorer
   std::vector<ViewMap<double>> pref;                // per scorer: (tag, key) -> value
   std::string kb;                                   // key buffer
-  // output buffers
-  std::vector<int32_t> sent_n, span_start, node_word, node_morph0, node_tag;
-  std::vector<int64_t> sent_node_off, sent_span_off, node_src;
-  std::vector<uint32_t> node_mask;
-  std::vector<double> node_pre, node_f4, node_f5, node_f6, node_post;
 
   int32_t id_of(std::string_view s) const {
-    const int32_t* v = vocab.get(s);
-    return v ? *v : 0;
+    const WordInfo* v = vocab.get(s);
+    return v ? v->id : 0;
   }
   uint32_t vm(int32_t id) const { return id >= 0 && (size_t)id < vmask.size() ? vmask[(size_t)id] : 0u; }
 };
@@ -134,12 +237,28 @@ lt_status lt_packer_create(const lt_packer_desc* d, lt_packer** out) {
   if (!p) return set_error(LT_ENOMEM, "lt_packer_create: out of memory");
   try {
     for (int64_t i = 0; i < d->vocab.n; ++i)
-      if (!is_null(d->vocab, i)) p->vocab.put(str_at(d->vocab, i), d->vocab_id[i]);
+      if (!is_null(d->vocab, i)) p->vocab.put(str_at(d->vocab, i), WordInfo{d->vocab_id[i], 0, 0});
     p->vmask.assign(d->vmask, d->vmask + d->n_vmask);
     for (int64_t i = 0; i < d->n4; ++i) p->c4.emplace(d->c4_len[i], d->c4_coef[i]);
     for (int64_t i = 0; i < d->n6; ++i) p->c6.emplace(d->c6_len[i], d->c6_coef[i]);
-    for (int64_t i = 0; i < d->c5_word.n; ++i)
-      p->c5.put(tuple_key(p->kb, str_at(d->c5_word, i), str_at(d->c5_tag, i), d->c5_isl[i]), d->c5_coef[i]);
+    // class-5 entries grouped by word, in input order within a word (the
+    // first of equal keys wins, as the Python dict the entries come from)
+    std::vector<int64_t> c5_order((size_t)d->c5_word.n);
+    for (int64_t i = 0; i < d->c5_word.n; ++i) c5_order[(size_t)i] = i;
+    std::stable_sort(c5_order.begin(), c5_order.end(), [&](int64_t x, int64_t y) {
+      return str_at(d->c5_word, x) < str_at(d->c5_word, y);
+    });
+    for (size_t j = 0; j < c5_order.size();) {
+      const std::string_view w = str_at(d->c5_word, c5_order[j]);
+      if (!p->vocab.get(w)) p->vocab.put(w, WordInfo{0, 0, 0});
+      WordInfo* wi = p->vocab.get_mut(w);
+      wi->c5_lo = (int32_t)p->c5e.size();
+      for (; j < c5_order.size() && str_at(d->c5_word, c5_order[j]) == w; ++j) {
+        const int64_t i = c5_order[j];
+        p->c5e.push_back(C5Entry{std::string(str_at(d->c5_tag, i)), d->c5_isl[i], d->c5_coef[i]});
+      }
+      wi->c5_n = (int32_t)p->c5e.size() - wi->c5_lo;
+    }
     p->n_local = d->n_local;
     p->n_pre = d->n_pre;
     p->kind.assign(d->local_kind, d->local_kind + d->n_local);
@@ -214,154 +333,189 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
     for (int64_t i = L->slot_off[g]; i < L->slot_off[g + 1]; ++i) c += L->e[i] == e;
     return c ? c : 1;
   };
-  try {
-    // pass 1: nodes per sentence -> offsets (span entries: 8 n + 1 per sentence)
-    p->sent_n.resize((size_t)S);
-    p->sent_node_off.assign((size_t)S + 1, 0);
-    p->sent_span_off.assign((size_t)S + 1, 0);
-    for (int32_t s = 0; s < S; ++s) {
+  std::unique_ptr<PackOut> o = p->pool->take();
+  if (!o) return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
+  o->pool = p->pool;
+  // pass 1: nodes per sentence (threads over sentences) -> offsets
+  // (span entries: 8 n + 1 per sentence)
+  if (!o->sent_n.alloc(S) || !o->sent_node_off.alloc((int64_t)S + 1) || !o->sent_span_off.alloc((int64_t)S + 1))
+    return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
+  parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
+    for (int64_t s = lo; s < hi; ++s) {
       const int64_t c0 = L->char_off[s];
       const int32_t n = (int32_t)(L->char_off[s + 1] - c0);
       int64_t cnt = 1;                                    // BOS
       for (int32_t e = 1; e <= n; ++e)
         for (int d = 1; d <= max_len && d <= e; ++d) cnt += span_count(c0 + e - d, e);
-      p->sent_n[(size_t)s] = n;
-      p->sent_node_off[(size_t)s + 1] = p->sent_node_off[(size_t)s] + cnt;
-      p->sent_span_off[(size_t)s + 1] = p->sent_span_off[(size_t)s] + 8 * (int64_t)n + 1;
+      o->sent_n[s] = n;
+      o->sent_node_off[s + 1] = cnt;
+      o->sent_span_off[s + 1] = 8 * (int64_t)n + 1;
     }
-    const size_t N = (size_t)p->sent_node_off[(size_t)S];
-    p->span_start.resize((size_t)p->sent_span_off[(size_t)S]);
-    p->node_word.resize(N); p->node_morph0.resize(N); p->node_tag.resize(N);
-    p->node_mask.resize(N); p->node_pre.resize(N); p->node_f4.resize(N); p->node_f5.resize(N);
-    p->node_f6.resize(N); p->node_src.resize(N);
-    p->node_post.assign((size_t)n_post * N, 0.0);
+  }, 256);
+  o->sent_node_off[0] = 0;
+  o->sent_span_off[0] = 0;
+  for (int32_t s = 0; s < S; ++s) {
+    o->sent_node_off[s + 1] += o->sent_node_off[s];
+    o->sent_span_off[s + 1] += o->sent_span_off[s];
+  }
+  const int64_t N = o->sent_node_off[S];
+  if (!o->span_start.alloc(o->sent_span_off[S]) || !o->node_word.alloc(N) || !o->node_morph0.alloc(N) ||
+      !o->node_tag.alloc(N) || !o->node_mask.alloc(N) || !o->node_pre.alloc(N) || !o->node_f4.alloc(N) ||
+      !o->node_f5.alloc(N) || !o->node_f6.alloc(N) || !o->node_src.alloc(N) ||
+      !o->node_post.alloc((int64_t)n_post * N))
+    return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
 
-    // pass 2: fill, sentences split over threads (the tables are read-only)
-    auto fill = [&](int32_t s_lo, int32_t s_hi) {
-      std::string kb, unk;
-      auto add_node = [&](size_t x, const NodeView& w, int64_t src) {
-        const int32_t wid = p->id_of(w.word), tid = p->id_of(w.tag0);
-        const int32_t mid = w.morph0.data() == w.word.data() && w.morph0.size() == w.word.size()
-                                ? wid : p->id_of(w.morph0);
-        uint32_t m = node_mask(p->vm(wid), p->vm(mid), p->vm(tid));
-        const bool unk_node = w.tag0 == kUnk;
-        if (unk_node) m |= F_UNK;
-        if (contextual(w.tag0)) m |= F_CTX;
-        double f4 = 0.0, f5 = 0.0, f6 = 0.0;
-        if (auto it = p->c4.find(w.len); it != p->c4.end()) { m |= F_HAS4; f4 = it->second; }
-        if (const double* v = p->c5.get(tuple_key(kb, w.word, w.tag0, w.is_l))) { m |= F_HAS5; f5 = *v; }
-        if (unk_node) {
-          if (auto it = p->c6.find(w.len < 8 ? w.len : 8); it != p->c6.end()) { m |= F_HAS6; f6 = it->second; }
-        }
-        // node-local scorers in constructor order (lowering.node_terms)
-        double pre = 0.0;
-        for (int t = 0; t < p->n_local; ++t) {
-          double v;
-          switch (p->kind[(size_t)t]) {
-            case LT_SCORER_REGULARIZATION: v = regularization(&p->reg[3 * (size_t)t], w); break;
-            case LT_SCORER_MORPH_PREF:                   // score_funcs.py:84-88
-              v = lookup(kb, p->pref[(size_t)t], w.tag0, w.morph0);
-              if (w.has_tag1) v = v + (w.has_morph1 ? lookup(kb, p->pref[(size_t)t], w.tag1, w.morph1) : 0.0);
-              break;
-            default:                                     // WordPreference, score_funcs.py:99-100
-              v = lookup(kb, p->pref[(size_t)t], w.tag0, w.word);
-          }
-          if (t < p->n_pre) pre = pre + v;
-          else p->node_post[(size_t)(t - p->n_pre) * N + x] = v;
-        }
-        p->node_word[x] = wid;
-        p->node_morph0[x] = mid;
-        p->node_tag[x] = tid;
-        p->node_mask[x] = m;
-        p->node_pre[x] = pre;
-        p->node_f4[x] = f4;
-        p->node_f5[x] = f5;
-        p->node_f6[x] = f6;
-        p->node_src[x] = src;
-      };
-      for (int32_t s = s_lo; s < s_hi; ++s) {
-        const int64_t c0 = L->char_off[s];
-        const int32_t n = p->sent_n[(size_t)s];
-        const size_t base = (size_t)p->sent_node_off[(size_t)s];
-        int32_t* ss = p->span_start.data() + p->sent_span_off[(size_t)s];
-        NodeView bos{kBOS, kBOS, kBOS, {}, {}, false, false, 0, 0};
-        add_node(base, bos, -1);
-        int32_t local = 1;
-        for (int32_t e = 1; e <= n; ++e) {
-          for (int d = LT_MAX_SPAN; d >= 1; --d) {
-            *ss++ = local;
-            const int32_t b = e - d;
-            if (d > max_len || b < 0) continue;
-            const int64_t g = c0 + b;
-            bool any = false;
-            for (int64_t i = L->slot_off[g]; i < L->slot_off[g + 1]; ++i) {
-              if (L->e[i] != e) continue;                 // beam.py:33 (w.e == e)
-              NodeView v;
-              v.word = str_at(L->word, i);
-              v.morph0 = str_at(L->morph0, i);
-              v.tag0 = str_at(L->tag0, i);
-              v.has_morph1 = !is_null(L->morph1, i);
-              v.has_tag1 = !is_null(L->tag1, i);
-              v.morph1 = v.has_morph1 ? str_at(L->morph1, i) : std::string_view();
-              v.tag1 = v.has_tag1 ? str_at(L->tag1, i) : std::string_view();
-              v.len = L->len[i];
-              v.is_l = L->is_l[i];
-              add_node(base + (size_t)local, v, i);
-              ++local;
-              any = true;
-            }
-            if (!any) {                                   // beam.py:36-38: Unknown chars[b:e]
-              unk.clear();
-              for (int32_t x = b; x < e; ++x) utf8_append(unk, L->chars[c0 + x]);
-              NodeView u{unk, unk, kUnk, {}, {}, false, false, (int64_t)d, 0};
-              add_node(base + (size_t)local, u, -2 - (8 * (int64_t)b + d - 1));
-              ++local;
-            }
-          }
-        }
-        *ss = local;
+  // pass 2: fill, sentences split over threads (the tables are read-only)
+  PackOut& q = *o;
+
+  auto fill = [&](int, int64_t s_lo, int64_t s_hi) {
+    std::string kb, unk;
+    // tags are few: remember the last distinct ones (their strings live in
+    // the lattice blobs for the whole call)
+    std::string_view memo_s[16];
+    int32_t memo_id[16];
+    int n_memo = 0;
+    auto tag_id = [&](std::string_view t) {
+      for (int i = 0; i < n_memo; ++i)
+        if (memo_s[i] == t) return memo_id[i];
+      const int32_t id = p->id_of(t);
+      if (n_memo < 16) {
+        memo_s[n_memo] = t;
+        memo_id[n_memo++] = id;
       }
+      return id;
     };
-    const int64_t work = (int64_t)N;
-    int nt = std::min(lt::host_threads(), 16);
-    if (work < 200000) nt = 1;
-    if (const char* env = std::getenv("LT_PACK_THREADS")) nt = std::max(1, std::atoi(env));
-    nt = std::min<int>(nt, std::max<int32_t>(S, 1));
-    if (nt <= 1) {
-      fill(0, S);
-    } else {
-      std::vector<std::thread> th;
-      for (int t = 0; t < nt; ++t) {
-        const int32_t lo = (int32_t)((int64_t)S * t / nt), hi = (int32_t)((int64_t)S * (t + 1) / nt);
-        th.emplace_back(fill, lo, hi);
+    auto add_node = [&](int64_t x, const NodeView& w, int64_t src) {
+      const WordInfo* wi = p->vocab.get(w.word);
+      const int32_t wid = wi ? wi->id : 0, tid = tag_id(w.tag0);
+      const int32_t mid = w.morph0.data() == w.word.data() && w.morph0.size() == w.word.size()
+                              ? wid : p->id_of(w.morph0);
+      uint32_t m = node_mask(p->vm(wid), p->vm(mid), p->vm(tid));
+      const bool unk_node = w.tag0 == kUnk;
+      if (unk_node) m |= F_UNK;
+      if (contextual(w.tag0)) m |= F_CTX;
+      double f4 = 0.0, f5 = 0.0, f6 = 0.0;
+      if (auto it = p->c4.find(w.len); it != p->c4.end()) { m |= F_HAS4; f4 = it->second; }
+      if (wi) {                                          // (word, tag0, is_l) -> coef
+        for (int32_t j = wi->c5_lo; j < wi->c5_lo + wi->c5_n; ++j) {
+          const C5Entry& c = p->c5e[(size_t)j];
+          if (c.is_l == w.is_l && c.tag == w.tag0) {
+            m |= F_HAS5;
+            f5 = c.coef;
+            break;
+          }
+        }
       }
-      for (auto& x : th) x.join();
+      if (unk_node) {
+        if (auto it = p->c6.find(w.len < 8 ? w.len : 8); it != p->c6.end()) { m |= F_HAS6; f6 = it->second; }
+      }
+      // node-local scorers in constructor order (lowering.node_terms)
+      double pre = 0.0;
+      for (int t = 0; t < p->n_local; ++t) {
+        double v;
+        switch (p->kind[(size_t)t]) {
+          case LT_SCORER_REGULARIZATION: v = regularization(&p->reg[3 * (size_t)t], w); break;
+          case LT_SCORER_MORPH_PREF:                   // score_funcs.py:84-88
+            v = lookup(kb, p->pref[(size_t)t], w.tag0, w.morph0);
+            if (w.has_tag1) v = v + (w.has_morph1 ? lookup(kb, p->pref[(size_t)t], w.tag1, w.morph1) : 0.0);
+            break;
+          default:                                     // WordPreference, score_funcs.py:99-100
+            v = lookup(kb, p->pref[(size_t)t], w.tag0, w.word);
+        }
+        if (t < p->n_pre) pre = pre + v;
+        else q.node_post[(int64_t)(t - p->n_pre) * N + x] = v;
+      }
+      q.node_word[x] = wid;
+      q.node_morph0[x] = mid;
+      q.node_tag[x] = tid;
+      q.node_mask[x] = m;
+      q.node_pre[x] = pre;
+      q.node_f4[x] = f4;
+      q.node_f5[x] = f5;
+      q.node_f6[x] = f6;
+      q.node_src[x] = src;
+    };
+    for (int64_t s = s_lo; s < s_hi; ++s) {
+      const int64_t c0 = L->char_off[s];
+      const int32_t n = q.sent_n[s];
+      const int64_t base = q.sent_node_off[s];
+      int32_t* ss = q.span_start.data() + q.sent_span_off[s];
+      NodeView bos{kBOS, kBOS, kBOS, {}, {}, false, false, 0, 0};
+      add_node(base, bos, -1);
+      int32_t local = 1;
+      for (int32_t e = 1; e <= n; ++e) {
+        for (int d = LT_MAX_SPAN; d >= 1; --d) {
+          *ss++ = local;
+          const int32_t b = e - d;
+          if (d > max_len || b < 0) continue;
+          const int64_t g = c0 + b;
+          bool any = false;
+          for (int64_t i = L->slot_off[g]; i < L->slot_off[g + 1]; ++i) {
+            if (L->e[i] != e) continue;                 // beam.py:33 (w.e == e)
+            NodeView v;
+            v.word = str_at(L->word, i);
+            v.morph0 = str_at(L->morph0, i);
+            v.tag0 = str_at(L->tag0, i);
+            v.has_morph1 = !is_null(L->morph1, i);
+            v.has_tag1 = !is_null(L->tag1, i);
+            v.morph1 = v.has_morph1 ? str_at(L->morph1, i) : std::string_view();
+            v.tag1 = v.has_tag1 ? str_at(L->tag1, i) : std::string_view();
+            v.len = L->len[i];
+            v.is_l = L->is_l[i];
+            add_node(base + local, v, i);
+            ++local;
+            any = true;
+          }
+          if (!any) {                                   // beam.py:36-38: Unknown chars[b:e]
+            unk.clear();
+            for (int32_t x = b; x < e; ++x) utf8_append(unk, L->chars[c0 + x]);
+            NodeView u{unk, unk, kUnk, {}, {}, false, false, (int64_t)d, 0};
+            add_node(base + local, u, -2 - (8 * (int64_t)b + d - 1));
+            ++local;
+          }
+        }
+      }
+      *ss = local;
     }
+  };
+  int64_t per = 256;                                   // sentences per thread range, at least
+  if (const char* env = std::getenv("LT_PACK_THREADS"))
+    per = std::max<int64_t>(1, ((int64_t)S + std::max(1, std::atoi(env)) - 1) / std::max(1, std::atoi(env)));
+  try {
+    parallel_ranges(S, fill, per);
   } catch (...) {
     return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
   }
 
   lt_batch_desc& b = out->batch;
-  std::memset(&b, 0, sizeof b);
+  std::memset(out, 0, sizeof *out);
   b.n_sent = S;
   b.max_len = max_len;
   b.n_post = n_post;
   b.has_trigram = 0;            // set by the caller (the trigram is not the packer's concern)
-  b.n_nodes = (int64_t)p->node_word.size();
-  b.n_span = (int64_t)p->span_start.size();
-  b.sent_n = p->sent_n.data();
-  b.sent_node_off = p->sent_node_off.data();
-  b.sent_span_off = p->sent_span_off.data();
-  b.span_start = p->span_start.data();
-  b.node_word = p->node_word.data();
-  b.node_morph0 = p->node_morph0.data();
-  b.node_tag = p->node_tag.data();
-  b.node_mask = p->node_mask.data();
-  b.node_pre = p->node_pre.data();
-  b.node_f4 = p->node_f4.data();
-  b.node_f5 = p->node_f5.data();
-  b.node_f6 = p->node_f6.data();
-  b.node_post = n_post ? p->node_post.data() : nullptr;
-  out->node_src = p->node_src.data();
+  b.n_nodes = N;
+  b.n_span = o->sent_span_off[S];
+  b.sent_n = o->sent_n.data();
+  b.sent_node_off = o->sent_node_off.data();
+  b.sent_span_off = o->sent_span_off.data();
+  b.span_start = o->span_start.data();
+  b.node_word = o->node_word.data();
+  b.node_morph0 = o->node_morph0.data();
+  b.node_tag = o->node_tag.data();
+  b.node_mask = o->node_mask.data();
+  b.node_pre = o->node_pre.data();
+  b.node_f4 = o->node_f4.data();
+  b.node_f5 = o->node_f5.data();
+  b.node_f6 = o->node_f6.data();
+  b.node_post = n_post ? o->node_post.data() : nullptr;
+  out->node_src = o->node_src.data();
+  out->owner = o.release();
+  return LT_OK;
+}
+
+lt_status lt_packed_release(lt_packed* out) {
+  if (!out) return LT_OK;
+  if (out->owner) release_block(static_cast<PackOut*>(out->owner));
+  std::memset(out, 0, sizeof *out);
   return LT_OK;
 }

@@ -54,7 +54,28 @@ class LatticeDesc(C.Structure):
 
 
 class Packed(C.Structure):
-    _fields_ = [('batch', _capi.BatchDesc), ('node_src', C.c_void_p)]
+    _fields_ = [('batch', _capi.BatchDesc), ('node_src', C.c_void_p), ('owner', C.c_void_p)]
+
+
+class _PackBlock:
+    """Owns one lt_packer_pack result; the arrays handed out are views of it
+    (numpy bases hold this object), so the block lives as long as any view."""
+
+    def __init__(self, lib, out):
+        self.lib, self.out = lib, out
+
+    def view(self, p, ct, n, dt):
+        if n == 0 or not p:
+            return np.zeros(0, dtype=dt)
+        buf = (ct * n).from_address(p)
+        buf._block = self
+        return np.frombuffer(buf, dtype=dt)
+
+    def __del__(self):
+        try:
+            self.lib.lt_packed_release(C.byref(self.out))
+        except Exception:
+            pass
 
 
 def _ptr(a):
@@ -250,13 +271,10 @@ class NativePacker:
         the sentences' characters.  -> (PackedBatch, node views)."""
         out = Packed()
         _capi.check(self.lib.lt_packer_pack(self.handle, C.byref(desc), int(max_len), C.byref(out)))
+        block = _PackBlock(self.lib, out)       # no copies: the arrays are views of the pack
         b = out.batch
         N, S, nspan, npost = b.n_nodes, b.n_sent, b.n_span, b.n_post
-
-        def arr(p, ct, n, dt):
-            if n == 0 or not p:
-                return np.zeros(0, dtype=dt)
-            return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(n,)).astype(dt, copy=True)
+        arr = block.view
         batch = PackedBatch(
             max_len=int(max_len), n_post=int(npost), has_trigram=int(self.model.has_trigram),
             sent_n=arr(b.sent_n, C.c_int32, S, np.int32),

@@ -82,3 +82,34 @@ def test_unsupported_inputs_are_refused():
         npk.pack([([[Word(3, 'a', None, 'Noun', None, 1, 0, 1, False)]], 'a')])
     with pytest.raises(Unsupported):
         NativePacker(lowered_model(SF.BeamScoreFunctions(SF.WordPreferenceScore({'Noun': {1: 2.0}}))))
+
+
+def test_pack_blocks_are_independent_and_recycled():
+    """Each pack's arrays are views of their own block: a later pack (which
+    may reuse a released block's memory) leaves live arrays untouched, and
+    a recycled block packs the same values as a fresh one."""
+    import gc
+    raw = synth.make_lattices(120, seed=9, extra_lambda=2.0, dup_rate=0.3)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=9, n_features=20_000)
+    dic, coef = synth.render_model(raw, sm)
+    funcs = SF.BeamScoreFunctions(SF.RegularizationScore(),
+                                  SF.SimpleTrigramFeatureScore(FE.SimpleTrigramEncoder(dic), coef))
+    sents = synth.render_sentences(raw, range(raw.S))
+    npk = NativePacker(lowered_model(funcs))
+    a, _ = npk.pack(sents[:60])
+    keep = {f: getattr(a, f).copy() for f in FIELDS}
+    for _ in range(4):                                   # blocks released and taken again
+        b, _ = npk.pack(sents[60:])
+        del b
+        gc.collect()
+    for f in FIELDS:
+        assert np.array_equal(getattr(a, f), keep[f]), f
+    del a
+    gc.collect()
+    again, _ = npk.pack(sents[:60])                      # a recycled block
+    for f in FIELDS:
+        assert np.array_equal(getattr(again, f), keep[f]), f
+    npk.close()
+    assert again.node_word.sum() == keep['node_word'].sum()   # the views outlive the packer
