@@ -112,8 +112,22 @@ def load(path=None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        # Calls that only queue work or copy a few bytes, bound a second time
+        # through PyDLL (the GIL stays held): a CDLL call releases the GIL
+        # and must win it back from whichever pipeline thread runs Python --
+        # up to a switch interval (5 ms) per call -- which costs more than
+        # these calls do.
+        held = C.PyDLL(path)
+        for name in HELD_CALLS:
+            fn = getattr(held, name)
+            fn.restype, fn.argtypes = sig[name]
+        lib.held = held
         _lib = lib
         return lib
+
+
+# lt_* entry points that return in microseconds (see load)
+HELD_CALLS = ('lt_decode_launch', 'lt_result_fetch', 'lt_result_view')
 
 
 def check(status):
@@ -275,15 +289,15 @@ class DeviceBatch:
         self.max_k = int(max_k)
 
     def launch(self, model, k):
-        check(self.ctx._lib.lt_decode_launch(self.ctx.handle, model.handle, self.handle, int(k)))
+        check(self.ctx._lib.held.lt_decode_launch(self.ctx.handle, model.handle, self.handle, int(k)))
 
     def fetch(self):
-        check(self.ctx._lib.lt_result_fetch(self.ctx.handle, self.handle))
+        check(self.ctx._lib.held.lt_result_fetch(self.ctx.handle, self.handle))
 
     def results(self, k):
         """numpy copies of (count, length, score, codes) after fetch + sync."""
         v = Result()
-        check(self.ctx._lib.lt_result_view(self.handle, C.byref(v)))
+        check(self.ctx._lib.held.lt_result_view(self.handle, C.byref(v)))
         S = self.n_sent
         nc = int(self.cum_n[-1]) * k
 

@@ -136,17 +136,42 @@ class Decoder:
     # node records per launch (lt_batch_create takes < 2^31 B of 48 B records)
     MAX_NODES = 40_000_000
 
-    def decode_packed(self, model, packed, k):
-        """Decode a PackedBatch (in launches of at most MAX_NODES nodes);
-        returns (count, length, score, codes, cum_n)."""
+    def upload(self, model, packed, k):
+        """Device batches of a PackedBatch, one per launch piece of at most
+        MAX_NODES nodes, as (s0, s1, DeviceBatch).  Safe from a worker thread
+        while this thread's caller decodes (lt_batch_create only queues
+        copies on the context's stream), so uploads overlap decodes."""
+        out = []
+        try:
+            for s0, s1 in packed.split(self.MAX_NODES):
+                piece = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
+                out.append((s0, s1, _capi.DeviceBatch(self.ctx, piece, max_k=k)))
+        except BaseException:
+            for _, _, db in out:
+                db.close()
+            raise
+        return out
+
+    def decode_packed(self, model, packed, k, uploaded=None):
+        """Decode a PackedBatch (in launches of at most MAX_NODES nodes, or
+        the pieces ``upload`` made of it); returns (count, length, score,
+        codes, cum_n)."""
         dm = self.device_model(model)
         parts = []
-        for s0, s1 in packed.split(self.MAX_NODES):
-            piece = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
-            db = _capi.DeviceBatch(self.ctx, piece, max_k=k)
+        pieces = uploaded if uploaded is not None else packed.split(self.MAX_NODES)
+        for piece in pieces:
+            if uploaded is not None:
+                db = piece[2]
+            else:
+                s0, s1 = piece
+                sub = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
+                db = _capi.DeviceBatch(self.ctx, sub, max_k=k)
             try:
                 parts.append(db.decode(dm, k))
             finally:
+                db.close()
+        if uploaded is not None:
+            for _, _, db in uploaded:
                 db.close()
         if len(parts) == 1:
             count, length, score, codes = parts[0]
@@ -190,16 +215,19 @@ def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device
     return decode_batch(packed, objs, [ch for _, ch in sentences], model, k, device)
 
 
-def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False):
+def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, uploaded=None):
     """Decode a packed batch and re-materialise the matures: ``objs[s][i]`` is
     the Word of sentence s's local node i, ``chars_list[s]`` its characters.
     ``best_only``: only the best mature of each sentence (what Tagger.tag
-    returns, tagger.py:78)."""
+    returns, tagger.py:78).  ``uploaded``: ``Decoder.upload``'s device
+    batches of ``packed`` (closed here)."""
     if k == 0:
+        for _, _, db in uploaded or ():
+            db.close()
         # beam_size=0 keeps no hypothesis past BOS (beam.py:85 slices to [])
         return [[Sequence([bos_word(), eos_word(0)], 0)] if len(ch) == 0 else []
                 for ch in chars_list]
-    count, length, score, codes, cum_n = Decoder.get(device).decode_packed(model, packed, k)
+    count, length, score, codes, cum_n = Decoder.get(device).decode_packed(model, packed, k, uploaded)
     T = 1 if best_only else k
     if objs and hasattr(getattr(objs[0], 'words', None), 'words_bulk'):
         return _materialise_bulk(packed, objs, chars_list, k, T, count, length, score, codes, cum_n)

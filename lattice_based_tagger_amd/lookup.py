@@ -70,6 +70,9 @@ def _lib():
         for name, (res, args) in _SIGS.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
+        # a short gather: keep the GIL across it (see _capi.load)
+        fn = lib.held.lt_lattices_strings
+        fn.restype, fn.argtypes = _SIGS['lt_lattices_strings']
         lib._lookup_sigs = True
     return lib
 
@@ -368,7 +371,7 @@ class NativeLattices:
             need = int((off[idx + 1] - off[idx]).sum()) + idx.size
             buf = C.create_string_buffer(need)
             used = C.c_int64()
-            _capi.check(self.lib.lt_lattices_strings(self.handle, f, idx.ctypes.data, idx.size, buf,
+            _capi.check(self.lib.held.lt_lattices_strings(self.handle, f, idx.ctypes.data, idx.size, buf,
                                                      need, C.byref(used)))
             vals = buf.raw[:need].decode('utf-8').split('\0')[:idx.size] if b'\0' not in blob else \
                 [blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()]

@@ -14,6 +14,7 @@ Python, grouped into a begin index as `lookup.py:7-62, 344-369` do.
 Decoding runs on the device.
 """
 
+import gc
 import sys
 
 from .beam import beam_search_batch
@@ -179,15 +180,17 @@ class Tagger:
         return self.tag_batch([sent], beam_size=beam_size)[0]
 
     # sentences per pipeline chunk of tag_batch
-    CHUNK = 8192
+    CHUNK = 4096
 
     def tag_batch(self, sents, beam_size=5):
         """Best ``Sequence`` per sentence.  Raises IndexError like ``tag``
         when a non-empty sentence has no dictionary node at all
-        (`beam.py:32`).  With native lattices the batch runs as a two-stage
-        pipeline over chunks of CHUNK sentences: a worker thread builds and
-        packs chunk i+1 (C++, outside the GIL) while this thread uploads,
-        decodes and re-materialises chunk i."""
+        (`beam.py:32`).  With native lattices the batch runs as a
+        three-stage pipeline over chunks of CHUNK sentences: one worker
+        thread builds and packs chunk i+2 (C++, outside the GIL), a second
+        uploads chunk i+1 (node records, host-to-device copies), while this
+        thread decodes and re-materialises chunk i.  The cyclic GC is paused
+        meanwhile (millions of fresh tuples, no cycles)."""
         sents = list(sents)
         lex = self.native_lexicon()
         if lex is None:
@@ -195,8 +198,18 @@ class Tagger:
             matures = beam_search_batch(lattices, self.score_funcs, beam_size=beam_size,
                                         device=self.device)
             return [m[0] for m in matures]
+        enabled = gc.isenabled()
+        gc.disable()
+        try:
+            return self._tag_native(lex, sents, beam_size)
+        finally:
+            if enabled:
+                gc.enable()
+
+    def _tag_native(self, lex, sents, beam_size):
+        from collections import deque
         from concurrent.futures import ThreadPoolExecutor
-        from .beam import _check_beam, decode_batch, lowered_model
+        from .beam import Decoder, _check_beam, decode_batch, lowered_model
         from .native_packer import packer_for
         k = _check_beam(beam_size)
         chunks = [sents[i:i + self.CHUNK] for i in range(0, len(sents), self.CHUNK)] or [[]]
@@ -211,6 +224,10 @@ class Tagger:
         lat0 = lookup(chunks[0])                   # (the reference raises before scoring)
         model = lowered_model(self.score_funcs)
         npk = packer_for(model)
+        dec = None
+        if npk is not None and k > 0:
+            dec = Decoder.get(self.device)
+            dec.device_model(model)                # built here, before any worker uses it
 
         def front(chunk, lat=None):
             lat = lat if lat is not None else lookup(chunk)
@@ -219,19 +236,40 @@ class Tagger:
             packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
             return lat, packed, views
 
+        def upload(fut):
+            lat, packed, views = fut.result()
+            dbs = dec.upload(model, packed, k) if dec is not None and packed is not None else None
+            return lat, packed, views, dbs
+
         out = []
-        with ThreadPoolExecutor(max_workers=1) as pool:
-            fut = pool.submit(front, chunks[0], lat0)
-            for i in range(len(chunks)):
-                lat, packed, views = fut.result()
-                if i + 1 < len(chunks):
-                    fut = pool.submit(front, chunks[i + 1])
-                if packed is None:
-                    lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(chunks[i]))]
-                    matures = beam_search_batch(lattices, self.score_funcs, beam_size=k,
-                                                device=self.device)
-                else:
-                    matures = decode_batch(packed, views, lat.chars, model, k, self.device,
-                                           best_only=True)
-                out += [m[0] for m in matures]
+        with ThreadPoolExecutor(max_workers=1) as builder, ThreadPoolExecutor(max_workers=1) as uploader:
+            stages = deque()
+
+            def feed(i):
+                if i < len(chunks):
+                    stages.append(uploader.submit(upload, builder.submit(front, chunks[i],
+                                                                         lat0 if i == 0 else None)))
+            feed(0)
+            feed(1)
+            try:
+                for i in range(len(chunks)):
+                    lat, packed, views, dbs = stages.popleft().result()
+                    feed(i + 2)
+                    if packed is None:
+                        lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(chunks[i]))]
+                        matures = beam_search_batch(lattices, self.score_funcs, beam_size=k,
+                                                    device=self.device)
+                    else:
+                        matures = decode_batch(packed, views, lat.chars, model, k, self.device,
+                                               best_only=True, uploaded=dbs)
+                    out += [m[0] for m in matures]
+            finally:
+                for f in stages:                   # an error: drop what is still in flight
+                    f.cancel()
+                    if not f.cancelled():
+                        try:
+                            for _, _, db in f.result()[3] or ():
+                                db.close()
+                        except BaseException:
+                            pass
         return out

@@ -37,6 +37,7 @@ def main():
     ap.add_argument('--threads', type=int, default=0)
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--chunk', type=int, default=0, help='Tagger.tag_batch pipeline chunk (0: default)')
+    ap.add_argument('--profile', action='store_true', help='cProfile the tag_batch call (stderr)')
     a = ap.parse_args()
     entry = _fixture()['base']
     funcs = load('base')[0].funcs
@@ -85,6 +86,14 @@ def main():
     t0 = time.perf_counter()
     out = tagger.tag_batch(sents, beam_size=a.k)
     api = time.perf_counter() - t0
+    if a.profile:
+        import cProfile
+        import pstats
+        prof = cProfile.Profile()
+        prof.enable()
+        tagger.tag_batch(sents, beam_size=a.k)
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats('tottime').print_stats(25)
     assert len(out) == len(sents) and all(o.score == m[0].score for o, m in zip(out, matures))
     line = {'metric': 'end-to-end Tagger.tag_batch sentences/s (text -> best Sequence)',
             'sentences': len(sents), 'k': a.k, 'lattice_nodes': n_words,
