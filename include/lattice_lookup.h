@@ -97,6 +97,18 @@ lt_status lt_lattices_destroy(lt_lattices* lattices);
  * needed, with LT_EINVAL, when cap is too small). */
 lt_status lt_lattices_strings(const lt_lattices* lattices, int field, const int64_t* idx, int64_t n,
                               char* out, int64_t cap, int64_t* used);
+/* The same strings dictionary-coded: codes[i] is the index of node idx[i]'s
+ * string among the distinct strings (first-appearance order), -1 for None;
+ * the distinct strings are written to out NUL-terminated, *n_unique of them.
+ * cap >= the field's blob bytes + n always suffices; a smaller cap that
+ * does not fit fails with LT_EINVAL and *used = the bytes needed.  A string
+ * holding a NUL byte fails with LT_EUNSUPPORTED (use lt_lattices_strings'
+ * offsets instead). */
+lt_status lt_lattices_strings_coded(const lt_lattices* lattices, int field, const int64_t* idx, int64_t n,
+                                    int32_t* codes, char* out, int64_t cap, int64_t* used,
+                                    int64_t* n_unique);
+/* Bytes of one string field's blob (the cap bound above, less n). */
+int64_t lt_lattices_field_bytes(const lt_lattices* lattices, int field);
 
 /* CPython 3.10 hash() of the str with these code points under SipHash key
  * (k0, k1) -- test hook for the set-order reproduction. */

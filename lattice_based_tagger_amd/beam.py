@@ -282,23 +282,28 @@ def _materialise_bulk_body(packed, objs, chars_list, k, T, count, length, score,
     dic = np.flatnonzero(src >= 0)
     for j, w in zip(dic.tolist(), lat.words_bulk(src[dic])):
         flat[j] = w
-    for j in np.flatnonzero(src < 0).tolist():          # synthesised Unknown nodes (BOS never on a path)
-        code = -2 - int(src[j])
-        b, d = code // 8, code % 8 + 1
-        sub = chars_list[int(seg[j]) // T][b:b + d]
-        flat[j] = Word(sub, sub, None, Unk, None, d, b, b + d, False)
+    unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
+    if unk.size:
+        code = -2 - src[unk]
+        for j, b, d, s in zip(unk.tolist(), (code // 8).tolist(), (code % 8 + 1).tolist(),
+                              (seg[unk] // T).tolist()):
+            sub = chars_list[s][b:b + d]
+            flat[j] = Word(sub, sub, None, Unk, None, d, b, b + d, False)
+    # the sentinels are immutable tuples: one BOS, one EOS per sentence length
+    bos, eos = bos_word(), {}
     out = []
     pos = 0
     cnt = np.minimum(count, T).tolist()
     Ll = L.tolist()
     sc = score.tolist()
-    for s in range(S):
-        nch = len(chars_list[s])
+    for s, nch in enumerate(n.tolist()):
+        e = eos.get(nch)
+        if e is None:
+            e = eos[nch] = eos_word(nch)
         matures = []
         for tt in range(cnt[s]):
             ln = Ll[s][tt]
-            matures.append(Sequence([bos_word()] + flat[pos:pos + ln] + [eos_word(nch)],
-                                    sc[s][tt] if nch > 0 else 0, 0))
+            matures.append(Sequence([bos] + flat[pos:pos + ln] + [e], sc[s][tt] if nch > 0 else 0, 0))
             pos += ln
         out.append(matures)
     return out

@@ -208,6 +208,7 @@ lt_status lt_ctx_create(int device, lt_ctx** out) {
   if (!c) return fail(LT_ENOMEM, "lt_ctx_create: out of host memory");
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
@@ -227,6 +228,7 @@ lt_status lt_ctx_destroy(lt_ctx* c) {
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->ustream) (void)hipStreamDestroy(c->ustream);
   delete c;
   return LT_OK;
 }
@@ -590,7 +592,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
                 slots);
   }
 
-  hipStream_t stm = c->stream;
+  hipStream_t stm = c->ustream;     // complete when this returns (synchronised below)
   hipError_t e = hipSuccess;
   auto up = [&](auto** dst, const auto* src, size_t count) {
     if (e == hipSuccess) e = dalloc_copy(dst, src, count, stm);

@@ -10,7 +10,9 @@
 
 struct lt_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;    // decodes, result copies, gathers
+  hipStream_t ustream = nullptr;   // lt_batch_create's uploads (a pipeline's upload
+                                   // thread does not queue behind the decodes)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   unsigned long long* d_counters = nullptr;
 };

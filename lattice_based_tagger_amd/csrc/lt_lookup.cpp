@@ -23,6 +23,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <string_view>
 #include <vector>
 
 #include "../../include/lattice_lookup.h"
@@ -818,6 +819,78 @@ lt_status lt_lattices_strings(const lt_lattices* L, int field, const int64_t* id
     *p++ = '\0';
   }
   return LT_OK;
+}
+
+lt_status lt_lattices_strings_coded(const lt_lattices* L, int field, const int64_t* idx, int64_t n,
+                                    int32_t* codes, char* out, int64_t cap, int64_t* used,
+                                    int64_t* n_unique) {
+  if (!L || (n > 0 && (!idx || !codes)) || field < 0 || field > 4)
+    return lt::set_error(LT_EINVAL, "lt_lattices_strings_coded: bad argument");
+  const Arr<char>* blobs[] = {&L->wb, &L->mb, &L->m1b, &L->tb, &L->t1b};
+  const Arr<int64_t>* offs[] = {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off};
+  const uint8_t* null = field == 2 ? L->m1null.data() : field == 4 ? L->t1null.data() : nullptr;
+  const char* blob = blobs[field]->data();
+  const int64_t* off = offs[field]->data();
+  // open addressing over (hash, code); the distinct strings in `uniq`
+  struct Slot {
+    uint64_t h;                                    // 0: empty
+    int32_t code;
+  };
+  size_t tn = 64;
+  while (tn < (size_t)n * 2) tn <<= 1;
+  std::vector<Slot> tab;
+  std::vector<std::string_view> uniq;
+  try {
+    tab.assign(tn, Slot{0, 0});
+  } catch (...) {
+    return lt::set_error(LT_ENOMEM, "lt_lattices_strings_coded: out of memory");
+  }
+  const uint64_t mask = tn - 1;
+  int64_t need = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = idx[i];
+    if (v < 0 || v >= L->n_words)
+      return lt::set_error(LT_EINVAL, "lt_lattices_strings_coded: index %lld", (long long)v);
+    if (null && null[v]) {
+      codes[i] = -1;
+      continue;
+    }
+    const std::string_view sv(blob + off[v], (size_t)(off[v + 1] - off[v]));
+    uint64_t h = 0xCBF29CE484222325ull;            // FNV-1a, then a final mix
+    for (unsigned char ch : sv) h = (h ^ ch) * 0x100000001B3ull;
+    h ^= h >> 29;
+    h = (h * 0xBF58476D1CE4E5B9ull) | 1ull;
+    uint64_t j = h & mask;
+    for (;; j = (j + 1) & mask) {
+      if (tab[j].h == 0) {
+        if (std::memchr(sv.data(), 0, sv.size()))   // NUL inside: the NUL-separated form cannot hold it
+          return lt::set_error(LT_EUNSUPPORTED, "lt_lattices_strings_coded: string with a NUL byte");
+        tab[j] = Slot{h, (int32_t)uniq.size()};
+        uniq.push_back(sv);
+        need += (int64_t)sv.size() + 1;
+        break;
+      }
+      if (tab[j].h == h && uniq[(size_t)tab[j].code] == sv) break;
+    }
+    codes[i] = tab[j].code;
+  }
+  if (used) *used = need;
+  if (n_unique) *n_unique = (int64_t)uniq.size();
+  if (need > cap || (need > 0 && !out))
+    return lt::set_error(LT_EINVAL, "lt_lattices_strings_coded: %lld bytes needed", (long long)need);
+  char* p = out;
+  for (const std::string_view& sv : uniq) {
+    memcpy(p, sv.data(), sv.size());
+    p += sv.size();
+    *p++ = '\0';
+  }
+  return LT_OK;
+}
+
+int64_t lt_lattices_field_bytes(const lt_lattices* L, int field) {
+  if (!L || field < 0 || field > 4) return 0;
+  const Arr<int64_t>* offs[] = {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off};
+  return L->n_words ? (*offs[field])[L->n_words] : 0;
 }
 
 lt_status lt_lattices_destroy(lt_lattices* L) {

@@ -61,6 +61,10 @@ _SIGS = {
     'lt_py_set2_second_first': (C.c_int, [C.c_int64, C.c_int64]),
     'lt_lattices_strings': (C.c_int32, [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
                                         C.c_int64, C.POINTER(C.c_int64)]),
+    'lt_lattices_strings_coded': (C.c_int32, [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
+                                              C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
+                                              C.POINTER(C.c_int64)]),
+    'lt_lattices_field_bytes': (C.c_int64, [C.c_void_p, C.c_int]),
 }
 
 
@@ -70,9 +74,10 @@ def _lib():
         for name, (res, args) in _SIGS.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
-        # a short gather: keep the GIL across it (see _capi.load)
-        fn = lib.held.lt_lattices_strings
-        fn.restype, fn.argtypes = _SIGS['lt_lattices_strings']
+        # short gathers: keep the GIL across them (see _capi.load)
+        for name in ('lt_lattices_strings', 'lt_lattices_strings_coded', 'lt_lattices_field_bytes'):
+            fn = getattr(lib.held, name)
+            fn.restype, fn.argtypes = _SIGS[name]
         lib._lookup_sigs = True
     return lib
 
@@ -321,6 +326,17 @@ class NativeLattices:
                             if S else 1)
         self.char_off = arr(d.char_off, C.c_int64, S + 1)
         self._cols = None
+        self._ints = None
+
+    def _int_columns(self):
+        """len / b / e / is_l as views of the library's arrays (no copies)."""
+        if self._ints is None:
+            d, N = self.desc, self.n_words
+
+            def ints(p):
+                return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), shape=(N,)) if N else None
+            self._ints = {'len': ints(d.len), 'b': ints(self.view.b), 'e': ints(d.e), 'is_l': ints(d.is_l)}
+        return self._ints
 
     def _columns(self):
         if self._cols is None:
@@ -358,31 +374,40 @@ class NativeLattices:
         return self.word(int(i))
 
     def words_bulk(self, idx):
-        """[Word] of global node indices ``idx`` (int array), built with one
-        ragged gather + one UTF-8 decode per field instead of per node."""
-        idx = np.asarray(idx, dtype=np.int64)
+        """[Word] of global node indices ``idx`` (int array).  Each string
+        field comes back dictionary-coded from one C call (the distinct
+        strings, decoded once, plus an int32 code per node), so a path's
+        repeated tags and words share str objects instead of being decoded
+        per node."""
+        idx = np.ascontiguousarray(np.asarray(idx, dtype=np.int64))
         if idx.size == 0:
             return []
-        c = self._columns()
         fields = []
-        idx = np.ascontiguousarray(idx)
+        codes = np.empty(idx.size, dtype=np.int32)
+        lib = self.lib.held
+        cap = max(int(lib.lt_lattices_field_bytes(self.handle, f)) for f in range(5)) + idx.size
+        buf = C.create_string_buffer(cap)                       # one for the five fields
+        used, n_u = C.c_int64(), C.c_int64()
         for f, name in enumerate(('word', 'morph0', 'morph1', 'tag0', 'tag1')):
-            (blob, off), null = c[name]
-            need = int((off[idx + 1] - off[idx]).sum()) + idx.size
-            buf = C.create_string_buffer(need)
-            used = C.c_int64()
-            _capi.check(self.lib.held.lt_lattices_strings(self.handle, f, idx.ctypes.data, idx.size, buf,
-                                                     need, C.byref(used)))
-            vals = buf.raw[:need].decode('utf-8').split('\0')[:idx.size] if b'\0' not in blob else \
-                [blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()]
-            if null is not None:
-                for j in np.flatnonzero(null[idx]).tolist():
-                    vals[j] = None
-            fields.append(vals)
-        lens = c['len'][idx].tolist()
-        bs = c['b'][idx].tolist()
-        es = c['e'][idx].tolist()
-        isl = (c['is_l'][idx] != 0).tolist()
+            st = lib.lt_lattices_strings_coded(self.handle, f, idx.ctypes.data, idx.size,
+                                               codes.ctypes.data, buf, cap, C.byref(used), C.byref(n_u))
+            if st == _capi.LT_EUNSUPPORTED:                     # a NUL inside a string: slice each
+                (blob, off), null = self._columns()[name]
+                vals = [blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()]
+                if null is not None:
+                    for j in np.flatnonzero(null[idx]).tolist():
+                        vals[j] = None
+                fields.append(vals)
+                continue
+            _capi.check(st)
+            uniq = np.empty(n_u.value + 1, dtype=object)        # [-1] -> None
+            uniq[:n_u.value] = C.string_at(buf, used.value).decode('utf-8').split('\0')[:n_u.value]
+            fields.append(uniq[codes].tolist())
+        ints = self._int_columns()
+        lens = ints['len'][idx].tolist()
+        bs = ints['b'][idx].tolist()
+        es = ints['e'][idx].tolist()
+        isl = (ints['is_l'][idx] != 0).tolist()
         return list(map(_new_word, zip(*fields, lens, bs, es, isl)))
 
     def empty(self, s):

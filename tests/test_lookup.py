@@ -151,3 +151,18 @@ def test_words_bulk_equals_word(fix):
     assert [tuple(w) for w in bulk] == [tuple(lat.word(int(i))) for i in idx]
     assert all(type(w.is_l) is bool for w in bulk)
     assert lat.words_bulk(np.zeros(0, dtype=np.int64)) == []
+
+
+def test_words_bulk_strings_with_nul():
+    """A dictionary word holding a NUL byte cannot travel NUL-separated: the
+    coded gather refuses it and words_bulk slices that field instead."""
+    import numpy as np
+    from types import SimpleNamespace
+    d = SimpleNamespace(tag_to_morphs={'Noun': {'a\x00b', 'c'}}, verbs=set(), adjectives=set(),
+                        eomis=set(), rules={})
+    lex = LK.NativeLexicon(d, [], 3, True, hash_key=ZERO_KEY)
+    lat = lex.lookup(['a\x00b c', 'c'])
+    idx = np.arange(lat.n_words, dtype=np.int64)
+    bulk = lat.words_bulk(idx)
+    assert [tuple(w) for w in bulk] == [tuple(lat.word(int(i))) for i in idx]
+    assert any('\x00' in w.word for w in bulk)
