@@ -306,6 +306,34 @@ struct Worker {
 
   const Info* find(const uint32_t* s, uint32_t n) const { return lx.table.find(s, n); }
 
+  // Lookups of substrings of the current eojeol, memoised: the lemmatizer
+  // and the lr / standalone scans probe the same (start, length) pairs many
+  // times over (every substring's lemmatisation re-probes its 1-3 syllable
+  // windows and its suffixes).  Eojeols longer than MEMO_MAX probe directly.
+  static constexpr uint32_t MEMO_MAX = 48;
+  uint32_t m_off = 0, m_n = 0;
+  std::vector<const Info*> memo;
+  std::vector<uint8_t> memo_ok;
+  void begin_eojeol(uint32_t off, uint32_t n) {
+    m_off = off;
+    m_n = n <= MEMO_MAX ? n : 0;
+    const size_t sz = (size_t)(m_n + 1) * (m_n + 1);
+    if (memo.size() < sz) memo.resize(sz);
+    memo_ok.assign(sz, 0);
+  }
+  // find(text + s, len) for a substring of the text
+  const Info* find_t(uint32_t s, uint32_t len) {
+    if (s >= m_off && len <= m_n && s - m_off <= m_n - len) {
+      const size_t k = (size_t)(s - m_off) * (m_n + 1) + len;
+      if (!memo_ok[k]) {
+        memo[k] = find(text + s, len);
+        memo_ok[k] = 1;
+      }
+      return memo[k];
+    }
+    return find(text + s, len);
+  }
+
   static bool has(const Info* in, int32_t tag) { return tag >= 0 && in && ((in->tags >> tag) & 1u); }
 
   int32_t keep(const std::vector<uint32_t>& s) {
@@ -329,6 +357,17 @@ struct Worker {
       out.push_back(WordRec{w_off, m, so, sl, eo, el, lx.name_verb, lx.name_eomi, len, b, e, is_l});
   }
 
+  // consider() of the split text[s .. s + sl) + text[s + sl .. s + sl + el)
+  void consider_text(uint32_t s, uint32_t sl, uint32_t el, uint32_t w_off, uint32_t m, int32_t len,
+                     int32_t b, int32_t e, bool is_l, std::vector<WordRec>& out) {
+    const Info* ei = find_t(s + sl, el);
+    if (!ei || !(ei->flags & F_EOMI)) return;
+    const Info* si = find_t(s, sl);
+    if (!si || !(si->flags & (F_ADJ | F_VERB))) return;
+    set_cand(text + s, sl, nullptr, 0, text + s + sl, el, nullptr, 0);
+    consider(w_off, m, len, b, e, is_l, out);
+  }
+
   void set_cand(const uint32_t* s1, size_t n1, const uint32_t* s2, size_t n2,
                 const uint32_t* e1, size_t m1, const uint32_t* e2, size_t m2) {
     sbuf.assign(s1, s1 + n1);
@@ -347,14 +386,11 @@ struct Worker {
     const uint32_t* P = lx.table.pool.data();
     for (uint32_t i = 0; i < m; ++i) {
       // (l, r) = (word[:i+1], word[i+1:]), while i < max_i
-      if (i + 1 < m) {
-        set_cand(w, i + 1, nullptr, 0, w + i + 1, m - i - 1, nullptr, 0);
-        consider(w_off, m, len, b, e, is_l, out);
-      }
+      if (i + 1 < m) consider_text(w_off, i + 1, m - i - 1, w_off, m, len, b, e, is_l, out);
       // 1 syllable conjugation: the pairs of rules[c], |rules[c]| times over
       // (the nested loop of lemmatizer.py:100-101) -- every repetition emits
       // the same words, so one pass is scored and its words repeated
-      if (const Info* ci = find(w + i, 1); ci && ci->rule_n > 0) {
+      if (const Info* ci = find_t(w_off + i, 1); ci && ci->rule_n > 0) {
         const size_t first = out.size();
         for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
           const RulePair& rp = R[(size_t)q];
@@ -372,8 +408,8 @@ struct Worker {
       const uint32_t n2 = std::min<uint32_t>(2, m - i), n3 = std::min<uint32_t>(3, m - i);
       const uint32_t* rest = w + std::min<uint32_t>(m, i + 2);
       const uint32_t nrest = m - std::min<uint32_t>(m, i + 2);
-      const Info* c2 = find(w + i, n2);
-      const Info* c3 = n3 != n2 ? find(w + i, n3) : nullptr;
+      const Info* c2 = find_t(w_off + i, n2);
+      const Info* c3 = n3 != n2 ? find_t(w_off + i, n3) : nullptr;
       const Info* conj[2] = {c2 && c2->rule_n ? c2 : nullptr, c3 && c3->rule_n ? c3 : nullptr};
       if (conj[0] && conj[1] &&
           set2_second_first(py_str_hash(w + i, n2, lx.k0, lx.k1), py_str_hash(w + i, n3, lx.k0, lx.k1)))
@@ -391,7 +427,7 @@ struct Worker {
 
   // MorphemeDictionary.lookup(word, b, is_l) (dictionary.py:304-315)
   void dict_lookup(uint32_t w_off, uint32_t n, int32_t b, bool is_l, std::vector<WordRec>& out) {
-    if (const Info* in = find(text + w_off, n)) {
+    if (const Info* in = find_t(w_off, n)) {
       for (int32_t t = 0; t < lx.n_dict_tags; ++t)
         if ((in->tags >> t) & 1u)
           out.push_back(WordRec{w_off, n, -1, 0, -1, 0, t, -1, (int32_t)n, b, b + (int32_t)n, is_l});
@@ -407,7 +443,7 @@ struct Worker {
 
   bool is_noun_josa(uint32_t e_off, uint32_t n, uint32_t i) {
     if (lx.dict_noun < 0 || lx.dict_josa < 0) return false;
-    return has(find(text + e_off, i), lx.dict_noun) && has(find(text + e_off + i, n - i), lx.dict_josa);
+    return has(find_t(e_off, i), lx.dict_noun) && has(find_t(e_off + i, n - i), lx.dict_josa);
   }
 
   // lr_lookup (lookup.py:171-210)
@@ -433,6 +469,7 @@ struct Worker {
 
   // morpheme_lookup (lookup.py:212-279)
   void morpheme_lookup(uint32_t e_off, uint32_t n, int32_t offset, std::vector<WordRec>& out) {
+    begin_eojeol(e_off, n);
     const size_t start = out.size();
     lr_lookup(e_off, n, offset, false, out);
     if (lx.prefer_exact && out.size() > start) return;
@@ -444,7 +481,7 @@ struct Worker {
       const uint32_t e_hi = std::min(b + max_len, n);
       for (uint32_t e = b + 1; e <= e_hi; ++e) {
         const uint32_t so = e_off + b, sl = e - b;
-        const Info* in = find(text + so, sl);
+        const Info* in = find_t(so, sl);
         const int32_t B = offset + (int32_t)b, E = offset + (int32_t)e;
         for (const Standalone& st : lx.standalones)
           if (has(in, st.dict_tag)) {
