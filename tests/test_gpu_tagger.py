@@ -44,3 +44,25 @@ def test_tagger_native_lattices_match_reference(gpu_decoder, name, chunk, monkey
                     assert tuple(w) == tuple(c.node(code)), (sent, k)
     one = tagger.tag(sents[0], beam_size=5)
     assert float(one.score).hex() == by_chars[sents[0].replace(' ', '')].expected['5']['matures'][0][1]
+
+
+def test_tagger_pipeline_error_in_a_later_chunk(gpu_decoder, monkeypatch):
+    """A sentence without any dictionary node in the fourth pipeline chunk
+    raises the reference's IndexError from tag_batch (the chunks before it
+    already decoded), and the tagger decodes correctly afterwards -- nothing
+    in flight is left behind."""
+    monkeypatch.setattr(Tagger, 'CHUNK', 8)
+    entry = _fixture()['base']
+    cases = load('base')
+    by_chars = {c.chars: c for c in cases}
+    sents = [s for s in entry['sentences'] if s.replace(' ', '') in by_chars
+             and by_chars[s.replace(' ', '')].bindex][:48]
+    tagger = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=fixture_lexicon(entry),
+                    score_funcs=cases[0].funcs)
+    bad = sents[:27] + ['ㅋㅋㅋ'] + sents[27:]
+    with pytest.raises(IndexError):
+        tagger.tag_batch(bad, beam_size=5)
+    best = tagger.tag_batch(sents, beam_size=5)
+    for sent, seq in zip(sents, best):
+        shex = by_chars[sent.replace(' ', '')].expected['5']['matures'][0][1]
+        assert float(seq.score).hex() == shex, sent
