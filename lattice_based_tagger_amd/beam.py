@@ -229,7 +229,7 @@ def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, 
                 for ch in chars_list]
     count, length, score, codes, cum_n = Decoder.get(device).decode_packed(model, packed, k, uploaded)
     T = 1 if best_only else k
-    if objs and hasattr(getattr(objs[0], 'words', None), 'words_bulk'):
+    if objs and hasattr(objs[0], 'src') and hasattr(objs[0], 'words'):      # native packer's views
         return _materialise_bulk(packed, objs, chars_list, k, T, count, length, score, codes, cum_n)
     out = []
     for s, chars in enumerate(chars_list):
@@ -248,8 +248,9 @@ def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, 
 
 
 def _materialise_bulk(*args):
-    """decode_batch's result for lattices built natively: every path node's
-    Word is built in bulk (lookup.NativeLattices.words_bulk).  The cyclic GC
+    """decode_batch's result for lattices packed natively: every path node's
+    Word is gathered in bulk (lookup.NativeLattices.words_bulk for native
+    lattices, the caller's Word list otherwise).  The cyclic GC
     is paused meanwhile: millions of fresh tuples would otherwise trigger
     repeated full collections (4x the construction time)."""
     enabled = gc.isenabled()
@@ -280,7 +281,11 @@ def _materialise_bulk_body(packed, objs, chars_list, k, T, count, length, score,
     lat = objs[0].words
     flat = [None] * total
     dic = np.flatnonzero(src >= 0)
-    for j, w in zip(dic.tolist(), lat.words_bulk(src[dic])):
+    sel = src[dic]
+    # native lattices build their Words in bulk; Word lists hand back the
+    # caller's own objects (as the reference's paths hold them)
+    words = lat.words_bulk(sel) if hasattr(lat, 'words_bulk') else [lat[i] for i in sel.tolist()]
+    for j, w in zip(dic.tolist(), words):
         flat[j] = w
     unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
     if unk.size:
