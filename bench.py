@@ -267,9 +267,12 @@ def main():
     if not a.no_cpu_baseline and d.world == 1:
         # forked workers: before this process initialises the GPU
         pool_baseline = cpu_baseline_pool(raw, sm, host_cores, a.cpu_seconds / 2)
-    if lib.lt_device_count() < 1:
+    ndev = lib.lt_device_count()
+    if ndev < 1:
         raise SystemExit('bench.py: no HIP device visible')
-    ctx = _capi.Context(d.local)
+    # one GPU per local rank; a launcher that shows each rank only its own
+    # GPU (or a rehearsal with more ranks than GPUs) maps round-robin
+    ctx = _capi.Context(d.local % ndev)
     dm = _capi.DeviceModel(ctx, keys, coefs)
     t_up = time.perf_counter()
     db = _capi.DeviceBatch(ctx, packed, max_k=a.k)          # H2D, outside the timed region
@@ -406,7 +409,8 @@ def main():
             'kernel_only_sentences_per_s': a.sentences / avg_kernel_s,
             'pcie_inclusive_sentences_per_s': pcie_rate,
             'gather': gather_info,
-            'host': {'gen_s': t_gen, 'h2d_s': t_up, 'nproc': os.cpu_count(), 'cpu': cpu_model()},
+            'host': {'gen_s': t_gen, 'h2d_s': t_up, 'nproc': os.cpu_count(), 'cpu': cpu_model(),
+                     'visible_gpus': ndev},
         }
         if not a.no_cpu_baseline and d.world == 1:
             line['cpu_baseline'] = cpu_baseline(raw, sm, a.cpu_seconds)
