@@ -1,3 +1,4 @@
+# Tagger end-to-end bench with a cProfile of the caller thread, plus chunk-size variants.
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
