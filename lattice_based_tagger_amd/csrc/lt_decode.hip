@@ -9,26 +9,31 @@
 //   SimpleTrigramFeatureScore.score  score_funcs.py:137-144
 //   trigram_encoder        features/feature.py:76-121
 //
-// Two kernels:
-//  * lt_viterbi_k  -- beam_size 1.  A 16-lane group owns one sentence; the
-//    candidates of end position e are the contiguous node range
-//    [A_e, A_{e+1}) of the packed layout, lane l scores node A_e + l.  The
-//    next position's span start and candidate node fields are loaded while
-//    the current position is scored (software prefetch), so the only
-//    dependent memory round trip per position is the hash probe.  The
-//    winner lane writes the new frontier entry from its registers.
-//  * lt_beam_k<KT,G> -- beam_size 2..32.  Expansions enumerated in the
+// Kernels, chosen per beam size by launch_decode:
+//  * lt_viterbi_pk<W>  -- beam_size 1 (default W = 6).  W sentences share a
+//    wave in lockstep: the candidates of their current end positions are
+//    packed onto the 64 lanes by prefix sums, each lane scores one
+//    candidate, a segmented DPP argmax per sentence picks the winner
+//    (lowest generation index on ties), and the next position's node records
+//    are staged while the current one is probed.
+//  * lt_beam_hw<KT,G>  -- beam_size 2..8.  64/G sentences per wave in G-lane
+//    groups (G = 16 for k <= 3, 32 above); expansions enumerated in the
 //    reference's generation order (begin ascending, hypothesis rank,
-//    candidate order), each lane keeps its own top-k, k rounds of group
-//    argmax merge them.
-// Both: the frontier (beams of the last 9 end positions) lives in LDS as a
+//    candidate order), scored one per lane, ranked by counting within the
+//    group (Python's stable sort), the top k written to the ring.
+//  * lt_beam_pk<KT>    -- beam_size 9..32 (KT = 16, 32): one sentence per wave,
+//    the same enumeration and rank counting over several scoring rounds.
+//  * lt_viterbi_k / lt_beam_k -- the first versions (one 16-lane row per
+//    sentence; per-lane top-k merged by k argmax rounds), kept for A/B runs
+//    (LT_VITERBI=row16, LT_BEAM=v1).
+// All: the frontier (beams of the last 9 end positions) lives in LDS as a
 // ring whose entries cache the fields of the hypothesis' last two nodes;
-// trigram classes 4/5/6 arrive pre-resolved per node, classes 0,1,2,3,7,8 are
-// probed in an open-addressing table -- all probes of an expansion issued
-// together as buffer loads, an unneeded probe gets an out-of-range offset
-// (returns 0, touches no memory) instead of a branch.  Present coefficients
-// are summed in numpy's pairwise order; ties go to the lower
-// generation index (Python's stable sort).
+// trigram classes 4/5/6 arrive pre-resolved per node, class 3 (tag, tag)
+// comes from a dense LDS table where the kernel stages one, the other
+// classes are probed in a two-choice cuckoo table -- all probes of an expansion issued together as buffer loads, an
+// unneeded probe gets an out-of-range offset (returns 0, touches no memory)
+// instead of a branch.  Present coefficients are summed in numpy's pairwise
+// order.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <cstring>
