@@ -1562,14 +1562,15 @@ static bool beam_one_per_wave() {
 }
 
 // ---------------------------------------------------------------------------
-// beam_size 2..8, half waves: lanes 0-31 decode one sentence and lanes 32-63
-// another, in lockstep over end positions.  lt_beam_pk leaves about half of a
-// wave's lanes idle at k = 5 (about 27 expansions per position) and is
-// issue-bound; here each half scores its own sentence's expansions in rounds
-// of 32 lanes, so one instruction stream serves two sentences.  Everything
-// per sentence (span starts, expansion prefix, counts) lives in VGPRs that
-// are uniform within a half; top-k is lt_beam_pk's exact rank counting and
-// threshold pruning, per half.
+// beam_size 2..8, lane groups: the wave's G-lane groups (G = 32: two
+// sentences per wave; G = 16: four, used for k <= 3) decode one sentence each,
+// in lockstep over end positions.  lt_beam_pk leaves about half of a wave's
+// lanes idle at k = 5 (about 27 expansions per position) and is issue-bound;
+// here each group scores its own sentence's expansions in rounds of G lanes,
+// so one instruction stream serves 64/G sentences.  Everything per sentence
+// (span starts, expansion prefix, counts) lives in VGPRs that are uniform
+// within a group; top-k is lt_beam_pk's exact rank counting and threshold
+// pruning, per group.
 // ---------------------------------------------------------------------------
 template <int KT, int G, int WPB, bool NARROW>
 __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu((G == 16 && KT > 2) ? 2 : 3, 3)))
@@ -2036,7 +2037,7 @@ hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
 
 template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
-  // half waves (two sentences per wave, 32 lanes each) for k = 2..8;
+  // lane groups (beam_group_lanes: 16 lanes for k <= 3, 32 above) for k = 2..8;
   // LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
   if (!COUNT && !beam_v1() && !beam_one_per_wave() && kt <= 8) {
     if (beam_group_lanes(p.k) == 16) {

@@ -172,10 +172,10 @@ def test_decode_in_several_launches(gpu_decoder, monkeypatch):
 
 
 def test_half_wave_beam_kernel_multi_chunk(gpu_decoder):
-    """k=2 runs lt_beam_hw (two sentences per wave, 32 lanes each).  Very
+    """k=2 runs lt_beam_hw in 16-lane groups (four sentences per wave).  Very
     dense lattices (about 64 candidates per end position) give positions with
-    several 64-expansion chunks per half, so the threshold-pruning path and
-    the carried running top-k run in both halves at once, with ties; results
+    several expansion chunks per group, so the threshold-pruning path and the
+    carried running top-k run in every group at once, with ties; results
     bit-exact against the C restatement."""
     from lattice_based_tagger_amd import _capi as C
     assert C.load().lt_kernel_name(2) == b'lt_beam_hw'
