@@ -225,6 +225,10 @@ lt_status lt_ctx_destroy(lt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->d_counters);
+  for (lt_arena& a : c->spare) {
+    dfree(a.d);
+    if (a.h) (void)hipHostFree(a.h);
+  }
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -539,17 +543,83 @@ static lt_status validate(const lt_batch_desc* d) {
   return LT_OK;
 }
 
+static void arena_free(lt_arena& a) {
+  dfree(a.d);
+  if (a.h) (void)hipHostFree(a.h);
+  a = lt_arena{};
+}
+
+// Arenas up to this size are kept for reuse, at most SPARE_N per context.
+constexpr size_t SPARE_MAX = (size_t)1 << 30;
+constexpr size_t SPARE_N = 2;
+
+// An arena with at least (dn, hn) bytes: the smallest fitting spare, else a
+// new allocation (a spare that does not fit stays for a later batch).
+static hipError_t arena_take(lt_ctx* c, size_t dn, size_t hn, lt_arena& out) {
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    int best = -1;
+    for (int i = 0; i < (int)c->spare.size(); ++i)
+      if (c->spare[i].d_bytes >= dn && c->spare[i].h_bytes >= hn &&
+          (best < 0 || c->spare[i].d_bytes < c->spare[best].d_bytes))
+        best = i;
+    if (best >= 0) {
+      out = c->spare[best];
+      c->spare.erase(c->spare.begin() + best);
+      return hipSuccess;
+    }
+  }
+  out = lt_arena{};
+  hipError_t e = hipSuccess;
+  if (dn) e = hipMalloc((void**)&out.d, dn);
+  if (e == hipSuccess) out.d_bytes = dn;
+  if (e == hipSuccess && hn) e = hipHostMalloc((void**)&out.h, hn, hipHostMallocDefault);
+  if (e == hipSuccess) out.h_bytes = hn;
+  if (e != hipSuccess) arena_free(out);
+  return e;
+}
+
+static void arena_give(lt_ctx* c, lt_arena& a) {
+  if (!a.d && !a.h) return;
+  if (a.d_bytes <= SPARE_MAX) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->spare.size() < SPARE_N) {
+      c->spare.push_back(a);
+      a = lt_arena{};
+      return;
+    }
+  }
+  arena_free(a);
+}
+
 static void batch_free(lt_batch* b) {
   if (!b) return;
-  void* dev[] = {b->d_order, b->d_sent_n, b->d_span_start, b->d_node_off, b->d_span_off,
-                 b->d_bp_off, b->d_cum_n, b->d_nodes, b->d_post, b->d_bp, b->d_count,
-                 b->d_len, b->d_codes, b->d_score, b->d_hot};
-  for (void* p : dev) dfree(p);
-  void* host[] = {b->h_count, b->h_len, b->h_codes, b->h_score};
-  for (void* p : host)
-    if (p) (void)hipHostFree(p);
+  dfree(b->d_hot);
+  arena_give(b->ctx, b->arena);
   delete b;
 }
+
+// Sub-buffers of an arena: 256 B aligned, nullptr for empty ones.
+struct Carve {
+  size_t d = 0, h = 0;
+  static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+  size_t dev(size_t bytes) {
+    const size_t o = d;
+    d += al(bytes);
+    return bytes ? o : SIZE_MAX;
+  }
+  size_t host(size_t bytes) {
+    const size_t o = h;
+    h += al(bytes);
+    return bytes ? o : SIZE_MAX;
+  }
+};
+extern "C++" {
+template <class T>
+static T* at(char* base, size_t off) {
+  return off == SIZE_MAX ? nullptr : reinterpret_cast<T*>(base + off);
+}
+}  // extern "C++"
 
 lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch** out) {
   if (!c || !d || !out) return fail(LT_EINVAL, "lt_batch_create: NULL argument");
@@ -593,17 +663,56 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   }
 
   hipStream_t stm = c->ustream;     // complete when this returns (synchronised below)
-  hipError_t e = hipSuccess;
-  auto up = [&](auto** dst, const auto* src, size_t count) {
-    if (e == hipSuccess) e = dalloc_copy(dst, src, count, stm);
+  const size_t nres = (size_t)S * max_k;
+  const size_t ncodes = (size_t)b->total_chars * max_k;
+  const size_t npost = (size_t)d->n_post * (size_t)d->n_nodes;
+  // the batch's buffers as offsets into one arena
+  Carve cv;
+  const size_t o_order = cv.dev((size_t)S * 4), o_sent_n = cv.dev((size_t)S * 4),
+               o_node_off = cv.dev(((size_t)S + 1) * 8), o_span_off = cv.dev(((size_t)S + 1) * 8),
+               o_bp_off = cv.dev(((size_t)S + 1) * 8), o_cum_n = cv.dev(((size_t)S + 1) * 8),
+               o_span_start = cv.dev((size_t)d->n_span * 4),
+               o_nodes = cv.dev((size_t)d->n_nodes * sizeof(NodeRec)), o_post = cv.dev(npost * 8),
+               o_bp = cv.dev((size_t)b->bp_entries * 4), o_count = cv.dev((size_t)S * 4),
+               o_len = cv.dev(nres * 4), o_score = cv.dev(nres * 8), o_codes = cv.dev(ncodes * 4);
+  const size_t h_count = cv.host((size_t)S * 4), h_len = cv.host(nres * 4), h_score = cv.host(nres * 8),
+               h_codes = cv.host(ncodes * 4);
+  hipError_t e = arena_take(c, cv.d, cv.h, b->arena);
+  if (e != hipSuccess) {
+    delete b;
+    return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "lt_batch_create: %s", hipGetErrorString(e));
+  }
+  char* D = b->arena.d;
+  char* H = b->arena.h;
+  b->d_order = at<int32_t>(D, o_order);
+  b->d_sent_n = at<int32_t>(D, o_sent_n);
+  b->d_node_off = at<int64_t>(D, o_node_off);
+  b->d_span_off = at<int64_t>(D, o_span_off);
+  b->d_bp_off = at<int64_t>(D, o_bp_off);
+  b->d_cum_n = at<int64_t>(D, o_cum_n);
+  b->d_span_start = at<int32_t>(D, o_span_start);
+  b->d_nodes = at<NodeRec>(D, o_nodes);
+  b->d_post = at<double>(D, o_post);
+  b->d_bp = at<uint32_t>(D, o_bp);
+  b->d_count = at<int32_t>(D, o_count);
+  b->d_len = at<int32_t>(D, o_len);
+  b->d_score = at<double>(D, o_score);
+  b->d_codes = at<int32_t>(D, o_codes);
+  b->h_count = at<int32_t>(H, h_count);
+  b->h_len = at<int32_t>(H, h_len);
+  b->h_score = at<double>(H, h_score);
+  b->h_codes = at<int32_t>(H, h_codes);
+  auto up = [&](auto* dst, const auto* src, size_t count) {
+    if (e == hipSuccess && count)
+      e = hipMemcpyAsync(dst, src, count * sizeof(*src), hipMemcpyHostToDevice, stm);
   };
-  up(&b->d_order, order.data(), (size_t)S);
-  up(&b->d_sent_n, d->sent_n, (size_t)S);
-  up(&b->d_node_off, d->sent_node_off, (size_t)S + 1);
-  up(&b->d_span_off, d->sent_span_off, (size_t)S + 1);
-  up(&b->d_bp_off, bp_off.data(), (size_t)S + 1);
-  up(&b->d_cum_n, cum_n.data(), (size_t)S + 1);
-  up(&b->d_span_start, d->span_start, (size_t)d->n_span);
+  up(b->d_order, order.data(), (size_t)S);
+  up(b->d_sent_n, d->sent_n, (size_t)S);
+  up(b->d_node_off, d->sent_node_off, (size_t)S + 1);
+  up(b->d_span_off, d->sent_span_off, (size_t)S + 1);
+  up(b->d_bp_off, bp_off.data(), (size_t)S + 1);
+  up(b->d_cum_n, cum_n.data(), (size_t)S + 1);
+  up(b->d_span_start, d->span_start, (size_t)d->n_span);
   // device node records: AoS, mask + each node's span length d-1 (bits 24-26)
   std::unique_ptr<NodeRec[]> recs(new (std::nothrow) NodeRec[(size_t)std::max<int64_t>(d->n_nodes, 1)]);
   if (!recs) {
@@ -633,7 +742,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       }
     }
   }, 256);
-  up(&b->d_nodes, recs.get(), (size_t)d->n_nodes);
+  up(b->d_nodes, recs.get(), (size_t)d->n_nodes);
   if (hot_enabled()) {
     const uint32_t lim = 1u << NARROW_ID_BITS;
     b->f_word.assign(lim, 0u);
@@ -647,18 +756,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       if (mo < lim) ++b->f_morph[mo];
     }
   }
-  up(&b->d_post, d->node_post, (size_t)d->n_post * (size_t)d->n_nodes);
-  const size_t nres = (size_t)S * max_k;
-  const size_t ncodes = (size_t)b->total_chars * max_k;
-  up(&b->d_bp, (const uint32_t*)nullptr, (size_t)b->bp_entries);
-  up(&b->d_count, (const int32_t*)nullptr, (size_t)S);
-  up(&b->d_len, (const int32_t*)nullptr, nres);
-  up(&b->d_score, (const double*)nullptr, nres);
-  up(&b->d_codes, (const int32_t*)nullptr, ncodes);
-  if (e == hipSuccess && S) e = hipHostMalloc((void**)&b->h_count, (size_t)S * 4, hipHostMallocDefault);
-  if (e == hipSuccess && nres) e = hipHostMalloc((void**)&b->h_len, nres * 4, hipHostMallocDefault);
-  if (e == hipSuccess && nres) e = hipHostMalloc((void**)&b->h_score, nres * 8, hipHostMallocDefault);
-  if (e == hipSuccess && ncodes) e = hipHostMalloc((void**)&b->h_codes, ncodes * 4, hipHostMallocDefault);
+  up(b->d_post, d->node_post, npost);
   if (e == hipSuccess) e = hipStreamSynchronize(stm);
   if (e != hipSuccess) {
     batch_free(b);

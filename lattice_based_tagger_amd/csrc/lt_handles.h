@@ -4,9 +4,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <vector>
 
 #include "lt_common.h"
+
+// One batch's device buffers (one hipMalloc) and pinned result buffers (one
+// hipHostMalloc), carved into the lt_batch pointers.  lt_batch_destroy hands
+// a small arena back to its context (lt_ctx::spare) for the next batch that
+// fits: a sentence-at-a-time caller (Tagger.tag) then allocates and frees
+// nothing per call (each hipFree / hipHostFree synchronises the device).
+struct lt_arena {
+  char* d = nullptr;
+  size_t d_bytes = 0;
+  char* h = nullptr;
+  size_t h_bytes = 0;
+};
 
 struct lt_ctx {
   int device = 0;
@@ -15,6 +28,8 @@ struct lt_ctx {
                                    // thread does not queue behind the decodes)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   unsigned long long* d_counters = nullptr;
+  std::mutex mu;                   // spare (batches are created and destroyed on several threads)
+  std::vector<lt_arena> spare;     // arenas of destroyed batches, kept for reuse
 };
 
 struct lt_batch {
@@ -39,4 +54,5 @@ struct lt_batch {
   std::vector<uint32_t> f_word, f_tag, f_morph;
   uint64_t hot_uid = 0;      // lt_model::uid the hot table was built for (0: none)
   lt::SlotN* d_hot = nullptr;
+  lt_arena arena;
 };

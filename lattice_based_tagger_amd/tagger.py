@@ -241,6 +241,20 @@ class Tagger:
             dbs = dec.upload(model, packed, k) if dec is not None and packed is not None else None
             return lat, packed, views, dbs
 
+        def finish(i, lat, packed, views, dbs):
+            if packed is None:
+                lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(chunks[i]))]
+                matures = beam_search_batch(lattices, self.score_funcs, beam_size=k, device=self.device)
+            else:
+                matures = decode_batch(packed, views, lat.chars, model, k, self.device,
+                                       best_only=True, uploaded=dbs)
+            return [m[0] for m in matures]
+
+        if len(chunks) == 1:                       # nothing to overlap (Tagger.tag): no worker threads
+            lat, packed, views = front(chunks[0], lat0)
+            dbs = dec.upload(model, packed, k) if dec is not None and packed is not None else None
+            return finish(0, lat, packed, views, dbs)
+
         out = []
         with ThreadPoolExecutor(max_workers=1) as builder, ThreadPoolExecutor(max_workers=1) as uploader:
             stages = deque()
@@ -255,14 +269,7 @@ class Tagger:
                 for i in range(len(chunks)):
                     lat, packed, views, dbs = stages.popleft().result()
                     feed(i + 2)
-                    if packed is None:
-                        lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(chunks[i]))]
-                        matures = beam_search_batch(lattices, self.score_funcs, beam_size=k,
-                                                    device=self.device)
-                    else:
-                        matures = decode_batch(packed, views, lat.chars, model, k, self.device,
-                                               best_only=True, uploaded=dbs)
-                    out += [m[0] for m in matures]
+                    out += finish(i, lat, packed, views, dbs)
             finally:
                 for f in stages:                   # an error: drop what is still in flight
                     f.cancel()
