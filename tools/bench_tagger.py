@@ -11,6 +11,7 @@ replicated to --sentences; the model is the golden 'base' set's
     python tools/bench_tagger.py [--sentences 65536] [--k 1] [--threads 0] [--reps 3]
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -85,7 +86,10 @@ def main():
             best = t
             n_words = lat.n_words
     api_times = []
-    for _ in range(a.api_reps):                   # steady state: allocator and pools warm after the first
+    out = None
+    for _ in range(a.api_reps):
+        out = None                                # the previous call's results are freed untimed
+        gc.collect()
         t0 = time.perf_counter()
         out = tagger.tag_batch(sents, beam_size=a.k)
         api_times.append(time.perf_counter() - t0)
