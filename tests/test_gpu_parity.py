@@ -186,3 +186,24 @@ def test_half_wave_beam_kernel_multi_chunk(gpu_decoder):
     assert np.array_equal(count, o[0]) and np.array_equal(length, o[1])
     assert np.array_equal(score.view(np.uint64), o[2].view(np.uint64))
     assert np.array_equal(codes, o[3])
+
+
+def test_recycled_batch_buffers(gpu_decoder):
+    """Batch buffers are recycled through the context (lt_batch_destroy keeps
+    small arenas): decoding batches of alternating sizes and beams -- a large
+    one after a small one reuses nothing, a small one after a large one runs
+    in the large one's arena with stale data around it -- gives each batch the
+    C restatement's results, bit for bit."""
+    ctx = gpu_decoder.ctx
+    small = _synthetic(40, seed=901, n_features=20_000)
+    large = _synthetic(600, seed=902, n_features=20_000)
+    ref = {}
+    for name, (packed, keys, coefs) in (('s', small), ('l', large)):
+        for k in (1, 5):
+            o = lt_oracle.decode(packed, keys, coefs, k, nthreads=16)
+            ref[name, k] = (o[0], o[1], o[2].view(np.uint64), o[3])
+    for name, k in [('l', 5), ('s', 1), ('l', 1), ('s', 5), ('s', 1), ('l', 5), ('s', 5)]:
+        packed, keys, coefs = small if name == 's' else large
+        count, length, score, codes = _gpu_decode(ctx, packed, keys, coefs, k)[0]
+        for x, y in zip((count, length, score.view(np.uint64), codes), ref[name, k]):
+            assert np.array_equal(x, y), (name, k)
