@@ -15,7 +15,11 @@
  * (outputs) during the call; the library never frees them.  Device memory is
  * owned by the handles.  Functions return lt_status (0 = OK, < 0 = error);
  * lt_last_error() returns a thread-local message for the last failure.
- * A handle is not re-entrant: use one lt_ctx per host thread.
+ * A handle is not re-entrant: one thread at a time per lt_ctx, except that
+ * lt_batch_create / lt_batch_destroy may run on another thread while that
+ * ctx decodes (uploads go to the ctx's own upload stream; the cache of
+ * recycled batch buffers is locked) -- a pipeline uploads batch i+1 while
+ * batch i decodes.
  */
 #ifndef LATTICE_DECODE_H
 #define LATTICE_DECODE_H
@@ -128,7 +132,10 @@ typedef struct {
 } lt_batch_desc;
 
 /* Copies the batch to the device (H2D) and allocates result buffers for
- * beams up to max_k.  Blocking. */
+ * beams up to max_k.  Blocking.  The batch's device buffers are one
+ * allocation and its pinned result buffers another; lt_batch_destroy keeps
+ * up to two such pairs (each up to 1 GiB) in the ctx for later batches that
+ * fit, so per-call decoding frees and allocates nothing. */
 lt_status lt_batch_create(lt_ctx* ctx, const lt_batch_desc* desc, int max_k, lt_batch** out);
 lt_status lt_batch_destroy(lt_batch* batch);
 /* Total path-code slots of the results for beam k: k * sum_s n_s. */
