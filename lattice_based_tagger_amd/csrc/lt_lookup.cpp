@@ -511,8 +511,23 @@ void run_chunk(const lt_lexicon& lx, const lt_text_desc& td, int32_t s0, int32_t
   Worker wk(lx, td.text);
   std::vector<WordRec> words, grouped;
   std::vector<int64_t> cnt;
+  std::string u8;                     // the sentence's text in UTF-8 ...
+  std::vector<uint32_t> u8pos;        // ... and each character's byte offset (+ the end)
   for (int32_t s = s0; s < s1; ++s) {
     const int64_t n = td.char_off[s + 1] - td.char_off[s];
+    // every surface is a substring of the sentence's text: encode it once
+    const int64_t t0 = td.eoj_off[td.sent_eoj[s]], t1 = td.eoj_off[td.sent_eoj[s + 1]];
+    u8.clear();
+    u8pos.clear();
+    for (int64_t x = t0; x < t1; ++x) {
+      u8pos.push_back((uint32_t)u8.size());
+      utf8_append(u8, td.text + x, 1);
+    }
+    u8pos.push_back((uint32_t)u8.size());
+    auto surface = [&](std::string& dst, const WordRec& w) {
+      const uint32_t a = u8pos[w.w_off - t0], z = u8pos[w.w_off - t0 + w.w_len];
+      dst.append(u8, a, z - a);
+    };
     words.clear();
     int32_t offset = 0;
     for (int64_t j = td.sent_eoj[s]; j < td.sent_eoj[s + 1]; ++j) {
@@ -535,9 +550,9 @@ void run_chunk(const lt_lexicon& lx, const lt_text_desc& td, int32_t s0, int32_t
     for (const WordRec& w : words) grouped[(size_t)cnt[(size_t)w.b]++] = w;
     ck.sent_n.push_back((int64_t)words.size());
     for (const WordRec& w : grouped) {
-      utf8_append(ck.wb, td.text + w.w_off, w.w_len);
+      surface(ck.wb, w);
       ck.woff.push_back((int64_t)ck.wb.size());
-      if (w.m0_off < 0) utf8_append(ck.mb, td.text + w.w_off, w.w_len);
+      if (w.m0_off < 0) surface(ck.mb, w);
       else utf8_append(ck.mb, wk.pool.data() + w.m0_off, (size_t)w.m0_len);
       ck.moff.push_back((int64_t)ck.mb.size());
       if (w.m1_off >= 0) utf8_append(ck.m1b, wk.pool.data() + w.m1_off, (size_t)w.m1_len);
