@@ -296,6 +296,15 @@ def _materialise_bulk_body(packed, objs, chars_list, k, T, count, length, score,
             flat[j] = Word(sub, sub, None, Unk, None, d, b, b + d, False)
     # the sentinels are immutable tuples: one BOS, one EOS per sentence length
     bos, eos = bos_word(), {}
+    if T == 1:                                          # best path only (Tagger.tag): one comprehension
+        nl = n.tolist()
+        for nch in set(nl):
+            eos[nch] = eos_word(nch)
+        L1 = L[:, 0]
+        ends = np.cumsum(L1)
+        return [[Sequence([bos] + flat[a:z] + [eos[nch]], sc if nch > 0 else 0, 0)] if c else []
+                for a, z, nch, c, sc in zip((ends - L1).tolist(), ends.tolist(), nl,
+                                            (np.minimum(count, 1) > 0).tolist(), score[:, 0].tolist())]
     out = []
     pos = 0
     cnt = np.minimum(count, T).tolist()
