@@ -1,3 +1,4 @@
+# Tagger.tag latency (one sentence per call) with a per-phase breakdown.
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
