@@ -2035,6 +2035,10 @@ hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+#ifndef HW_WPB
+#define HW_WPB 4                        // waves per block of lt_beam_hw
+#endif
+
 template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
   // lane groups (beam_group_lanes: 16 lanes for k <= 3, 32 above) for k = 2..8;
@@ -2042,16 +2046,16 @@ hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
   if (!COUNT && !beam_v1() && !beam_one_per_wave() && kt <= 8) {
     if (beam_group_lanes(p.k) == 16) {
       switch (kt) {
-        case 2: return launch_hw<2, 16, 4, NARROW>(p, st);
-        case 4: return launch_hw<4, 16, 4, NARROW>(p, st);
-        case 8: return launch_hw<8, 16, 4, NARROW>(p, st);
+        case 2: return launch_hw<2, 16, HW_WPB, NARROW>(p, st);
+        case 4: return launch_hw<4, 16, HW_WPB, NARROW>(p, st);
+        case 8: return launch_hw<8, 16, HW_WPB, NARROW>(p, st);
         default: break;
       }
     }
     switch (kt) {
-      case 2: return launch_hw<2, 32, 4, NARROW>(p, st);
-      case 4: return launch_hw<4, 32, 4, NARROW>(p, st);
-      case 8: return launch_hw<8, 32, 4, NARROW>(p, st);
+      case 2: return launch_hw<2, 32, HW_WPB, NARROW>(p, st);
+      case 4: return launch_hw<4, 32, HW_WPB, NARROW>(p, st);
+      case 8: return launch_hw<8, 32, HW_WPB, NARROW>(p, st);
       default: break;
     }
   }
