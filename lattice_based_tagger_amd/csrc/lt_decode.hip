@@ -2038,6 +2038,12 @@ hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
 #ifndef HW_WPB
 #define HW_WPB 4                        // waves per block of lt_beam_hw
 #endif
+#ifndef BP16_WPB
+#define BP16_WPB 2                      // waves per block of lt_beam_pk, k = 9..16
+#endif
+#ifndef BP32_WPB
+#define BP32_WPB 2                      // waves per block of lt_beam_pk, k = 17..32
+#endif
 
 template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
@@ -2064,8 +2070,8 @@ hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
       case 2: return launch_bp<2, 4, NARROW, COUNT>(p, st);
       case 4: return launch_bp<4, 4, NARROW, COUNT>(p, st);
       case 8: return launch_bp<8, 4, NARROW, COUNT>(p, st);
-      case 16: return launch_bp<16, 2, NARROW, COUNT>(p, st);
-      case 32: return launch_bp<32, 2, NARROW, COUNT>(p, st);
+      case 16: return launch_bp<16, BP16_WPB, NARROW, COUNT>(p, st);
+      case 32: return launch_bp<32, BP32_WPB, NARROW, COUNT>(p, st);
       default: return hipErrorInvalidValue;
     }
   }
