@@ -1,21 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X lattice decoder (BASELINE.json metric).
 
-One step = one decode of a 64K-sentence synthetic batch (BASELINE.json config
-3: 20 eojeols x 2-5 characters, full-dictionary lattice statistics, 1M-key
-trigram model, RegularizationScore + SimpleTrigramFeatureScore, beam k=1 =
-Viterbi) that is already resident in HBM: decode kernel (incl. backtrace),
-results written to HBM, stream sync.  Lattice build, packing and H2D happen
-before the timed region.  The PCIe-inclusive rate (results copied to pinned
-host memory every step) is measured separately and reported as
-``pcie_inclusive_sentences_per_s`` -- never as ``value``.
+One step = one decode of the batch that is already resident in HBM, with
+its results delivered to pinned host memory (kernel(s) +
+backtrace + D2H of results inside the timed region): decode kernel (incl.
+backtrace), results packed on the device (lt_results.hip) and their used
+bytes copied to the host on a copy stream -- step i's copy runs under step
+i+1's decode (two result slots per batch).  Lattice build, packing and H2D
+happen before the timed region.
+
+The default workload is BASELINE.json config 3: a 64K-sentence synthetic
+batch (20 eojeols x 2-5 characters, full-dictionary lattice statistics,
+1M-key trigram model, RegularizationScore + SimpleTrigramFeatureScore,
+beam k=1 = Viterbi).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--k 1] [--sentences 65536]
+                    [--scaling strong|weak]
 
-N > 1 is launched by torch.distributed.run (one process per GPU); each rank
-decodes its own 64K-sentence shard (weak scaling, no data-path collective),
-ranks are timed between barriers and the max over ranks is reported.
-Rank 0 prints one JSON line.
+N > 1 is launched by torch.distributed.run (one process per GPU).  Strong
+scaling (default, the north star's "64K batch at 1, 2, 4 and 8 GPUs"): every
+rank builds the same seeded batch and decodes one contiguous shard of it
+(``dist.shard_range`` on sum (n+1)*k); each step ends with one RCCL gather
+of every rank's packed results to rank 0 over xGMI and rank 0's D2H of all
+of them.  ``--sentences 1048576`` is config 4 (the 64K generated lattices
+in 16 seeded permutations).  ``--scaling weak``: each rank its own
+64K-sentence batch.  Ranks are timed between barriers, the max over ranks
+is reported; rank 0 checks the gathered results against a single-process
+decode of the batch and prints one JSON line.
 """
 
 import argparse
@@ -37,17 +48,23 @@ METRIC = 'sentences/sec Viterbi decode, 64K-sentence batch; achieved HBM GB/s vs
 HBM_PEAK_GBS = 8000.0
 
 
+BASE_SENTENCES = 65536         # lattices generated per seed (config 3); larger batches permute them
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--k', type=int, default=1, help='beam size (1 = Viterbi headline)')
-    ap.add_argument('--sentences', type=int, default=65536)
+    ap.add_argument('--sentences', type=int, default=65536,
+                    help='batch size (strong: whole batch; weak: per rank)')
+    ap.add_argument('--scaling', choices=('strong', 'weak'), default='strong')
     ap.add_argument('--features', type=int, default=1_000_000)
     ap.add_argument('--cpu-seconds', type=float, default=10.0,
                     help='budget of the pure-Python CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-check', action='store_true', help='skip the post-run result check')
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--gather', type=int, default=None,
                     help='1: gather every rank\'s results to rank 0 with RCCL inside each step '
@@ -121,21 +138,54 @@ def make_workload(n_sent, seed, n_features):
     return raw, lay, sm, packed, keys, coefs
 
 
-def reachable_dict_nodes(raw):
-    """Dictionary candidates on spans <= 8 inside the sentence (all generated ones)."""
-    return int(len(raw.word))
+def batch_order(total, base, seed):
+    """Sentence order of a `total`-sentence batch over `base` generated
+    lattices: identity when total <= base, else seeded permutations of the
+    base lattices back to back (config 4's 1M batch = 16 permutations of
+    the 64K lattices)."""
+    if total <= base:
+        return None
+    rng = np.random.default_rng(seed + 4242)
+    reps = -(-total // base)
+    return np.concatenate([rng.permutation(base) for _ in range(reps)])[:total].astype(np.int64)
 
 
-def algorithmic_bytes(raw, packed, tuples, length, k):
+def shard_of(packed, order, k, world, rank):
+    """Rank's contiguous shard [lo, hi) of the batch (balanced on (n+1)*k,
+    SURVEY §8(e)) and its PackedBatch."""
+    from lattice_based_tagger_amd.dist import shard_range
+    n = np.asarray(packed.sent_n, dtype=np.int64)
+    w = (n if order is None else n[order]) + 1
+    lo, hi = shard_range(w * k, world, rank)
+    if order is None:
+        piece = packed if (lo, hi) == (0, packed.n_sent) else packed.slice(lo, hi)
+    else:
+        piece = packed.take(order[lo:hi])
+    return lo, hi, piece
+
+
+def algorithmic_bytes(piece, n_dict, tuples, length, count, k):
     """B = 32*N + 8*(8n+1) + 4*8n + 24*P + 8*T*N + sum_matures (4*(L+1)+8),
-    summed over the batch (N dictionary nodes, n chars, P trigram feature tuples
-    of the reference algorithm, T = 1 node-local term, L words per mature)."""
-    n = packed.sent_n.astype(np.int64)
-    N = reachable_dict_nodes(raw)
+    summed over the launch's sentences (N dictionary nodes, n chars, P trigram
+    feature tuples of the reference algorithm, T = 1 node-local term, L words
+    per mature)."""
+    n = np.asarray(piece.sent_n, dtype=np.int64)
     T = 1
-    out = int(np.sum(4 * (length[length > 0] + 1) + 8)) if k else 0
-    out += int(np.sum(length == 0) * 0)
-    return 32 * N + int(np.sum(8 * (8 * n + 1) + 4 * 8 * n)) + 24 * tuples + 8 * T * N + out
+    valid = np.arange(length.shape[1])[None, :] < count[:, None]
+    out = int(np.sum(np.where(valid, 4 * (length.astype(np.int64) + 1) + 8, 0)))
+    return 32 * n_dict + int(np.sum(8 * (8 * n + 1) + 4 * 8 * n)) + 24 * tuples + 8 * T * n_dict + out
+
+
+def kernel_bytes(piece, probes, k):
+    """Bytes the decode kernel itself issues per launch (not the §8(d)
+    algorithm count): every node record once (48 B), the span starts and
+    per-sentence offsets, 32 B per cuckoo-table probe (both 16 B slots),
+    the backpointer and padded result writes."""
+    S = piece.n_sent
+    n = np.asarray(piece.sent_n, dtype=np.int64)
+    chars = int(n.sum())
+    return (48 * piece.n_nodes + 4 * int(len(piece.span_start)) + 36 * S + 32 * probes
+            + 4 * int(((n + 1) * k).sum()) + 4 * chars * k + 12 * S * k + 4 * S)
 
 
 def cpu_baseline(raw, sm, budget_s):
@@ -259,8 +309,18 @@ def main():
     a = parse()
     lib = _capi.load()          # liblt binds its HIP runtime before torch (gloo) is imported
     d = Dist(a.gpus)
+    strong = a.scaling == 'strong'
+    k = a.k
     t_gen = time.perf_counter()
-    raw, lay, sm, packed, keys, coefs = make_workload(a.sentences, a.seed + 1000 * d.rank, a.features)
+    seed = a.seed if strong else a.seed + 1000 * d.rank
+    base_n = min(a.sentences, BASE_SENTENCES)
+    raw, lay, sm, packed, keys, coefs = make_workload(base_n, seed, a.features)
+    order = batch_order(a.sentences, base_n, seed)
+    if strong:
+        lo, hi, piece = shard_of(packed, order, k, d.world, d.rank)
+    else:
+        lo, hi = 0, a.sentences
+        piece = packed if order is None else packed.take(order)
     t_gen = time.perf_counter() - t_gen
     host_cores = max(1, min(int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1)), 64))
     pool_baseline = None
@@ -275,9 +335,9 @@ def main():
     ctx = _capi.Context(d.local % ndev)
     dm = _capi.DeviceModel(ctx, keys, coefs)
     t_up = time.perf_counter()
-    db = _capi.DeviceBatch(ctx, packed, max_k=a.k)          # H2D, outside the timed region
+    db = _capi.DeviceBatch(ctx, piece, max_k=k)          # H2D, outside the timed region
     t_up = time.perf_counter() - t_up
-    expansions, tuples, probes = db.count_ops(dm, a.k)
+    expansions, tuples, probes = db.count_ops(dm, k)
 
     # result gather to rank 0 over RCCL/xGMI (the path's one exchange step)
     gather = d.world > 1 if a.gather is None else bool(a.gather)
@@ -286,7 +346,7 @@ def main():
         try:
             uid = d.broadcast_bytes(_capi.comm_unique_id() if d.rank == 0 else None)
             comm = _capi.Comm(ctx, d.world, d.rank, uid)
-            comm.prepare(db, a.k, root=0)
+            comm.prepare(db, k, root=0)
         except (_capi.LTError, OSError) as exc:      # reported in the JSON line, never silent
             gather_error = '%s: %s' % (type(exc).__name__, exc)
             print('bench.py: result gather disabled on rank %d: %s' % (d.rank, gather_error),
@@ -296,76 +356,74 @@ def main():
                 comm.close()
             comm = None
             gather_error = gather_error or 'failed on another rank'
+    root = d.rank == 0
 
     def step():
-        db.launch(dm, a.k)
+        db.launch(dm, k)
         if comm:
-            comm.launch(db)
+            comm.launch(db)            # pack into the send slot + ncclGather (own stream)
+            if root:
+                comm.fetch()           # every rank's used bytes -> pinned host (copy stream)
+        else:
+            db.fetch()                 # DMA of the results -> pinned host (copy stream)
+
+    def drain():
         ctx.sync()
+        if comm:
+            comm.sync()
+            ctx.sync()
 
     for _ in range(max(1, a.warmup)):
         step()
+    drain()
 
     d.barrier()
-    ctx.sync()
-    kern_ms, gather_ms = [], []
+    drain()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-        kern_ms.append(ctx.kernel_ms())
-    if comm:
-        comm.sync()
-        gather_ms.append(comm.gather_ms())
-    ctx.sync()
-    if comm:
-        comm.sync()
+    drain()
     t1 = time.perf_counter()
     d.barrier()
     elapsed = d.max(t1 - t0)
-    total_sent = d.sum(float(a.sentences * a.steps))
+    kern = ctx.kernel_ms_recent(a.steps)
+    gather_ms = comm.gather_ms() if comm else None
+    total_sent = float(a.sentences * a.steps) if strong else d.sum(float(a.sentences * a.steps))
 
-    # PCIe-inclusive rate (results to pinned host memory each step), untimed above
-    pcie_steps = max(3, a.steps // 4)
-    ctx.sync()
-    tp = time.perf_counter()
-    for _ in range(pcie_steps):
-        db.launch(dm, a.k)
-        db.fetch()
-        ctx.sync()
-    tp = time.perf_counter() - tp
-    pcie_rate = d.sum(float(a.sentences * pcie_steps)) / d.max(tp)
-
-    count, length, score, codes = db.results(a.k)
-    gather_info = {'error': gather_error} if gather_error else None
-    if comm:
-        # the last gather delivered every rank's results of the same batch
-        step()
-        db.fetch()
-        ctx.sync()
-        comm.sync()
-        count, length, score, codes = db.results(a.k)
-        if d.rank == 0:
-            comm.fetch()
-            ctx.sync()
-            g0 = comm.view(0)
-            for x, y in zip(g0, (count, length, score, codes)):
-                assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8)), \
-                    'gathered rank-0 block differs from the local results'
-            got = [comm.view(r) for r in range(d.world)]
-            assert all(int(g[0].shape[0]) == a.sentences and int((g[0] > 0).sum()) == a.sentences
-                       for g in got), 'gathered result blocks incomplete'
-        gather_info = {'collective': 'ncclGather x4 in one group (RCCL), root 0, on its own '
-                                     'stream: gather of step i overlaps decode of step i+1',
-                       'rccl': (lib.lt_comm_library() or b'?').decode(),
-                       'last_gather_ms': float(np.mean(gather_ms)) if gather_ms else None,
-                       'in_timed_region': True}
-    kernel = (lib.lt_kernel_name(a.k) or b'?').decode()
-    traffic = traffic_from_profiles(kernel, a.k, a.sentences, a.features, a.seed)
-    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
-    B = algorithmic_bytes(raw, packed, tuples, length, a.k)
+    # results of the timed region's last step, checked (untimed)
+    check = None
+    if comm and root:
+        got = [comm.view(r) for r in range(d.world)]
+    elif not comm:
+        got = [padded_as_packed(db.results(k), piece.sent_n, k)]
+    else:
+        got = None
+    mine = db.decode(dm, k)                                   # padded layout, this rank's shard
+    if got is not None:
+        mine_pk = got[0]
+        assert all(np.array_equal(x, y) for x, y in zip(mine_pk.padded(piece.sent_n), mine)), \
+            'packed results differ from the padded results of the same decode'
+    if root and got is not None and not a.no_check:
+        check = result_check(got, strong, d.world, comm is not None, packed, order, ctx, dm, k,
+                             a.sentences)
+    count, length = mine[0], mine[1]
+    kernel = (lib.lt_kernel_name(k) or b'?').decode()
+    traffic = traffic_from_profiles(kernel, k, piece.n_sent, a.features, a.seed) \
+        if (d.world == 1 or not strong) else None
+    avg_kernel_s = float(np.mean(kern)) / 1e3
+    nd = dict_nodes(raw, order, lo, hi)
+    B = algorithmic_bytes(piece, nd, tuples, length, count, k)
+    KB = kernel_bytes(piece, probes, k)
     achieved = B / avg_kernel_s / 1e9
+    al = lambda x: (x + 15) // 16 * 16                      # noqa: E731
+    if comm:
+        d2h = sum(32 + al(4 * g.n_sent) + al(4 * g.length.size) + al(8 * g.length.size) +
+                  al(4 * g.codes.size) for g in got) if got is not None else None
+    else:
+        d2h = 4 * piece.n_sent * (1 + 3 * k) + 4 * int(np.sum(piece.sent_n)) * k
 
-    if d.rank == 0:
+    if root:
+        wl = ('config3' if a.sentences == 65536 else 'config4' if a.sentences == 1048576 else 'custom')
         line = {
             'metric': METRIC,
             'value': total_sent / elapsed,
@@ -375,20 +433,25 @@ def main():
             'warmup': a.warmup,
             'ms_per_step': elapsed / a.steps * 1e3,
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': a.scaling,
             'vs_baseline': None,
             'dtype': 'f64',
-            'data': 'synthetic (lattice_based_tagger_amd/synth.py, seed %d + 1000*rank)' % a.seed,
+            'data': 'synthetic (lattice_based_tagger_amd/synth.py, seed %d%s)%s' % (
+                a.seed, '' if strong else ' + 1000*rank',
+                '' if order is None else '; %d generated lattices in seeded permutations' % base_n),
             'config': {
-                'workload': 'config3: %d synthetic sentences/GPU, 20 eojeols x 2-5 chars, '
+                'workload': '%s: %d synthetic sentences%s, 20 eojeols x 2-5 chars, '
                             'full-dictionary lattice stats, %d-key trigram model, '
-                            'Regularization+SimpleTrigram scorers, beam k=%d, max_len 8'
-                            % (a.sentences, a.features, a.k),
-                'sentences_per_gpu': a.sentences,
-                'beam': a.k,
+                            'Regularization+SimpleTrigram scorers, beam k=%d, max_len 8; '
+                            'step = decode + result D2H%s'
+                            % (wl, a.sentences, ' split over %d GPUs' % d.world if strong else ' per GPU',
+                               a.features, k, ' + RCCL gather to rank 0' if comm else ''),
+                'sentences': a.sentences if strong else a.sentences * d.world,
+                'sentences_rank0': piece.n_sent,
+                'beam': k,
                 'max_len': 8,
-                'chars_per_sentence': float(packed.sent_n.mean()),
-                'dict_nodes_per_sentence': reachable_dict_nodes(raw) / a.sentences,
+                'chars_per_sentence': float(np.mean(piece.sent_n)),
+                'dict_nodes_per_sentence': nd / max(piece.n_sent, 1),
                 'parallelism': 'dp%d' % d.world,
             },
             'roofline': {
@@ -402,19 +465,31 @@ def main():
                 'traffic_source': traffic[1] if traffic else None,
                 'kernel': kernel,
                 'algorithmic_bytes_per_launch': B,
+                'kernel_bytes_per_launch': KB,
+                'kernel_bytes_frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                 'avg_kernel_ms': avg_kernel_s * 1e3,
+                'launch': 'rank 0 shard' if d.world > 1 else 'whole batch',
             },
             'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                                'table_probes': probes},
-            'kernel_only_sentences_per_s': a.sentences / avg_kernel_s,
-            'pcie_inclusive_sentences_per_s': pcie_rate,
-            'gather': gather_info,
+            'kernel_only_sentences_per_s': piece.n_sent / avg_kernel_s,
+            'd2h': {'bytes_per_step': d2h, 'in_timed_region': True,
+                    'how': ('rank 0: every rank\'s packed results (gathered slabs), used bytes to '
+                            'pinned host memory on a copy stream' if comm else
+                            'padded results by DMA to pinned host memory on a copy stream') +
+                           ', under the next decode'},
+            'gather': ({'error': gather_error} if gather_error else
+                       {'collective': 'one ncclGather of packed result slabs (RCCL), root 0, on its '
+                                      'own stream: gather of step i overlaps decode of step i+1',
+                        'rccl': (lib.lt_comm_library() or b'?').decode(),
+                        'last_gather_ms': gather_ms, 'in_timed_region': True} if comm else None),
+            'check': check,
             'host': {'gen_s': t_gen, 'h2d_s': t_up, 'nproc': os.cpu_count(), 'cpu': cpu_model(),
                      'visible_gpus': ndev},
         }
         if not a.no_cpu_baseline and d.world == 1:
             line['cpu_baseline'] = cpu_baseline(raw, sm, a.cpu_seconds)
-            line['cpu_baseline_c'] = cpu_baseline_c(packed, keys, coefs, a.k, a.cpu_seconds / 2)
+            line['cpu_baseline_c'] = cpu_baseline_c(packed, keys, coefs, k, a.cpu_seconds / 2)
             line['cpu_baseline_pool'] = pool_baseline
         else:
             line['cpu_baseline'] = None
@@ -425,6 +500,70 @@ def main():
     dm.close()
     ctx.close()
     d.close()
+
+
+def padded_as_packed(res, sent_n, k):
+    """PackedResults of padded results (count, length, score, codes)."""
+    count, length, score, codes = res
+    n = np.asarray(sent_n, dtype=np.int64)
+    cum = np.zeros(len(n) + 1, dtype=np.int64)
+    np.cumsum(n, out=cum[1:])
+    out = _capi.PackedResults.__new__(_capi.PackedResults)
+    out.k = k
+    t = np.arange(k)[None, :]
+    valid = t < count[:, None]
+    out.count, out.length = count, np.where(valid, length, 0).astype(np.int32)
+    out.score = np.where(valid, score, 0.0)
+    L = out.length.ravel().astype(np.int64)
+    out.off = np.zeros(L.size + 1, dtype=np.int64)
+    np.cumsum(L, out=out.off[1:])
+    e = np.repeat(np.arange(L.size, dtype=np.int64), L)
+    j = np.arange(int(L.sum()), dtype=np.int64) - out.off[e]
+    out.codes = codes[k * cum[e // k] + (e % k) * n[e // k] + j]
+    return out
+
+
+def dict_nodes(raw, order, lo, hi):
+    """Dictionary nodes of the batch's sentences [lo, hi)."""
+    per = np.bincount(raw.char_sent[raw.node_char], minlength=raw.S).astype(np.int64)
+    return int(per[lo:hi].sum() if order is None else per[order[lo:hi]].sum())
+
+
+def result_check(got, strong, world, gathered, packed, order, ctx, dm, k, total):
+    """Rank 0: the results delivered to the host by the timed region's last
+    step, against a single-process decode of the (base) batch on this GPU."""
+    ref_db = _capi.DeviceBatch(ctx, packed, max_k=k)
+    ref = ref_db.decode_packed(dm, k)
+    ref_db.close()
+    if strong:
+        from lattice_based_tagger_amd.beam import concat_results
+        whole = concat_results(got)
+        idx = np.arange(packed.n_sent) if order is None else order
+        assert whole.n_sent == total, 'gathered %d of %d sentences' % (whole.n_sent, total)
+        exp_count = ref.count[idx]
+        exp_len = ref.length[idx]
+        exp_score = ref.score[idx]
+        L = ref.length.ravel().astype(np.int64)
+        sel = (idx[:, None] * k + np.arange(k)[None, :]).ravel()
+        seg = np.repeat(sel, L[sel])
+        first = np.repeat(np.cumsum(L[sel]) - L[sel], L[sel])
+        within = np.arange(int(L[sel].sum())) - first
+        exp_codes = ref.codes[ref.off[seg] + within]
+        ok = (np.array_equal(whole.count, exp_count) and np.array_equal(whole.length, exp_len) and
+              np.array_equal(whole.score.view(np.uint64), exp_score.view(np.uint64)) and
+              np.array_equal(whole.codes, exp_codes))
+        assert ok, 'reassembled results differ from the single-process decode'
+        return {'what': 'all %d sentences from %d rank(s)%s equal a single-process decode of the '
+                        'batch byte for byte' % (total, world, ' (RCCL gather)' if gathered else ''),
+                'ok': True}
+    g0 = got[0]
+    ok = all(np.array_equal(x.view(np.uint8), y.view(np.uint8))
+             for x, y in zip((g0.count, g0.length, g0.score, g0.codes),
+                             (ref.count, ref.length, ref.score, ref.codes)))
+    assert ok, 'rank-0 results differ from its single-process decode'
+    assert all(g.n_sent == packed.n_sent for g in got), 'gathered result blocks incomplete'
+    return {'what': 'rank 0 results equal its single-process decode; %d complete blocks' % len(got),
+            'ok': True}
 
 
 if __name__ == '__main__':

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 1
+#define LT_ABI_VERSION 2   /* 2: compact results (slabs), gathers of slabs */
 #define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
 #define LT_MAX_BEAM 32     /* largest beam_size compiled in */
 
@@ -54,9 +54,10 @@ const char* lt_last_error(void);
 /* Number of visible HIP devices (0 when no GPU). */
 int lt_device_count(void);
 
-/* ---- context: one device + one HIP stream ------------------------------- */
+/* ---- context: one device, a decode stream, a copy stream ---------------- */
 lt_status lt_ctx_create(int device, lt_ctx** out);
 lt_status lt_ctx_destroy(lt_ctx* ctx);
+/* Waits for everything queued on the ctx (decodes and result copies). */
 lt_status lt_sync(lt_ctx* ctx);
 
 /* ---- model: the lowered scorer composite ---------------------------------
@@ -150,6 +151,9 @@ lt_status lt_decode_launch(lt_ctx* ctx, const lt_model* model, lt_batch* batch, 
 /* Device time of the last decode kernel (HIP events on the ctx stream), ms.
  * Valid after lt_sync. */
 lt_status lt_last_kernel_ms(lt_ctx* ctx, float* ms);
+/* Device times of the ctx's last min(n, 64) decode kernels, oldest first;
+ * *got receives how many were written.  Valid after lt_sync. */
+lt_status lt_kernel_ms_recent(lt_ctx* ctx, int n, float* ms, int* got);
 /* Name of the HIP kernel lt_decode_launch runs for beam k (profiling:
  * matches the rocprofv3 kernel name prefix); NULL for an unsupported k. */
 const char* lt_kernel_name(int k);
@@ -168,11 +172,43 @@ typedef struct {
   int32_t* codes;    /* [lt_batch_code_slots(batch, k)] */
 } lt_result;
 
-/* D2H of the last decode's results into library-owned pinned buffers
- * (async on the ctx stream; complete after lt_sync). */
+/* D2H of the last decode's results into library-owned pinned buffers.
+ * Asynchronous: the copies run on the ctx's copy stream once the decode
+ * stream has produced the results, so they overlap the next decode (a batch
+ * keeps two device result slots and decodes alternate between them; a
+ * decode reusing a slot whose copy is still queued waits for it on the
+ * device).  Complete after lt_sync; the pinned buffers are overwritten by
+ * the next fetch of the batch. */
 lt_status lt_result_fetch(lt_ctx* ctx, lt_batch* batch);
 /* Pointers to the pinned result buffers (valid until the next decode). */
 lt_status lt_result_view(lt_batch* batch, lt_result* view);
+/* ---- compact results ------------------------------------------------------
+ * A path holds about 1/2.5 of its sentence's code slots, so results cross
+ * PCIe (and xGMI, lt_gather_*) as a *slab*: a 32 B header {int32 n_sent,
+ * int32 k, int64 n_codes, int64 bytes, int64 0}, then 16 B aligned sections
+ * count int32[n_sent], length int32[n_sent*k], score f64[n_sent*k] (entries
+ * t >= count[s] are 0) and codes int32[n_codes] -- the length[s*k+t] codes of
+ * every mature t < count[s], sentence-major, best mature first.  The slab is
+ * built by kernels on the device and only its used bytes are copied (the
+ * size is read on the device; the host never waits for it). */
+typedef struct {
+  int32_t n_sent;
+  int32_t k;
+  int64_t n_codes;
+  const int32_t* count;    /* [n_sent] */
+  const int32_t* length;   /* [n_sent * k] */
+  const double* score;     /* [n_sent * k] */
+  const int32_t* codes;    /* [n_codes] */
+} lt_packed_view;
+/* As lt_result_fetch, for the slab: packing on the decode stream, the copy
+ * of the used bytes into the batch's pinned slab on the copy stream (under
+ * the next decode).  Complete after lt_sync; overwritten by the next fetch. */
+lt_status lt_result_fetch_packed(lt_ctx* ctx, lt_batch* batch);
+/* View of the batch's pinned slab (after lt_result_fetch_packed + lt_sync). */
+lt_status lt_result_view_packed(lt_batch* batch, lt_packed_view* view);
+/* View of any slab in host memory of `bytes` bytes (checks the header). */
+lt_status lt_slab_parse(const void* slab, uint64_t bytes, lt_packed_view* view);
+
 /* Blocking convenience: launch + fetch + sync + copy into caller buffers. */
 lt_status lt_decode(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k, lt_result* out);
 
@@ -203,23 +239,23 @@ lt_status lt_comm_create(lt_ctx* ctx, int nranks, int rank, const uint8_t id[LT_
                          lt_comm** out);
 lt_status lt_comm_destroy(lt_comm* comm);
 /* Agree on every rank's result sizes for beam k (<= the batch's max_k) and
- * allocate two padded send slots (and, on the root, two receive slots).
- * Blocking. */
+ * allocate two send slots (and, on the root, two receive slots of nranks
+ * slabs and one pinned mirror).  Blocking. */
 lt_status lt_gather_prepare(lt_comm* comm, lt_batch* batch, int k, int root);
-/* Gather the last decode's results (beam k of the prepare) to the root:
- * a device copy into the next send slot on the ctx stream, then one RCCL
- * group of four ncclGather calls (count, length, score, codes) on the
+/* Gather the last decode's results (beam k of the prepare) to the root: the
+ * results are packed into the next send slot on the ctx stream (a slab, see
+ * "compact results"), then one ncclGather of the slabs runs on the
  * communicator's own stream -- so the next decode on the ctx stream overlaps
  * this gather.  Complete after lt_gather_sync. */
 lt_status lt_gather_launch(lt_comm* comm, lt_batch* batch);
 /* Wait for this rank's outstanding gathers (local, not collective). */
 lt_status lt_gather_sync(lt_comm* comm);
-/* Root only: D2H of the last gathered block into pinned host buffers (async
- * on the ctx stream, after the gather; complete after lt_sync). */
+/* Root only: copy the used bytes of every rank's slab of the last gather
+ * into pinned host memory (on the ctx's copy stream, after the gather;
+ * complete after lt_sync). */
 lt_status lt_gather_fetch(lt_comm* comm);
-/* Root only: rank r's results in the lt_result layout for beam k (host
- * pointers valid until the next fetch), its sentence count and code slots. */
-lt_status lt_gather_view(lt_comm* comm, int r, lt_result* view, int32_t* n_sent, int64_t* code_slots);
+/* Root only: rank r's results (host pointers valid until the next fetch). */
+lt_status lt_gather_view(lt_comm* comm, int r, lt_packed_view* view);
 /* Device time of the last lt_gather_launch (HIP events around the RCCL
  * group on the communicator stream), ms.  Valid after lt_gather_sync. */
 lt_status lt_last_gather_ms(lt_comm* comm, float* ms);

@@ -13,6 +13,7 @@ import numpy as np
 from ._build import LIB
 
 LT_OK = 0
+ABI_VERSION = 2           # include/lattice_decode.h LT_ABI_VERSION
 LT_MAX_BEAM = 32
 LT_EUNSUPPORTED = -4
 _STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED', -5: 'LT_ERCCL'}
@@ -20,8 +21,10 @@ _STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED
 EXPORTED_SYMBOLS = (
     'lt_abi_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
     'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
-    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms', 'lt_kernel_name',
+    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms',
+    'lt_kernel_ms_recent', 'lt_kernel_name',
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
+    'lt_result_fetch_packed', 'lt_result_view_packed', 'lt_slab_parse',
     'lt_image_build', 'lt_image_view', 'lt_image_destroy', 'lt_model_create_from_image',
     'lt_evaluate',
     'lt_comm_library', 'lt_comm_unique_id', 'lt_comm_create', 'lt_comm_destroy', 'lt_gather_prepare',
@@ -55,6 +58,56 @@ class Result(C.Structure):
                 ('score', C.POINTER(C.c_double)), ('codes', C.POINTER(C.c_int32))]
 
 
+class PackedView(C.Structure):
+    _fields_ = [('n_sent', C.c_int32), ('k', C.c_int32), ('n_codes', C.c_int64),
+                ('count', C.POINTER(C.c_int32)), ('length', C.POINTER(C.c_int32)),
+                ('score', C.POINTER(C.c_double)), ('codes', C.POINTER(C.c_int32))]
+
+
+def _arr(p, n, dt):
+    if n == 0:
+        return np.zeros(0, dtype=dt)
+    return np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+
+class PackedResults:
+    """Compact results of one decode (a slab, lattice_decode.h "compact
+    results"): ``count`` [S], ``length`` / ``score`` [S, k] (0 past count),
+    ``codes`` the paths' node codes back to back, sentence-major, best
+    mature first; ``off`` [S*k + 1] where mature (s, t) starts in ``codes``."""
+
+    def __init__(self, v):
+        S, k = int(v.n_sent), int(v.k)
+        self.k = k
+        self.count = _arr(v.count, S, np.int32)
+        self.length = _arr(v.length, S * k, np.int32).reshape(S, k)
+        self.score = _arr(v.score, S * k, np.float64).reshape(S, k)
+        self.codes = _arr(v.codes, int(v.n_codes), np.int32)
+        self.off = np.zeros(S * k + 1, dtype=np.int64)
+        np.cumsum(self.length.ravel(), out=self.off[1:])
+
+    @property
+    def n_sent(self):
+        return int(self.count.shape[0])
+
+    def padded(self, sent_n):
+        """(count, length, score, codes) in the padded layout of
+        ``lt_result`` (codes of mature t of sentence s at k*cum_n[s] + t*n_s,
+        -1 past the path)."""
+        k = self.k
+        n = np.asarray(sent_n, dtype=np.int64)
+        cum = np.zeros(len(n) + 1, dtype=np.int64)
+        np.cumsum(n, out=cum[1:])
+        codes = np.full(int(cum[-1]) * k, -1, dtype=np.int32)
+        L = self.length.ravel().astype(np.int64)
+        if L.sum():
+            e = np.repeat(np.arange(L.size, dtype=np.int64), L)
+            s, t = e // k, e % k
+            j = np.arange(int(L.sum()), dtype=np.int64) - self.off[e]
+            codes[k * cum[s] + t * n[s] + j] = self.codes
+        return self.count.copy(), self.length.copy(), self.score.copy(), codes
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -86,6 +139,7 @@ def load(path=None):
             'lt_batch_code_slots': (i64, [vp, C.c_int]),
             'lt_decode_launch': (i32, [vp, vp, vp, C.c_int]),
             'lt_last_kernel_ms': (i32, [vp, C.POINTER(C.c_float)]),
+            'lt_kernel_ms_recent': (i32, [vp, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
             'lt_kernel_name': (C.c_char_p, [C.c_int]),
             'lt_image_build': (i32, [vp, C.POINTER(vp)]),
             'lt_image_view': (i32, [vp, vp]),
@@ -94,6 +148,9 @@ def load(path=None):
             'lt_evaluate': (i32, [vp, vp, vp, vp]),
             'lt_result_fetch': (i32, [vp, vp]),
             'lt_result_view': (i32, [vp, C.POINTER(Result)]),
+            'lt_result_fetch_packed': (i32, [vp, vp]),
+            'lt_result_view_packed': (i32, [vp, C.POINTER(PackedView)]),
+            'lt_slab_parse': (i32, [vp, C.c_uint64, C.POINTER(PackedView)]),
             'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),
             'lt_count_ops': (i32, [vp, vp, vp, C.c_int, C.POINTER(i64), C.POINTER(i64),
                                    C.POINTER(i64)]),
@@ -105,14 +162,16 @@ def load(path=None):
             'lt_gather_launch': (i32, [vp, vp]),
             'lt_gather_sync': (i32, [vp]),
             'lt_gather_fetch': (i32, [vp]),
-            'lt_gather_view': (i32, [vp, C.c_int, C.POINTER(Result), C.POINTER(i32),
-                                     C.POINTER(i64)]),
+            'lt_gather_view': (i32, [vp, C.c_int, C.POINTER(PackedView)]),
             'lt_last_gather_ms': (i32, [vp, C.POINTER(C.c_float)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.lt_abi_version() != ABI_VERSION:
+            raise RuntimeError('%s has ABI %d, this package needs %d (rebuild it)'
+                               % (path, lib.lt_abi_version(), ABI_VERSION))
         # Calls that only queue work or copy a few bytes, bound a second time
         # through PyDLL (the GIL stays held): a CDLL call releases the GIL
         # and must win it back from whichever pipeline thread runs Python --
@@ -128,7 +187,8 @@ def load(path=None):
 
 
 # lt_* entry points that return in microseconds (see load)
-HELD_CALLS = ('lt_decode_launch', 'lt_result_fetch', 'lt_result_view')
+HELD_CALLS = ('lt_decode_launch', 'lt_result_fetch', 'lt_result_view', 'lt_result_fetch_packed',
+              'lt_result_view_packed')
 
 
 def check(status):
@@ -159,6 +219,14 @@ class Context:
         v = C.c_float()
         check(self._lib.lt_last_kernel_ms(self.handle, C.byref(v)))
         return float(v.value)
+
+    def kernel_ms_recent(self, n):
+        """Device times (ms) of the last min(n, 64) decode kernels, oldest
+        first (after sync)."""
+        buf = (C.c_float * max(int(n), 1))()
+        got = C.c_int()
+        check(self._lib.lt_kernel_ms_recent(self.handle, int(n), buf, C.byref(got)))
+        return [float(buf[i]) for i in range(got.value)]
 
     def close(self):
         if self.handle:
@@ -309,11 +377,26 @@ class DeviceBatch:
         return (arr(v.count, S, np.int32), arr(v.length, S * k, np.int32).reshape(S, k),
                 arr(v.score, S * k, np.float64).reshape(S, k), arr(v.codes, nc, np.int32))
 
+    def fetch_packed(self):
+        check(self.ctx._lib.held.lt_result_fetch_packed(self.ctx.handle, self.handle))
+
+    def results_packed(self):
+        """PackedResults of the last fetch_packed (after sync)."""
+        v = PackedView()
+        check(self.ctx._lib.held.lt_result_view_packed(self.handle, C.byref(v)))
+        return PackedResults(v)
+
     def decode(self, model, k):
         self.launch(model, k)
         self.fetch()
         self.ctx.sync()
         return self.results(k)
+
+    def decode_packed(self, model, k):
+        self.launch(model, k)
+        self.fetch_packed()
+        self.ctx.sync()
+        return self.results_packed()
 
     def count_ops(self, model, k):
         x, p, q = C.c_int64(), C.c_int64(), C.c_int64()
@@ -374,19 +457,10 @@ class Comm:
         return float(v.value)
 
     def view(self, r):
-        """Root, after fetch + sync: numpy copies of rank r's (count, length,
-        score, codes), shaped as ``DeviceBatch.results``."""
-        v = Result()
-        S, slots = C.c_int32(), C.c_int64()
-        check(self.ctx._lib.lt_gather_view(self.handle, int(r), C.byref(v), C.byref(S), C.byref(slots)))
-        S, nc, k = S.value, slots.value, self.k
-
-        def arr(p, n, dt):
-            if n == 0:
-                return np.zeros(0, dtype=dt)
-            return np.ctypeslib.as_array(p, shape=(n,)).copy()
-        return (arr(v.count, S, np.int32), arr(v.length, S * k, np.int32).reshape(S, k),
-                arr(v.score, S * k, np.float64).reshape(S, k), arr(v.codes, nc, np.int32))
+        """Root, after fetch + sync: rank r's PackedResults."""
+        v = PackedView()
+        check(self.ctx._lib.lt_gather_view(self.handle, int(r), C.byref(v)))
+        return PackedResults(v)
 
     def close(self):
         if self.handle:

@@ -13,9 +13,9 @@ high-throughput entry point.
 """
 
 import gc
-import weakref
-
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -108,42 +108,54 @@ def invalidate_model_cache():
 
 
 class Decoder:
-    """A device context plus the device-resident models it has seen."""
+    """A device context plus the device-resident models it has seen.
+
+    ``Decoder.get(device, slot)``: one per (device ordinal, slot); several
+    slots on one device are independent contexts (streams, buffers), which
+    is how a multi-device decode is exercised on a one-GPU machine."""
 
     _instances = {}
+    _lock = threading.Lock()
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, slot=0):
         self.ctx = _capi.Context(device)
         self.device = device
+        self.key = (int(device), int(slot))
 
     @classmethod
-    def get(cls, device=0):
-        dec = cls._instances.get(device)
-        if dec is None:
-            dec = cls._instances[device] = cls(device)
+    def get(cls, device=0, slot=0):
+        key = (int(device), int(slot))
+        with cls._lock:
+            dec = cls._instances.get(key)
+            if dec is None:
+                dec = cls._instances[key] = cls(device, slot)
         return dec
 
     def device_model(self, model):
-        dm = model._device_models.get(self.device)
+        dm = model._device_models.get(self.key)
         if dm is None:
-            if getattr(model, 'image', None) is not None:      # model pack: no table build
-                dm = _capi.DeviceModel.from_image(self.ctx, model.image)
+            image = getattr(model, 'image', None)           # model pack: no table build
+            if image is None and len(model.keys) and len(model._device_models):
+                image = _built_image(model)                 # second device: build the table once
+            if image is not None:
+                dm = _capi.DeviceModel.from_image(self.ctx, image)
             else:
                 dm = _capi.DeviceModel(self.ctx, model.keys, model.coefs)
-            model._device_models[self.device] = dm
+            model._device_models[self.key] = dm
         return dm
 
     # node records per launch (lt_batch_create takes < 2^31 B of 48 B records)
     MAX_NODES = 40_000_000
 
     def upload(self, model, packed, k):
-        """Device batches of a PackedBatch, one per launch piece of at most
-        MAX_NODES nodes, as (s0, s1, DeviceBatch).  Safe from a worker thread
-        while this thread's caller decodes (lt_batch_create only queues
-        copies on the context's stream), so uploads overlap decodes."""
+        """Device batches of a PackedBatch, one per launch piece
+        (``PackedBatch.split``), as (s0, s1, DeviceBatch).  Safe from a worker
+        thread while this thread's caller decodes (lt_batch_create only
+        queues copies on the context's upload stream), so uploads overlap
+        decodes."""
         out = []
         try:
-            for s0, s1 in packed.split(self.MAX_NODES):
+            for s0, s1 in packed.split(self.MAX_NODES, k):
                 piece = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
                 out.append((s0, s1, _capi.DeviceBatch(self.ctx, piece, max_k=k)))
         except BaseException:
@@ -153,33 +165,114 @@ class Decoder:
         return out
 
     def decode_packed(self, model, packed, k, uploaded=None):
-        """Decode a PackedBatch (in launches of at most MAX_NODES nodes, or
-        the pieces ``upload`` made of it); returns (count, length, score,
-        codes, cum_n)."""
+        """Decode a PackedBatch (in launch pieces of ``PackedBatch.split``, or
+        the pieces ``upload`` made of it); returns the batch's
+        ``_capi.PackedResults``.  Pieces pipeline: piece i+1 is uploaded
+        while piece i decodes."""
         dm = self.device_model(model)
-        parts = []
-        pieces = uploaded if uploaded is not None else packed.split(self.MAX_NODES)
-        for piece in pieces:
-            if uploaded is not None:
-                db = piece[2]
-            else:
-                s0, s1 = piece
-                sub = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
-                db = _capi.DeviceBatch(self.ctx, sub, max_k=k)
-            try:
-                parts.append(db.decode(dm, k))
-            finally:
-                db.close()
         if uploaded is not None:
-            for _, _, db in uploaded:
-                db.close()
-        if len(parts) == 1:
-            count, length, score, codes = parts[0]
+            pieces = [db for _, _, db in uploaded]
+            todo = []
         else:
-            count, length, score, codes = (np.concatenate([p[i] for p in parts]) for i in range(4))
-        cum_n = np.zeros(packed.n_sent + 1, dtype=np.int64)
-        np.cumsum(packed.sent_n, out=cum_n[1:])
-        return count, length, score, codes, cum_n
+            pieces = []
+            todo = packed.split(self.MAX_NODES, k)
+
+        def up(rng):
+            s0, s1 = rng
+            sub = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
+            return _capi.DeviceBatch(self.ctx, sub, max_k=k)
+        parts = []
+        try:
+            if todo:
+                pieces.append(up(todo[0]))
+            i = 0
+            while i < len(pieces):
+                db = pieces[i]
+                db.launch(dm, k)
+                db.fetch_packed()
+                if i + 1 < len(todo):
+                    pieces.append(up(todo[i + 1]))      # H2D under this decode
+                self.ctx.sync()
+                parts.append(db.results_packed())
+                db.close()
+                i += 1
+        finally:
+            for db in pieces:
+                db.close()
+        return concat_results(parts)
+
+
+def concat_results(parts):
+    """One PackedResults of consecutive sentence ranges' PackedResults."""
+    if len(parts) == 1:
+        return parts[0]
+    out = _capi.PackedResults.__new__(_capi.PackedResults)
+    out.k = parts[0].k
+    for f in ('count', 'length', 'score', 'codes'):
+        setattr(out, f, np.concatenate([getattr(p, f) for p in parts]))
+    out.off = np.zeros(out.length.size + 1, dtype=np.int64)
+    np.cumsum(out.length.ravel(), out=out.off[1:])
+    return out
+
+
+def _built_image(model):
+    """The model's device image (cuckoo + dense class-3 tables), built once
+    on the host and uploaded to each further device without a rebuild."""
+    with Decoder._lock:
+        image = getattr(model, '_built_image', None)
+        if image is None:
+            im = _capi.ModelImage(model.keys, model.coefs)
+            image = im.arrays()
+            im.close()
+            model._built_image = image
+    return image
+
+
+def decoders_for(devices):
+    """Decoders of a device list; a repeated ordinal gets a context of its
+    own (slot 0, 1, ... in order of appearance)."""
+    seen = {}
+    out = []
+    for d in devices:
+        d = int(d)
+        out.append(Decoder.get(d, seen.get(d, 0)))
+        seen[d] = seen.get(d, 0) + 1
+    return out
+
+
+def device_list(device):
+    """``device`` as a tuple of ordinals (an int, or a sequence of them)."""
+    if isinstance(device, (list, tuple)):
+        if not device:
+            raise ValueError('devices must not be empty')
+        return tuple(int(d) for d in device)
+    return (int(device),)
+
+
+def decode_packed_devices(model, packed, k, devices):
+    """Decode a PackedBatch over several devices: sentences
+    are independent (beam.py:5-61 keeps no cross-sentence state), so the
+    batch is cut into contiguous shards of about equal work -- sum of
+    (n_s + 1) * k, ``dist.shard_range`` -- one per device, decoded
+    concurrently (one host thread per device; the library calls release the
+    GIL) and concatenated in input order.  Returns the batch's
+    ``_capi.PackedResults``."""
+    from concurrent.futures import ThreadPoolExecutor
+    from .dist import shard_range
+    decs = decoders_for(devices)
+    if len(decs) == 1:
+        return decs[0].decode_packed(model, packed, k)
+    w = (np.asarray(packed.sent_n, dtype=np.int64) + 1) * k
+    ranges = [shard_range(w, len(decs), r) for r in range(len(decs))]
+    for dec in decs:                               # tables built before the threads start
+        dec.device_model(model)
+
+    def run(r):
+        lo, hi = ranges[r]
+        return decs[r].decode_packed(model, packed.slice(lo, hi), k)
+    with ThreadPoolExecutor(max_workers=len(decs)) as ex:
+        parts = list(ex.map(run, range(len(decs))))
+    return concat_results(parts)
 
 
 def pack_lattices(sentences, model, max_len):
@@ -207,7 +300,10 @@ def _check_beam(beam_size):
 
 def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device=0):
     """Decode ``sentences`` = list of ``(bindex, chars)``; returns one list of
-    matures per sentence, each as ``beam_search`` returns it."""
+    matures per sentence, each as ``beam_search`` returns it.  ``device``: a
+    HIP device ordinal, or a sequence of them -- the batch is then split
+    into one contiguous shard per entry, decoded concurrently, results in
+    input order (``decode_packed_devices``)."""
     sentences = list(sentences)
     k = _check_beam(beam_size)
     model = lowered_model(score_functions)
@@ -215,32 +311,38 @@ def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device
     return decode_batch(packed, objs, [ch for _, ch in sentences], model, k, device)
 
 
-def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, uploaded=None):
+def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, uploaded=None,
+                 decoder=None):
     """Decode a packed batch and re-materialise the matures: ``objs[s][i]`` is
     the Word of sentence s's local node i, ``chars_list[s]`` its characters.
     ``best_only``: only the best mature of each sentence (what Tagger.tag
     returns, tagger.py:78).  ``uploaded``: ``Decoder.upload``'s device
-    batches of ``packed`` (closed here)."""
+    batches of ``packed`` (closed here; made by ``decoder``, default
+    ``Decoder.get(device)``)."""
     if k == 0:
         for _, _, db in uploaded or ():
             db.close()
         # beam_size=0 keeps no hypothesis past BOS (beam.py:85 slices to [])
         return [[Sequence([bos_word(), eos_word(0)], 0)] if len(ch) == 0 else []
                 for ch in chars_list]
-    count, length, score, codes, cum_n = Decoder.get(device).decode_packed(model, packed, k, uploaded)
+    devices = device_list(device)
+    if decoder is not None or uploaded is not None or len(devices) == 1:
+        dec = decoder if decoder is not None else Decoder.get(devices[0])
+        res = dec.decode_packed(model, packed, k, uploaded)
+    else:
+        res = decode_packed_devices(model, packed, k, devices)
     T = 1 if best_only else k
     if objs and hasattr(objs[0], 'src') and hasattr(objs[0], 'words'):      # native packer's views
-        return _materialise_bulk(packed, objs, chars_list, k, T, count, length, score, codes, cum_n)
+        return _materialise_bulk(packed, objs, chars_list, T, res)
+    count, length, score, codes, off = res.count, res.length, res.score, res.codes, res.off
     out = []
     for s, chars in enumerate(chars_list):
         n = len(chars)
         nodes = objs[s]
-        base = k * int(cum_n[s])
         matures = []
         for t in range(min(int(count[s]), T)):
-            L = int(length[s, t])
-            off = base + t * n
-            path = [nodes[0]] + [nodes[c] for c in codes[off:off + L]] + [eos_word(n)]
+            a = int(off[s * k + t])
+            path = [nodes[0]] + [nodes[c] for c in codes[a:a + int(length[s, t])]] + [eos_word(n)]
             sc = float(score[s, t]) if n > 0 else 0
             matures.append(Sequence(path, sc, 0))
         out.append(matures)
@@ -262,13 +364,14 @@ def _materialise_bulk(*args):
             gc.enable()
 
 
-def _materialise_bulk_body(packed, objs, chars_list, k, T, count, length, score, codes, cum_n):
+def _materialise_bulk_body(packed, objs, chars_list, T, res):
+    count, length, score, codes, k = res.count, res.length, res.score, res.codes, res.k
     S = len(chars_list)
     n = np.asarray(packed.sent_n, dtype=np.int64)
     t = np.arange(T, dtype=np.int64)
     valid = t[None, :] < np.minimum(count, T)[:, None]                     # S x T
     L = np.where(valid, length[:, :T], 0).astype(np.int64)
-    starts = k * cum_n[:-1, None] + t[None, :] * n[:, None]
+    starts = res.off[np.arange(S, dtype=np.int64)[:, None] * k + t[None, :]]
     Lf = L.ravel()
     total = int(Lf.sum())
     seg = np.repeat(np.arange(Lf.size), Lf)

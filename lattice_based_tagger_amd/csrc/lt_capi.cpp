@@ -103,10 +103,8 @@ struct lt_model {
   int64_t slots = 0;
   uint32_t seed = 0;
   int narrow = 0;          // 16 B SlotN (all ids < 2^20) or 32 B SlotW
-  std::vector<KeyRec> keys;  // host copy (narrow models): hot-table selection
   double* d_d3 = nullptr;    // dense class-3 table or NULL
   uint32_t d3mul = 0;
-  uint64_t uid = 0;          // unique per created model (hot-table cache key)
 };
 
 namespace {
@@ -209,8 +207,17 @@ lt_status lt_ctx_create(int device, lt_ctx** out) {
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) {
+    // the copy stream's kernels (slab -> host) must get CUs while a decode
+    // occupies them all: highest stream priority
+    int lo = 0, hi = 0;
+    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi);
+  }
+  for (int i = 0; i < lt_ctx::KRING && e == hipSuccess; ++i) {
+    e = hipEventCreate(&c->kev0[i]);
+    if (e == hipSuccess) e = hipEventCreate(&c->kev1[i]);
+  }
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     lt_ctx_destroy(c);
@@ -224,15 +231,19 @@ lt_status lt_ctx_destroy(lt_ctx* c) {
   if (!c) return LT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   dfree(c->d_counters);
   for (lt_arena& a : c->spare) {
     dfree(a.d);
     if (a.h) (void)hipHostFree(a.h);
   }
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (int i = 0; i < lt_ctx::KRING; ++i) {
+    if (c->kev0[i]) (void)hipEventDestroy(c->kev0[i]);
+    if (c->kev1[i]) (void)hipEventDestroy(c->kev1[i]);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->ustream) (void)hipStreamDestroy(c->ustream);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
   delete c;
   return LT_OK;
 }
@@ -241,6 +252,7 @@ lt_status lt_sync(lt_ctx* c) {
   if (!c) return fail(LT_EINVAL, "lt_sync: ctx is NULL");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipStreamSynchronize(c->cstream));
   return LT_OK;
 }
 
@@ -295,7 +307,7 @@ struct lt_image {
   std::vector<SlotW> tw;
   uint32_t d3mul = 0;
   std::vector<double> d3;
-  std::vector<KeyRec> keys;   // narrow images: kept for the optional hot table
+  std::vector<KeyRec> keys;   // validated keys (freed once the tables are built)
 };
 
 lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
@@ -354,7 +366,7 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
   img->narrow = narrow ? 1 : 0;
   img->seed = seed;
   img->slots = slots;
-  if (!narrow) std::vector<KeyRec>().swap(keys);
+  std::vector<KeyRec>().swap(keys);
   *out = img.release();
   return LT_OK;
 }
@@ -377,8 +389,7 @@ lt_status lt_image_destroy(lt_image* img) {
   return LT_OK;
 }
 
-static lt_status model_upload(lt_ctx* c, const lt_model_image* v, std::vector<KeyRec>* keys,
-                              lt_model** out) {
+static lt_status model_upload(lt_ctx* c, const lt_model_image* v, lt_model** out) {
   HIP_TRY(hipSetDevice(c->device));
   lt_model* m = new (std::nothrow) lt_model;
   if (!m) return fail(LT_ENOMEM, "lt_model_create: out of host memory");
@@ -386,9 +397,6 @@ static lt_status model_upload(lt_ctx* c, const lt_model_image* v, std::vector<Ke
   m->slots = v->slots;
   m->seed = v->seed;
   m->narrow = v->narrow ? 1 : 0;
-  if (keys && m->narrow) m->keys.swap(*keys);
-  static std::atomic<uint64_t> next_uid{1};
-  m->uid = next_uid.fetch_add(1);
   hipError_t e = hipMalloc(&m->d_table, (size_t)v->table_bytes);
   if (e == hipSuccess)
     e = hipMemcpyAsync(m->d_table, v->table, (size_t)v->table_bytes, hipMemcpyHostToDevice, c->stream);
@@ -420,7 +428,7 @@ lt_status lt_model_create_from_image(lt_ctx* c, const lt_model_image* v, lt_mode
     return fail(LT_EINVAL, "model image: table size %lld does not match %lld slots",
                 (long long)v->table_bytes, (long long)v->slots);
   if (v->d3mul && !v->d3) return fail(LT_EINVAL, "model image: dense table missing");
-  return model_upload(c, v, nullptr, out);
+  return model_upload(c, v, out);
 }
 
 lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
@@ -431,7 +439,7 @@ lt_status lt_model_create(lt_ctx* c, const lt_model_desc* d, lt_model** out) {
   if (st != LT_OK) return st;
   lt_model_image v;
   lt_image_view(img, &v);
-  st = model_upload(c, &v, &img->keys, out);
+  st = model_upload(c, &v, out);
   lt_image_destroy(img);
   return st;
 }
@@ -448,16 +456,6 @@ lt_status lt_model_destroy(lt_model* m) {
 int64_t lt_model_slots(const lt_model* m) { return m ? m->slots : 0; }
 
 // ---------------------------------------------------------------- batch --
-extern "C++" {
-static bool hot_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("LT_HOT");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-}  // extern "C++"
-
 static lt_status validate(const lt_batch_desc* d) {
   if (d->n_sent < 0 || d->n_nodes < 0 || d->n_span < 0 || d->n_post < 0)
     return fail(LT_EINVAL, "batch: negative size");
@@ -594,9 +592,20 @@ static void arena_give(lt_ctx* c, lt_arena& a) {
 
 static void batch_free(lt_batch* b) {
   if (!b) return;
-  dfree(b->d_hot);
+  for (auto& evs : b->ev_rd)
+    for (hipEvent_t ev : evs)
+      if (ev) (void)hipEventDestroy(ev);
   arena_give(b->ctx, b->arena);
   delete b;
+}
+
+// Point the batch's current-result pointers at result slot i.
+static void use_slot(lt_batch* b, int i) {
+  b->cur = i;
+  b->d_count = b->res[i].count;
+  b->d_len = b->res[i].len;
+  b->d_score = b->res[i].score;
+  b->d_codes = b->res[i].codes;
 }
 
 // Sub-buffers of an arena: 256 B aligned, nullptr for empty ones.
@@ -673,8 +682,18 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
                o_bp_off = cv.dev(((size_t)S + 1) * 8), o_cum_n = cv.dev(((size_t)S + 1) * 8),
                o_span_start = cv.dev((size_t)d->n_span * 4),
                o_nodes = cv.dev((size_t)d->n_nodes * sizeof(NodeRec)), o_post = cv.dev(npost * 8),
-               o_bp = cv.dev((size_t)b->bp_entries * 4), o_count = cv.dev((size_t)S * 4),
-               o_len = cv.dev(nres * 4), o_score = cv.dev(nres * 8), o_codes = cv.dev(ncodes * 4);
+               o_bp = cv.dev((size_t)b->bp_entries * 4);
+  b->slab_cap = slab_layout(S, max_k, b->total_chars).capacity;
+  const uint64_t slab_alloc = slab_alloc_bytes(S, max_k, b->total_chars);
+  size_t o_count[2], o_len[2], o_score[2], o_codes[2], o_slab[2];
+  for (int i = 0; i < 2; ++i) {
+    o_count[i] = cv.dev((size_t)S * 4);
+    o_len[i] = cv.dev(nres * 4);
+    o_score[i] = cv.dev(nres * 8);
+    o_codes[i] = cv.dev(ncodes * 4);
+    o_slab[i] = cv.dev(slab_alloc);
+  }
+  const size_t h_slab = cv.host(b->slab_cap);
   const size_t h_count = cv.host((size_t)S * 4), h_len = cv.host(nres * 4), h_score = cv.host(nres * 8),
                h_codes = cv.host(ncodes * 4);
   hipError_t e = arena_take(c, cv.d, cv.h, b->arena);
@@ -694,10 +713,15 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   b->d_nodes = at<NodeRec>(D, o_nodes);
   b->d_post = at<double>(D, o_post);
   b->d_bp = at<uint32_t>(D, o_bp);
-  b->d_count = at<int32_t>(D, o_count);
-  b->d_len = at<int32_t>(D, o_len);
-  b->d_score = at<double>(D, o_score);
-  b->d_codes = at<int32_t>(D, o_codes);
+  for (int i = 0; i < 2; ++i) {
+    b->res[i].count = at<int32_t>(D, o_count[i]);
+    b->res[i].len = at<int32_t>(D, o_len[i]);
+    b->res[i].score = at<double>(D, o_score[i]);
+    b->res[i].codes = at<int32_t>(D, o_codes[i]);
+    b->res[i].slab = at<char>(D, o_slab[i]);
+  }
+  b->h_slab = at<char>(H, h_slab);
+  use_slot(b, 0);
   b->h_count = at<int32_t>(H, h_count);
   b->h_len = at<int32_t>(H, h_len);
   b->h_score = at<double>(H, h_score);
@@ -743,19 +767,6 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     }
   }, 256);
   up(b->d_nodes, recs.get(), (size_t)d->n_nodes);
-  if (hot_enabled()) {
-    const uint32_t lim = 1u << NARROW_ID_BITS;
-    b->f_word.assign(lim, 0u);
-    b->f_tag.assign(lim, 0u);
-    b->f_morph.assign(lim, 0u);
-    for (int64_t i = 0; i < d->n_nodes; ++i) {
-      const uint32_t w = (uint32_t)d->node_word[i], t = (uint32_t)d->node_tag[i],
-                     mo = (uint32_t)d->node_morph0[i];
-      if (w < lim) ++b->f_word[w];
-      if (t < lim) ++b->f_tag[t];
-      if (mo < lim) ++b->f_morph[mo];
-    }
-  }
   up(b->d_post, d->node_post, npost);
   if (e == hipSuccess) e = hipStreamSynchronize(stm);
   if (e != hipSuccess) {
@@ -771,63 +782,12 @@ lt_status lt_batch_destroy(lt_batch* b) {
   if (!b) return LT_OK;
   (void)hipSetDevice(b->ctx->device);
   (void)hipStreamSynchronize(b->ctx->stream);
+  (void)hipStreamSynchronize(b->ctx->cstream);
   batch_free(b);
   return LT_OK;
 }
 
 int64_t lt_batch_code_slots(const lt_batch* b, int k) { return b ? b->total_chars * (int64_t)k : 0; }
-
-// ----------------------------------------------------------- hot table --
-// Keys of a narrow model ranked by estimated probe frequency in this batch:
-// the product of the relative frequencies of the key's components among the
-// batch's nodes (word / tag / morph0 slots per feature class), the hottest
-// placed first into a direct-mapped HOT_SLOTS table (a key whose slot is
-// taken is simply not cached).
-static lt_status build_hot(lt_ctx* c, const lt_model* m, lt_batch* b) {
-  if (b->hot_uid == m->uid) return LT_OK;
-  b->hot_uid = 0;
-  if (!m->narrow) return LT_OK;
-  // opt-in (LT_HOT=1) until it pays: it trades global probe traffic for LDS
-  // reads and VALU, and the k=1 kernel is currently VALU/latency bound
-  if (!hot_enabled() || b->f_word.empty()) return LT_OK;
-  const double inv = b->n_nodes ? 1.0 / (double)b->n_nodes : 0.0;
-  auto fw = [&](uint32_t x) { return b->f_word[x] * inv; };
-  auto ft = [&](uint32_t x) { return b->f_tag[x] * inv; };
-  auto fm = [&](uint32_t x) { return b->f_morph[x] * inv; };
-  const size_t F = m->keys.size();
-  std::vector<std::pair<double, uint32_t>> score(F);
-  for (size_t i = 0; i < F; ++i) {
-    const KeyRec& k = m->keys[i];
-    double v = 0.0;
-    switch (k.cls) {
-      case 0: v = fw(k.a) * fw(k.b) * ft(k.c); break;
-      case 1: v = fw(k.a) * ft(k.b); break;
-      case 2: v = ft(k.a) * fw(k.b) * ft(k.c); break;
-      case 3: v = ft(k.a) * ft(k.b); break;
-      case 7: v = fw(k.a) * fw(k.b) * fw(k.c); break;
-      case 8: v = fm(k.a) * fm(k.b); break;
-    }
-    score[i] = {v, (uint32_t)i};
-  }
-  const size_t top = std::min(F, (size_t)HOT_SLOTS * 4);
-  std::partial_sort(score.begin(), score.begin() + top, score.end(),
-                    [](const std::pair<double, uint32_t>& x, const std::pair<double, uint32_t>& y) {
-                      return x.first > y.first || (x.first == y.first && x.second < y.second);
-                    });
-  std::vector<SlotN> hot(HOT_SLOTS, SlotN{0ull, 0.0});
-  for (size_t r = 0; r < top; ++r) {
-    if (score[r].first <= 0.0) break;
-    const KeyRec& k = m->keys[score[r].second];
-    SlotN& sl = hot[hot_slot(key_base<true>(k.a, k.b, k.c, k.cls))];
-    if (sl.key == 0) { sl.key = narrow_key(k.a, k.b, k.c, k.cls); sl.coef = k.coef; }
-  }
-  if (!b->d_hot) HIP_TRY(hipMalloc((void**)&b->d_hot, HOT_SLOTS * sizeof(SlotN)));
-  HIP_TRY(hipMemcpyAsync(b->d_hot, hot.data(), HOT_SLOTS * sizeof(SlotN), hipMemcpyHostToDevice,
-                         c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  b->hot_uid = m->uid;
-  return LT_OK;
-}
 
 // --------------------------------------------------------------- decode --
 static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, DecodeParams& p) {
@@ -841,14 +801,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.slots = (uint32_t)m->slots;
   p.seed = m->seed;
   p.hk = narrow_hash(m->seed);
-  lt_status hs = build_hot(c, m, b);
-  if (hs != LT_OK) return hs;
-  p.hot = (b->hot_uid == m->uid) ? b->d_hot : nullptr;
-  static const bool d3_off = [] {
-    const char* v = std::getenv("LT_D3");
-    return v && v[0] == '0';
-  }();
-  p.d3 = d3_off ? nullptr : m->d_d3;
+  p.d3 = m->d_d3;
   p.d3mul = m->d3mul;
   p.narrow = m->narrow;
   p.has_tri = b->has_tri;
@@ -877,17 +830,36 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   return LT_OK;
 }
 
+// The next decode writes the result slot the previous one did not: the D2H
+// of the previous results (copy stream) can run meanwhile.  A copy still
+// queued on the slot being reused is waited for on the decode stream.
+static lt_status next_slot(lt_ctx* c, lt_batch* b) {
+  const int i = b->cur ^ 1;
+  for (int r = 0; r < 2; ++r)
+    if (b->rd_pending[i][r]) {
+      // a reader that is already done costs the decode stream nothing
+      if (hipEventQuery(b->ev_rd[i][r]) != hipSuccess) HIP_TRY(hipStreamWaitEvent(c->stream, b->ev_rd[i][r], 0));
+      b->rd_pending[i][r] = false;
+    }
+  use_slot(b, i);
+  return LT_OK;
+}
+
 lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
-  // code slots past a path's length read as -1 (deterministic output)
-  const size_t ncodes = (size_t)b->total_chars * k;
-  if (ncodes) HIP_TRY(hipMemsetAsync(b->d_codes, 0xFF, ncodes * 4, c->stream));
-  HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  HIP_TRY(launch_decode(p, c->stream, false));
-  HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  if ((st = next_slot(c, b)) != LT_OK) return st;
+  p.out_count = b->d_count;
+  p.out_len = b->d_len;
+  p.out_score = b->d_score;
+  p.out_codes = b->d_codes;
+  const int r = (int)(c->n_launch % lt_ctx::KRING);
+  HIP_TRY(launch_decode(p, c->stream, false, c->kev0[r], c->kev1[r]));
+  b->last_end = c->kev1[r];          // other streams wait for this decode here
+  b->launch_serial = c->n_serial++;
+  ++c->n_launch;
   b->last_k = k;
   return LT_OK;
 }
@@ -979,24 +951,134 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
 
 lt_status lt_last_kernel_ms(lt_ctx* c, float* ms) {
   if (!c || !ms) return fail(LT_EINVAL, "lt_last_kernel_ms: NULL argument");
-  HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  if (c->n_launch < 1) return fail(LT_EINVAL, "lt_last_kernel_ms: no decode launched");
+  const int r = (int)((c->n_launch - 1) % lt_ctx::KRING);
+  HIP_TRY(hipEventElapsedTime(ms, c->kev0[r], c->kev1[r]));
   return LT_OK;
+}
+
+lt_status lt_kernel_ms_recent(lt_ctx* c, int n, float* ms, int* got) {
+  if (!c || (!ms && n > 0) || !got) return fail(LT_EINVAL, "lt_kernel_ms_recent: NULL argument");
+  const int64_t have = std::min<int64_t>(c->n_launch, lt_ctx::KRING);
+  const int m = (int)std::min<int64_t>(std::max(n, 0), have);
+  for (int j = 0; j < m; ++j) {   // oldest first
+    const int r = (int)((c->n_launch - m + j) % lt_ctx::KRING);
+    HIP_TRY(hipEventElapsedTime(&ms[j], c->kev0[r], c->kev1[r]));
+  }
+  *got = m;
+  return LT_OK;
+}
+
+// Stream `st` waits for the last decode of b (the decode stream's current end).
+// The decode's own end event (lt_ctx::kev1 of its launch; re-recorded at most
+// by a later launch of the same stream, which only waits longer) -- no extra
+// command on the decode stream.
+static hipError_t after_decode(lt_batch* b, hipStream_t st) {
+  if (!b->last_end) return hipSuccess;     // the last launch completed synchronously
+  return hipStreamWaitEvent(st, b->last_end, 0);
+}
+
+// Reader `r` is done with the current result slot at this point of `st`.
+static hipError_t slot_read(lt_batch* b, int r, hipStream_t st) {
+  const int i = b->cur;
+  hipError_t e = hipSuccess;
+  if (!b->ev_rd[i][r]) e = hipEventCreateWithFlags(&b->ev_rd[i][r], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(b->ev_rd[i][r], st);
+  if (e == hipSuccess) b->rd_pending[i][r] = true;
+  return e;
 }
 
 lt_status lt_result_fetch(lt_ctx* c, lt_batch* b) {
   if (!c || !b) return fail(LT_EINVAL, "lt_result_fetch: NULL argument");
+  if (b->ctx != c) return fail(LT_EINVAL, "lt_result_fetch: batch of another context");
   if (b->last_k < 1) return fail(LT_EINVAL, "lt_result_fetch: no decode launched");
   const int k = b->last_k;
   const size_t S = (size_t)b->n_sent;
   HIP_TRY(hipSetDevice(c->device));
+  hipStream_t cs = c->cstream;
+  // DMA copies on the copy stream once the decode is done -- under the next decode
+  HIP_TRY(after_decode(b, cs));
   if (S) {
-    HIP_TRY(hipMemcpyAsync(b->h_count, b->d_count, S * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(b->h_len, b->d_len, S * k * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(b->h_score, b->d_score, S * k * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(b->h_count, b->d_count, S * 4, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(b->h_len, b->d_len, S * k * 4, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(b->h_score, b->d_score, S * k * 8, hipMemcpyDeviceToHost, cs));
   }
   const size_t nc = (size_t)b->total_chars * k;
-  if (nc) HIP_TRY(hipMemcpyAsync(b->h_codes, b->d_codes, nc * 4, hipMemcpyDeviceToHost, c->stream));
+  if (nc) HIP_TRY(hipMemcpyAsync(b->h_codes, b->d_codes, nc * 4, hipMemcpyDeviceToHost, cs));
+  HIP_TRY(slot_read(b, lt_batch::RD_COPY, cs));
   return LT_OK;
+}
+
+}  // extern "C"
+
+uint64_t lt::slab_alloc_bytes(int64_t n_sent, int k, int64_t chars) {
+  return slab_layout(n_sent, k, chars).capacity + al16(8 * (uint64_t)(pack_blocks(n_sent * k) + 1));
+}
+
+hipError_t lt::pack_last_results_on(lt_batch* b, int reader, void* slab, hipStream_t st) {
+  hipError_t e = after_decode(b, st);
+  if (e != hipSuccess) return e;
+  ResultsPackParams p{};
+  p.count = b->d_count;
+  p.len = b->d_len;
+  p.score = b->d_score;
+  p.codes = b->d_codes;
+  p.sent_n = b->d_sent_n;
+  p.cum_n = b->d_cum_n;
+  p.n_sent = b->n_sent;
+  p.k = b->last_k;
+  p.n_entries = (int64_t)b->n_sent * b->last_k;
+  p.n_blocks = pack_blocks(p.n_entries);
+  p.lay = slab_layout(b->n_sent, b->last_k, b->total_chars);
+  p.block_sum = reinterpret_cast<int64_t*>(static_cast<char*>(slab) + p.lay.capacity);
+  p.slab = slab;
+  e = launch_pack_results(p, st);
+  if (e == hipSuccess) e = slot_read(b, reader, st);
+  return e;
+}
+
+extern "C" {
+
+lt_status lt_result_fetch_packed(lt_ctx* c, lt_batch* b) {
+  if (!c || !b) return fail(LT_EINVAL, "lt_result_fetch_packed: NULL argument");
+  if (b->ctx != c) return fail(LT_EINVAL, "lt_result_fetch_packed: batch of another context");
+  if (b->last_k < 1) return fail(LT_EINVAL, "lt_result_fetch_packed: no decode launched");
+  HIP_TRY(hipSetDevice(c->device));
+  const int i = b->cur;
+  // everything on the copy stream, under the next decode: pack the slot
+  // (once per decode), copy the used bytes
+  if (b->res[i].packed_launch != b->launch_serial) {
+    HIP_TRY(pack_last_results_on(b, lt_batch::RD_COPY, b->res[i].slab, c->cstream));
+    b->res[i].packed_launch = b->launch_serial;
+  }
+  HIP_TRY(launch_slab_to_host(b->res[i].slab, b->h_slab, b->slab_cap, c->cstream));
+  return LT_OK;
+}
+
+lt_status lt_slab_parse(const void* slab, uint64_t bytes, lt_packed_view* v) {
+  if (!slab || !v) return fail(LT_EINVAL, "lt_slab_parse: NULL argument");
+  if (bytes < sizeof(SlabHeader)) return fail(LT_EINVAL, "lt_slab_parse: %llu bytes", (unsigned long long)bytes);
+  const SlabHeader* h = static_cast<const SlabHeader*>(slab);
+  if (h->n_sent < 0 || h->k < 1 || h->n_codes < 0)
+    return fail(LT_EINVAL, "lt_slab_parse: bad header");
+  const SlabLayout L = slab_layout(h->n_sent, h->k, 0);
+  if ((uint64_t)h->bytes != slab_used_bytes(L, h->n_codes) || (uint64_t)h->bytes > bytes)
+    return fail(LT_EINVAL, "lt_slab_parse: slab of %lld bytes in a buffer of %llu", (long long)h->bytes,
+                (unsigned long long)bytes);
+  const char* base = static_cast<const char*>(slab);
+  v->n_sent = h->n_sent;
+  v->k = h->k;
+  v->n_codes = h->n_codes;
+  v->count = reinterpret_cast<const int32_t*>(base + L.count);
+  v->length = reinterpret_cast<const int32_t*>(base + L.len);
+  v->score = reinterpret_cast<const double*>(base + L.score);
+  v->codes = reinterpret_cast<const int32_t*>(base + L.codes);
+  return LT_OK;
+}
+
+lt_status lt_result_view_packed(lt_batch* b, lt_packed_view* v) {
+  if (!b || !v) return fail(LT_EINVAL, "lt_result_view_packed: NULL argument");
+  return lt_slab_parse(b->h_slab, b->slab_cap, v);
 }
 
 lt_status lt_result_view(lt_batch* b, lt_result* v) {
@@ -1031,8 +1113,15 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
+  if ((st = next_slot(c, b)) != LT_OK) return st;
+  p.out_count = b->d_count;
+  p.out_len = b->d_len;
+  p.out_score = b->d_score;
+  p.out_codes = b->d_codes;
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
   HIP_TRY(launch_decode(p, c->stream, true));
+  b->launch_serial = c->n_serial++;
+  b->last_end = nullptr;             // complete below
   unsigned long long h[4] = {0, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));

@@ -3,14 +3,16 @@
 //
 // Sentences shard across GPUs with no data-path exchange;
 // the only collective is one RCCL gather of the per-rank result blocks to a
-// root rank over xGMI.  Gathers need equal counts on every rank, so
-// lt_gather_prepare agrees on the largest per-rank sentence count and code
-// slot count (one small ncclAllGather) and sizes two padded send slots (and,
-// on the root, two receive slots) once.  Each gather snapshots the decode's
-// results into the next send slot with a device copy on the decoder stream
-// (a few microseconds at HBM speed) and runs the RCCL group on the
-// communicator's own stream, so gather i overlaps decode i+1; a slot is
-// reused only after its previous gather has completed (event wait).
+// root rank over xGMI.  Each rank's results travel as a slab (packed
+// results, lt_results.hip); gathers need equal counts on every rank, so
+// lt_gather_prepare agrees on the largest slab capacity (one small
+// ncclAllGather) and sizes two send slots (and, on the root, two receive
+// slots of nranks slabs) once.  Each gather packs the decode's results into
+// the next send slot and runs one ncclGather, both on the communicator's own
+// stream, so gather i overlaps decode i+1; a decode reuses a result slot
+// only after the packing has read it, the root reuses a receive slot only
+// after its host copy (event waits).  The root copies the used bytes of every rank's slab to pinned host
+// memory on the context's copy stream.
 //
 // RCCL is dlopen'ed on first use so that single-GPU users of the library
 // never load it; its ABI comes from ROCm's rccl.h (types only).
@@ -29,6 +31,7 @@
 #include "../../include/lattice_decode.h"
 #include "lt_error.h"
 #include "lt_handles.h"
+#include "lt_internal.h"
 
 namespace {
 
@@ -118,15 +121,6 @@ const Rccl& rccl() {
       return lt::set_error(LT_ERCCL, "%s failed: %s", #expr, rccl().error_string(_r));   \
   } while (0)
 
-template <class T>
-hipError_t dalloc_fill(T** p, size_t n, int byte) {
-  *p = nullptr;
-  if (n == 0) return hipSuccess;
-  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
-  if (e == hipSuccess) e = hipMemset(*p, byte, n * sizeof(T));
-  return e;
-}
-
 void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
@@ -137,63 +131,39 @@ void hfree(void* p) {
 
 }  // namespace
 
-// One result block (count, length, score, codes) at the padded per-rank size,
-// or world x that on the root.
-struct Block {
-  int32_t *count = nullptr, *len = nullptr, *codes = nullptr;
-  double* score = nullptr;
-};
-
 struct lt_comm {
   lt_ctx* ctx = nullptr;
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;          // RCCL stream: gathers overlap the next decode
   int nranks = 0, rank = 0, root = -1, k = 0;
   const lt_batch* batch = nullptr;       // prepared batch
-  int64_t s_pad = 0, c_pad = 0;          // per-rank padded sentences / characters
+  uint64_t cap = 0;                      // slab bytes per rank (max over ranks)
   std::vector<int64_t> rank_s, rank_c;   // every rank's sentences / characters
-  // two slots (ping-pong): the send copy of a decode's results and, on the
-  // root, the receive block
-  Block send[2], recv[2];
+  // two slots (ping-pong): this rank's packed results (send) and, on the
+  // root, every rank's slab at stride cap (receive)
+  char* send[2] = {nullptr, nullptr};
+  char* recv[2] = {nullptr, nullptr};
   bool used[2] = {false, false};
   int next = 0, last = -1;
-  hipEvent_t ready[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
   hipEvent_t g0[2] = {nullptr, nullptr}, g1[2] = {nullptr, nullptr};
-  // root: pinned mirror of one receive block
-  int32_t *h_count = nullptr, *h_len = nullptr, *h_codes = nullptr;
-  double* h_score = nullptr;
+  hipEvent_t fetched[2] = {nullptr, nullptr};   // root: copy of receive slot i to the host queued
+  bool fetch_pending[2] = {false, false};
+  // root: pinned mirror of one receive block (nranks slabs at stride cap)
+  char* h_slabs = nullptr;
 };
 
 namespace {
 
-void free_block(Block& b) {
-  dfree(b.count);
-  dfree(b.len);
-  dfree(b.score);
-  dfree(b.codes);
-  b = Block{};
-}
-
-hipError_t alloc_block(Block& b, size_t n_count, size_t n_res, size_t n_codes) {
-  hipError_t e = dalloc_fill(&b.count, n_count, 0);
-  if (e == hipSuccess) e = dalloc_fill(&b.len, n_res, 0);
-  if (e == hipSuccess) e = dalloc_fill(&b.score, n_res, 0);
-  if (e == hipSuccess) e = dalloc_fill(&b.codes, n_codes, 0xFF);
-  return e;
-}
-
 void free_slots(lt_comm* c) {
   for (int i = 0; i < 2; ++i) {
-    free_block(c->send[i]);
-    free_block(c->recv[i]);
+    dfree(c->send[i]);
+    dfree(c->recv[i]);
+    c->send[i] = c->recv[i] = nullptr;
     c->used[i] = false;
   }
-  hfree(c->h_count);
-  hfree(c->h_len);
-  hfree(c->h_score);
-  hfree(c->h_codes);
-  c->h_count = c->h_len = c->h_codes = nullptr;
-  c->h_score = nullptr;
+  hfree(c->h_slabs);
+  c->h_slabs = nullptr;
   c->next = 0;
   c->last = -1;
 }
@@ -240,13 +210,16 @@ lt_status lt_comm_create(lt_ctx* ctx, int nranks, int rank, const uint8_t id[LT_
   c->comm = nc;
   c->nranks = nranks;
   c->rank = rank;
-  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  // high priority: its packing kernels must find CUs while a decode runs
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-    e = hipEventCreateWithFlags(&c->ready[i], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
+    e = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&c->g0[i]);
     if (e == hipSuccess) e = hipEventCreate(&c->g1[i]);
   }
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->fetched[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     lt_comm_destroy(c);
     return lt::set_error(LT_EHIP, "lt_comm_create: %s", hipGetErrorString(e));
@@ -260,9 +233,12 @@ lt_status lt_comm_destroy(lt_comm* c) {
   (void)hipSetDevice(c->ctx->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->ctx->stream);
+  (void)hipStreamSynchronize(c->ctx->cstream);
   free_slots(c);
+  for (hipEvent_t ev : c->fetched)
+    if (ev) (void)hipEventDestroy(ev);
   for (int i = 0; i < 2; ++i) {
-    hipEvent_t evs[] = {c->ready[i], c->done[i], c->g0[i], c->g1[i]};
+    hipEvent_t evs[] = {c->done[i], c->g0[i], c->g1[i]};
     for (hipEvent_t ev : evs)
       if (ev) (void)hipEventDestroy(ev);
   }
@@ -283,16 +259,16 @@ lt_status lt_gather_prepare(lt_comm* c, lt_batch* b, int k, int root) {
   HIP_TRY(hipSetDevice(x->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipStreamSynchronize(x->stream));
-  // every rank's (sentences, characters)
+  // every rank's (sentences, characters, slab capacity)
   const int R = c->nranks;
-  int64_t mine[2] = {b->n_sent, b->total_chars};
+  int64_t mine[3] = {b->n_sent, b->total_chars, (int64_t)lt::slab_layout(b->n_sent, k, b->total_chars).capacity};
   int64_t *d_mine = nullptr, *d_all = nullptr;
-  std::vector<int64_t> all(2 * (size_t)R);
+  std::vector<int64_t> all(3 * (size_t)R);
   hipError_t e = hipMalloc((void**)&d_mine, sizeof mine);
   if (e == hipSuccess) e = hipMalloc((void**)&d_all, all.size() * sizeof(int64_t));
   if (e == hipSuccess) e = hipMemcpy(d_mine, mine, sizeof mine, hipMemcpyHostToDevice);
   ncclResult_t nr = ncclSuccess;
-  if (e == hipSuccess) nr = r.all_gather(d_mine, d_all, 2, ncclInt64, c->comm, c->stream);
+  if (e == hipSuccess) nr = r.all_gather(d_mine, d_all, 3, ncclInt64, c->comm, c->stream);
   if (e == hipSuccess && nr == ncclSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess && nr == ncclSuccess)
     e = hipMemcpy(all.data(), d_all, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost);
@@ -303,30 +279,21 @@ lt_status lt_gather_prepare(lt_comm* c, lt_batch* b, int k, int root) {
   if (e != hipSuccess) return lt::set_error(LT_EHIP, "lt_gather_prepare: %s", hipGetErrorString(e));
   c->rank_s.assign(R, 0);
   c->rank_c.assign(R, 0);
-  int64_t s_pad = 0, c_pad = 0;
+  uint64_t cap = 0;
   for (int q = 0; q < R; ++q) {
-    c->rank_s[q] = all[2 * q];
-    c->rank_c[q] = all[2 * q + 1];
-    s_pad = std::max(s_pad, c->rank_s[q]);
-    c_pad = std::max(c_pad, c->rank_c[q]);
+    c->rank_s[q] = all[3 * q];
+    c->rank_c[q] = all[3 * q + 1];
+    cap = std::max<uint64_t>(cap, (uint64_t)all[3 * q + 2]);
   }
-  s_pad = std::max<int64_t>(s_pad, 1);
-  c_pad = std::max<int64_t>(c_pad, 1);
-  // send slots (padding past this rank's results stays 0 / -1) and, on the
-  // root, receive slots + one pinned mirror
+  // send slots and, on the root, receive slots + one pinned mirror
   free_slots(c);
-  const size_t sp = (size_t)s_pad, cp = (size_t)c_pad;
+  const uint64_t scratch = lt::slab_alloc_bytes(b->n_sent, k, b->total_chars) -
+                           lt::slab_layout(b->n_sent, k, b->total_chars).capacity;
   for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-    e = alloc_block(c->send[i], sp, sp * k, cp * k);
-    if (e == hipSuccess && c->rank == root) e = alloc_block(c->recv[i], R * sp, R * sp * k, R * cp * k);
+    e = hipMalloc((void**)&c->send[i], cap + scratch);
+    if (e == hipSuccess && c->rank == root) e = hipMalloc((void**)&c->recv[i], cap * R);
   }
-  if (c->rank == root) {
-    const size_t rc = (size_t)R * sp, rr = rc * k, rcd = (size_t)R * cp * k;
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_count, rc * 4, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_len, rr * 4, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_score, rr * 8, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->h_codes, rcd * 4, hipHostMallocDefault);
-  }
+  if (e == hipSuccess && c->rank == root) e = hipHostMalloc((void**)&c->h_slabs, cap * R, hipHostMallocDefault);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     free_slots(c);
@@ -336,8 +303,7 @@ lt_status lt_gather_prepare(lt_comm* c, lt_batch* b, int k, int root) {
   c->root = root;
   c->k = k;
   c->batch = b;
-  c->s_pad = s_pad;
-  c->c_pad = c_pad;
+  c->cap = cap;
   return LT_OK;
 }
 
@@ -348,38 +314,23 @@ lt_status lt_gather_launch(lt_comm* c, lt_batch* b) {
     return lt::set_error(LT_EINVAL, "lt_gather_launch: last decode was beam %d, prepared for %d", b->last_k, c->k);
   const Rccl& r = rccl();
   lt_ctx* x = c->ctx;
-  const int k = c->k, i = c->next;
-  const size_t sp = (size_t)c->s_pad, cp = (size_t)c->c_pad, S = (size_t)b->n_sent;
-  const size_t nc = (size_t)b->total_chars * k;
+  const int i = c->next;
   const bool at_root = c->rank == c->root;
-  Block& snd = c->send[i];
-  Block& rcv = c->recv[i];
   HIP_TRY(hipSetDevice(x->device));
-  // the slot's previous gather (two launches ago) must be done with it
-  if (c->used[i]) HIP_TRY(hipStreamWaitEvent(x->stream, c->done[i], 0));
-  // snapshot the decode's results into the send slot (decoder stream), so the
-  // next decode may overwrite the batch's buffers while this gather runs
-  if (S) {
-    HIP_TRY(hipMemcpyAsync(snd.count, b->d_count, S * 4, hipMemcpyDeviceToDevice, x->stream));
-    HIP_TRY(hipMemcpyAsync(snd.len, b->d_len, S * k * 4, hipMemcpyDeviceToDevice, x->stream));
-    HIP_TRY(hipMemcpyAsync(snd.score, b->d_score, S * k * 8, hipMemcpyDeviceToDevice, x->stream));
+  // everything on the communicator stream (the decode stream goes on with
+  // the next decode): on the root, the host copy of receive slot i must be
+  // done with it; the decode's results are packed into send slot i (whose
+  // previous gather precedes on this stream), then gathered
+  if (at_root && c->fetch_pending[i]) {
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->fetched[i], 0));
+    c->fetch_pending[i] = false;
   }
-  if (nc) HIP_TRY(hipMemcpyAsync(snd.codes, b->d_codes, nc * 4, hipMemcpyDeviceToDevice, x->stream));
-  HIP_TRY(hipEventRecord(c->ready[i], x->stream));
-  HIP_TRY(hipStreamWaitEvent(c->stream, c->ready[i], 0));
   HIP_TRY(hipEventRecord(c->g0[i], c->stream));
-  NCCL_TRY(r.group_start());
-  ncclResult_t nr = r.gather(snd.count, at_root ? rcv.count : nullptr, sp, ncclInt32, c->root, c->comm,
-                             c->stream);
-  if (nr == ncclSuccess)
-    nr = r.gather(snd.len, at_root ? rcv.len : nullptr, sp * k, ncclInt32, c->root, c->comm, c->stream);
-  if (nr == ncclSuccess)
-    nr = r.gather(snd.score, at_root ? rcv.score : nullptr, sp * k, ncclFloat64, c->root, c->comm, c->stream);
-  if (nr == ncclSuccess)
-    nr = r.gather(snd.codes, at_root ? rcv.codes : nullptr, cp * k, ncclInt32, c->root, c->comm, c->stream);
-  ncclResult_t ne = r.group_end();
-  if (nr != ncclSuccess) return lt::set_error(LT_ERCCL, "lt_gather_launch: ncclGather: %s", r.error_string(nr));
-  if (ne != ncclSuccess) return lt::set_error(LT_ERCCL, "lt_gather_launch: ncclGroupEnd: %s", r.error_string(ne));
+  HIP_TRY(lt::pack_last_results_on(b, lt_batch::RD_GATHER, c->send[i], c->stream));
+  // one gather of the padded slabs (the used part of each is what the root
+  // copies to the host)
+  NCCL_TRY(r.gather(c->send[i], at_root ? c->recv[i] : nullptr, c->cap, ncclUint8, c->root, c->comm,
+                    c->stream));
   HIP_TRY(hipEventRecord(c->g1[i], c->stream));
   HIP_TRY(hipEventRecord(c->done[i], c->stream));
   c->used[i] = true;
@@ -400,29 +351,22 @@ lt_status lt_gather_fetch(lt_comm* c) {
   if (c->root < 0 || c->rank != c->root) return lt::set_error(LT_EINVAL, "lt_gather_fetch: not the root");
   if (c->last < 0) return lt::set_error(LT_EINVAL, "lt_gather_fetch: nothing gathered");
   lt_ctx* x = c->ctx;
-  const Block& rcv = c->recv[c->last];
-  const size_t rc = (size_t)c->nranks * c->s_pad, rr = rc * c->k, rcd = (size_t)c->nranks * c->c_pad * c->k;
   HIP_TRY(hipSetDevice(x->device));
-  HIP_TRY(hipStreamWaitEvent(x->stream, c->done[c->last], 0));
-  HIP_TRY(hipMemcpyAsync(c->h_count, rcv.count, rc * 4, hipMemcpyDeviceToHost, x->stream));
-  HIP_TRY(hipMemcpyAsync(c->h_len, rcv.len, rr * 4, hipMemcpyDeviceToHost, x->stream));
-  HIP_TRY(hipMemcpyAsync(c->h_score, rcv.score, rr * 8, hipMemcpyDeviceToHost, x->stream));
-  HIP_TRY(hipMemcpyAsync(c->h_codes, rcv.codes, rcd * 4, hipMemcpyDeviceToHost, x->stream));
+  // on the ctx's copy stream once the gather is done: each rank's used bytes
+  HIP_TRY(hipStreamWaitEvent(x->cstream, c->done[c->last], 0));
+  for (int q = 0; q < c->nranks; ++q)
+    HIP_TRY(lt::launch_slab_to_host(c->recv[c->last] + (size_t)q * c->cap, c->h_slabs + (size_t)q * c->cap, c->cap,
+                                    x->cstream));
+  HIP_TRY(hipEventRecord(c->fetched[c->last], x->cstream));
+  c->fetch_pending[c->last] = true;
   return LT_OK;
 }
 
-lt_status lt_gather_view(lt_comm* c, int q, lt_result* v, int32_t* n_sent, int64_t* code_slots) {
+lt_status lt_gather_view(lt_comm* c, int q, lt_packed_view* v) {
   if (!c || !v) return lt::set_error(LT_EINVAL, "lt_gather_view: NULL argument");
   if (c->root < 0 || c->rank != c->root) return lt::set_error(LT_EINVAL, "lt_gather_view: not the root");
   if (q < 0 || q >= c->nranks) return lt::set_error(LT_EINVAL, "lt_gather_view: rank %d", q);
-  const size_t sp = (size_t)c->s_pad, cp = (size_t)c->c_pad, k = (size_t)c->k;
-  v->count = c->h_count + q * sp;
-  v->length = c->h_len + q * sp * k;
-  v->score = c->h_score + q * sp * k;
-  v->codes = c->h_codes + q * cp * k;
-  if (n_sent) *n_sent = (int32_t)c->rank_s[q];
-  if (code_slots) *code_slots = c->rank_c[q] * (int64_t)k;
-  return LT_OK;
+  return lt_slab_parse(c->h_slabs + (size_t)q * c->cap, c->cap, v);
 }
 
 lt_status lt_last_gather_ms(lt_comm* c, float* ms) {

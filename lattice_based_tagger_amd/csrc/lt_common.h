@@ -134,13 +134,6 @@ LT_HD void narrow_slots(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c,
   i2 = slot_of(b2, slots);
 }
 
-// Hot-key table: a direct-mapped subset of the model (the keys with the
-// highest estimated probe frequency in a batch), staged in LDS by every
-// block.  Optional: a key missing from it is looked up in the full table.
-constexpr int HOT_SLOTS = 1024;
-constexpr uint32_t HOT_SEED = 0x6A09E667u;
-LT_HD uint32_t hot_slot(KeyBase kb) { return mix1(kb.b1 ^ HOT_SEED) & (HOT_SLOTS - 1); }
-
 // Dense class-3 table: the (t_j, t_k) keys of a model whose class-3 tag values
 // are few (<= D3_DIM) live in a D3_DIM x D3_DIM coefficient array, indexed by
 // a multiplicative hash the library picks to be injective on those values.

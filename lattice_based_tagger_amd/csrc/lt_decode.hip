@@ -23,9 +23,6 @@
 //    group (Python's stable sort), the top k written to the ring.
 //  * lt_beam_pk<KT>    -- beam_size 9..32 (KT = 16, 32): one sentence per wave,
 //    the same enumeration and rank counting over several scoring rounds.
-//  * lt_viterbi_k / lt_beam_k -- the first versions (one 16-lane row per
-//    sentence; per-lane top-k merged by k argmax rounds), kept for A/B runs
-//    (LT_VITERBI=row16, LT_BEAM=v1).
 // All: the frontier (beams of the last 9 end positions) lives in LDS as a
 // ring whose entries cache the fields of the hypothesis' last two nodes;
 // trigram classes 4/5/6 arrive pre-resolved per node, class 3 (tag, tag)
@@ -34,6 +31,7 @@
 // unneeded probe gets an out-of-range offset (returns 0, touches no memory)
 // instead of a branch.  Present coefficients are summed in numpy's pairwise
 // order.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <cstring>
@@ -46,6 +44,12 @@ using namespace lt;
 namespace {
 
 constexpr uint32_t INV = 0xFFFFFFFFu;
+
+// A decode launch: its stream and the events recorded with its dispatch.
+struct Launch {
+  hipStream_t st;
+  hipEvent_t e0, e1;
+};
 constexpr uint32_t OOB = 0x80000000u;   // >= every buffer's num_records (host-checked)
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -127,53 +131,11 @@ __device__ __forceinline__ Cand read_block(const uint4* wave_planes, int gbase, 
   return c;
 }
 
-// Pin prefetched values in registers: the empty asm makes them opaque, so the
-// compiler cannot re-issue ("rematerialise") the loads at their later use.
-__device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
-
 // Hypothesis fields the scorer needs (from the LDS frontier).
 struct Hyp {
   double score, f6;
   uint32_t jword, jmorph, jtag, jmask, iword, imorph, imask, depth;
 };
-
-__device__ __forceinline__ bool better(double s1, uint32_t g1, double s2, uint32_t g2) {
-  // (score desc, generation index asc); INV never wins.
-  if (g2 == INV) return g1 != INV;
-  if (g1 == INV) return false;
-  return (s1 > s2) || (s1 == s2 && g1 < g2);
-}
-
-template <int G>
-__device__ __forceinline__ void group_argmax(double& s, uint32_t& g) {
-#pragma unroll
-  for (int off = G / 2; off >= 1; off >>= 1) {
-    const double os = __shfl_xor(s, off, G);
-    const uint32_t og = __shfl_xor(g, off, G);
-    if (better(os, og, s, g)) { s = os; g = og; }
-  }
-}
-
-// Argmax over one 16-lane DPP row (the k=1 lane group): quad xor-1, quad
-// xor-2, half-row mirror, row mirror -- register-to-register, no LDS trip.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL>
-__device__ __forceinline__ void dpp_step(double& s, uint32_t& g) {
-  const uint64_t bits = __builtin_bit_cast(uint64_t, s);
-  const uint32_t lo = dpp_u32<CTRL>((uint32_t)bits), hi = dpp_u32<CTRL>((uint32_t)(bits >> 32));
-  const double os = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-  const uint32_t og = dpp_u32<CTRL>(g);
-  if (better(os, og, s, g)) { s = os; g = og; }
-}
-__device__ __forceinline__ void row16_argmax(double& s, uint32_t& g) {
-  dpp_step<0xB1>(s, g);    // quad_perm [1,0,3,2]
-  dpp_step<0x4E>(s, g);    // quad_perm [2,3,0,1]
-  dpp_step<0x141>(s, g);   // row_half_mirror
-  dpp_step<0x140>(s, g);   // row_mirror
-}
 
 template <int G>
 __device__ __forceinline__ unsigned long long group_sum(unsigned long long v) {
@@ -278,7 +240,6 @@ struct Probe {
 
 // LDS-resident parts of the model a block stages at its start.
 struct Aux {
-  const uint4* hot;       // hot-key table (HOT_SLOTS SlotN) or nullptr
   const double* d3;       // dense class-3 table (D3_DIM^2) or nullptr
   uint32_t d3mul;
   NarrowHash hk;          // narrow table slot hash
@@ -326,27 +287,17 @@ __device__ __forceinline__ uint32_t probe_need(const Hyp& h, const Cand& c) {
   return need;
 }
 
-// hot: the block's LDS copy of the batch hot table (HOT_SLOTS SlotN), or
-// nullptr.  A needed probe first reads its one hot slot; only a hot miss
-// issues the two global cuckoo loads.
 // Stage the LDS parts of the model (all threads of the block, before any
-// early exit): the hot table when `hotl` is given and the batch has one, and
-// the dense class-3 table when the model has one.
+// early exit): the dense class-3 table when the model has one.
 template <bool NARROW>
-__device__ __forceinline__ Aux stage_aux(const DecodeParams& p, uint4* hotl, double* d3l) {
+__device__ __forceinline__ Aux stage_aux(const DecodeParams& p, double* d3l) {
   Aux a;
-  const bool use_hot = NARROW && hotl != nullptr && p.hot != nullptr;
-  if (use_hot) {
-    const uint4* src = reinterpret_cast<const uint4*>(p.hot);
-    for (int i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) hotl[i] = src[i];
-  }
   if (p.d3) {
     const uint4* src = reinterpret_cast<const uint4*>(p.d3);
     uint4* dst = reinterpret_cast<uint4*>(d3l);
     for (int i = threadIdx.x; i < D3_DIM * D3_DIM / 2; i += blockDim.x) dst[i] = src[i];
   }
-  if (use_hot || p.d3) __syncthreads();
-  a.hot = use_hot ? hotl : nullptr;
+  if (p.d3) __syncthreads();
   a.d3 = p.d3 ? d3l : nullptr;
   a.d3mul = p.d3mul;
   a.hk = p.hk;
@@ -366,24 +317,6 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uin
     P.s1[3].coef = v;
     gneed &= ~8u;
     lpres |= (__builtin_bit_cast(uint64_t, v) != D3_ABSENT) ? 8u : 0u;
-  }
-  if constexpr (NARROW) {
-    if (aux.hot) {
-      // the hot slot is read into s1 (no extra registers); a hit keeps it
-#pragma unroll
-      for (int q = 0; q < 6; ++q)
-        if ((gneed >> q) & 1u) {
-          const uint4 hv = aux.hot[hot_slot(key_base<NARROW>(K.a[q], K.b[q], K.c[q], PCLS[q]))];
-          P.s1[q].key = ((uint64_t)hv.y << 32) | hv.x;
-          P.s1[q].coef = __builtin_bit_cast(double, (u32x2){hv.z, hv.w});
-        }
-#pragma unroll
-      for (int q = 0; q < 6; ++q)
-        if (((gneed >> q) & 1u) && T::hit(P.s1[q], T::key(K.a[q], K.b[q], K.c[q], PCLS[q]))) {
-          gneed &= ~(1u << q);
-          lpres |= 1u << q;
-        }
-    }
   }
   P.gneed = gneed;
   P.lpres = lpres;
@@ -466,9 +399,6 @@ __device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c
 // ===========================================================================
 // beam_size = 1
 // ===========================================================================
-constexpr int V_G = 16;                 // lanes per sentence
-constexpr int V_SPB = 256 / V_G;        // sentences per block
-constexpr int V_BP_LDS = 256;           // end positions whose backpointer stays in LDS
 
 struct alignas(16) VEntry {
   double score, f6;
@@ -482,166 +412,6 @@ __device__ __forceinline__ Hyp read_hyp(const VEntry& e) {
   h.jword = e.jword; h.jmorph = e.jmorph; h.jtag = e.jtag; h.jmask = e.jmask;
   h.iword = e.iword; h.imorph = e.imorph; h.imask = e.imask; h.depth = e.depth;
   return h;
-}
-
-template <bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
-lt_viterbi_k(DecodeParams p) {
-  __shared__ VEntry ring[V_SPB][RING];
-  __shared__ uint32_t bpl[V_SPB][V_BP_LDS];
-  __shared__ uint4 stg[4][3 * 64];             // per wave: 3 planes x 64 lanes x 16 B
-  __shared__ double d3l[D3_DIM * D3_DIM];
-  const Aux aux = stage_aux<NARROW>(p, nullptr, d3l);
-
-  const int grp = threadIdx.x / V_G;
-  const int gl = threadIdx.x % V_G;
-  const int slot = blockIdx.x * V_SPB + grp;
-  if (slot >= p.n_sent) return;
-  const Bufs B = make_bufs(p);
-  const int s = p.order[slot];
-  const int n = p.sent_n[s];
-  const uint32_t nbase = (uint32_t)p.node_off[s];
-  const int32_t* __restrict__ ssp = p.span_start + p.span_off[s];
-  uint32_t* __restrict__ bpg = p.bp + p.bp_off[s];
-  const bool bp_in_lds = n < V_BP_LDS;
-  const int bstride = p.bp_stride;
-  const uint32_t slots = p.slots, seed = p.seed;
-  const int has_tri = p.has_tri;
-  VEntry (&R)[RING] = ring[grp];
-  Counts cnt;
-
-  if (gl == 0) {                                   // beam[0] = [BOS] (beam.py:21-23)
-    const Cand b0 = load_cand(B, nbase);
-    VEntry e0;
-    e0.score = 0.0; e0.f6 = b0.f6;
-    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
-    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
-    R[0] = e0;
-  }
-  __builtin_amdgcn_wave_barrier();
-
-  // A_e = first node of end position e = ssp[(e-1)*8]; A_{n+1} = node count
-  int A0 = ssp[0];
-  int A1 = ssp[n >= 1 ? 8 : 0];
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint4* const wst = stg[wv];
-  const int gbase = (int)(threadIdx.x & 63) - gl;
-  dma_block<V_G>(B, nbase + (uint32_t)A0, n >= 1, wst, gl);
-  int em9 = 0;
-  for (int e = 1; e <= n; ++e) {
-    // everything still outstanding was issued a full position ago (prefetch,
-    // backpointer store): settle it here, before this position issues loads,
-    // so the compiler's own waits below only count this position's loads.
-    __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
-    em9 = em9 == RING - 1 ? 0 : em9 + 1;
-    const int dmax = min(e, p.max_len);
-    const int X = A1 - A0;
-    const Cand cur = read_block<V_G>(wst, gbase, gl);   // this position's candidate (staged by DMA)
-
-    double best_s = -INFINITY;
-    uint32_t best_g = INV;
-
-    // candidate gl: hypothesis from the LDS ring, probes issued
-    const bool act = gl < X;
-    const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
-    int bm0 = em9 - d0;
-    bm0 += bm0 < 0 ? RING : 0;
-    const Hyp h0 = read_hyp(R[act ? bm0 : 0]);
-    const bool skip0 = !act || ((h0.jmask & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));
-
-    // next position: span start and candidate record (software prefetch; the
-    // record goes straight to LDS by DMA once `cur` has been read out of it; a
-    // node past the batch end reads as zeros).  Issued ahead of the probes.
-    int A2 = ssp[min(e + 1, n) * 8];
-
-    // probes of candidate gl (unneeded ones read nothing)
-    Probe<NARROW> P;
-    probe_issue<NARROW>(P, B, slots, seed, h0, cur,
-                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, aux);
-    // DMA after the probes' own LDS reads (an LDS read behind a DMA waits for it)
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0): cur is out of the staging area
-    dma_block<V_G>(B, nbase + (uint32_t)A1, e < n, wst, gl);
-    __builtin_amdgcn_sched_barrier(0);
-    // re-read the hypothesis from LDS instead of holding it in VGPRs across
-    // the probe wait (the compiler barrier stops the reload being merged)
-    asm volatile("" ::: "memory");
-    const Hyp h1 = read_hyp(R[act ? bm0 : 0]);
-    if (!skip0) {
-      const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h1, cur, cnt) : 0.0;
-      if (COUNT) ++cnt.exp;
-      best_s = h1.score + increment(p, cur, tri, nbase + (uint32_t)(A0 + gl));  // beam.py:115
-      best_g = (uint32_t)gl;
-    }
-    // more than 16 candidates ending at e (rare): serial extra rounds
-    for (int g = gl + V_G; g < X; g += V_G) {
-      const Cand c = load_cand(B, nbase + (uint32_t)(A0 + g));
-      const int d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
-      int bm = em9 - d;
-      bm += bm < 0 ? RING : 0;
-      const Hyp h = read_hyp(R[bm]);
-      if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;   // beam.py:43-45
-      const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, aux) : 0.0;
-      if (COUNT) ++cnt.exp;
-      const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)(A0 + g));
-      if (better(sc, (uint32_t)g, best_s, best_g)) { best_s = sc; best_g = (uint32_t)g; }
-    }
-
-    double ws = best_s;
-    uint32_t wg = best_g;
-    row16_argmax(ws, wg);
-    __builtin_amdgcn_wave_barrier();
-    if (wg != INV && best_g == wg) {                 // the winner writes beam[e] (beam.py:112-116)
-      Cand c = cur;
-      Hyp h = h1;
-      int d = d0;
-      if (wg != (uint32_t)gl) {                      // won in an extra round: reload
-        c = load_cand(B, nbase + (uint32_t)(A0 + (int)wg));
-        d = (int)((c.mask & D_MASK) >> D_SHIFT) + 1;
-        int bm = em9 - d;
-        bm += bm < 0 ? RING : 0;
-        h = read_hyp(R[bm]);
-      }
-      VEntry ne;
-      ne.score = ws; ne.f6 = c.f6;
-      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
-      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
-      ne.depth = h.depth + 1;
-      R[em9] = ne;
-      const uint32_t bpv = bp_pack((uint32_t)(A0 + (int)wg), (uint32_t)d, 0u);
-      if (bp_in_lds) bpl[grp][e] = bpv;
-      else bpg[(int64_t)e * bstride] = bpv;
-    }
-    __builtin_amdgcn_wave_barrier();
-    pin(A2);
-    A0 = A1;
-    A1 = A2;
-  }
-
-  // matures = beam[n] + EOS (beam.py:59-61); backtrace
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  if (gl == 0) {
-    const VEntry& f = R[n % RING];
-    p.out_count[s] = 1;
-    p.out_score[s] = f.score + 0.0;
-    p.out_len[s] = (int32_t)f.depth;
-    int32_t* codes = p.out_codes + p.cum_n[s];
-    int pos = n;
-    for (int step = (int)f.depth - 1; step >= 0; --step) {
-      const uint32_t v = bp_in_lds ? bpl[grp][pos] : bpg[(int64_t)pos * bstride];
-      codes[step] = (int32_t)bp_node(v);
-      pos -= (int)bp_d(v);
-    }
-  }
-  if (COUNT) {
-    const unsigned long long ex = group_sum<V_G>(cnt.exp), tu = group_sum<V_G>(cnt.tup),
-                             pb = group_sum<V_G>(cnt.probe);
-    if (gl == 0) {
-      atomicAdd(p.counters + 0, ex);
-      atomicAdd(p.counters + 1, tu);
-      atomicAdd(p.counters + 2, pb);
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -712,7 +482,7 @@ lt_viterbi_pk(DecodeParams p) {
   __shared__ unsigned long long amax[P_WPB][2][W];
   __shared__ uint32_t amin[P_WPB][2][W];
   __shared__ double d3l[D3_DIM * D3_DIM];
-  const Aux aux = stage_aux<NARROW>(p, nullptr, d3l);
+  const Aux aux = stage_aux<NARROW>(p, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
@@ -908,6 +678,7 @@ lt_viterbi_pk(DecodeParams p) {
       codes[step] = (int32_t)bp_node(v);
       pos -= (int)bp_d(v);
     }
+    for (int j = (int)f.depth; j < nw; ++j) codes[j] = -1;      // padded layout
   }
   if (COUNT) {
     const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
@@ -937,274 +708,16 @@ __device__ __forceinline__ Hyp read_entry(const Entry& e) {
   return h;
 }
 
-__device__ __forceinline__ uint32_t rdlane(uint32_t v, int lane) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
-}
-__device__ __forceinline__ double rdlane(double v, int lane) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  return dbl(rdlane((uint32_t)b, lane), rdlane((uint32_t)(b >> 32), lane));
-}
-
-// Argmax over a G-lane group (G = 32 or 64): DPP within 16-lane rows, then the
-// row leaders are read with v_readlane (group-uniform control flow only).
-template <int G>
-__device__ __forceinline__ void group_argmax_fast(double& s, uint32_t& g) {
-  row16_argmax(s, g);
-  const double s0 = rdlane(s, 0), s1 = rdlane(s, 16), s2 = rdlane(s, 32), s3 = rdlane(s, 48);
-  const uint32_t g0 = rdlane(g, 0), g1 = rdlane(g, 16), g2 = rdlane(g, 32), g3 = rdlane(g, 48);
-  double a = s0, c = s2;
-  uint32_t ga = g0, gc = g2;
-  if (better(s1, g1, a, ga)) { a = s1; ga = g1; }
-  if (better(s3, g3, c, gc)) { c = s3; gc = g3; }
-  if (G == 64) {
-    if (better(c, gc, a, ga)) { a = c; ga = gc; }
-    s = a; g = ga;
-  } else {                                   // two groups per wave: rows {0,1}, {2,3}
-    const bool hi = (threadIdx.x & 63) >= 32;
-    s = hi ? c : a;
-    g = hi ? gc : ga;
-  }
-}
-
-// Insert (s, g) into a sorted (score desc, g asc) register list of capacity C.
-template <int C>
-__device__ __forceinline__ void list_insert(double (&ls)[C], uint32_t (&lg)[C], double s, uint32_t g) {
-  if (!better(s, g, ls[C - 1], lg[C - 1])) return;
-  ls[C - 1] = s; lg[C - 1] = g;
-#pragma unroll
-  for (int q = C - 1; q > 0; --q) {
-    if (better(ls[q], lg[q], ls[q - 1], lg[q - 1])) {
-      const double ts = ls[q]; ls[q] = ls[q - 1]; ls[q - 1] = ts;
-      const uint32_t tg = lg[q]; lg[q] = lg[q - 1]; lg[q - 1] = tg;
-    }
-  }
-}
-
-// Expansion index g of end position e -> (span slot j, hypothesis rank r,
-// candidate i) in the reference's generation order (beam.py:31-42).
-struct Exp {
-  int j, r, i, d;
-};
-__device__ __forceinline__ Exp decode_g(int g, const int (&pre)[MAX_SPAN + 1],
-                                        const int (&ss)[MAX_SPAN + 1]) {
-  Exp x;
-  int j = 0;
-#pragma unroll
-  for (int q = 1; q < MAX_SPAN; ++q) j = (g >= pre[q]) ? q : j;
-  const int m = ss[j + 1] - ss[j];
-  const int local = g - pre[j];
-  x.r = local / m;
-  x.i = local - x.r * m;
-  x.j = j;
-  x.d = MAX_SPAN - j;
-  return x;
-}
-
-template <int KT, int G, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(256)
-lt_beam_k(DecodeParams p) {
-  constexpr int SPB = 256 / G;               // sentences per block
-  constexpr int LCAP = 4;                    // expansions per lane per chunk
-  constexpr int STAGE = G;                   // candidate records staged in LDS
-  static_assert(KT <= G, "beam width must not exceed the lane group");
-  __shared__ Entry ring[SPB][RING][KT];
-  __shared__ int32_t cntl[SPB][RING];
-  __shared__ uint4 stg[2][4][3 * 64];        // [position parity][wave][plane x lane]
-  // the dense class-3 table only where its 8 KiB does not cost a block per CU
-  constexpr bool USE_D3 = KT <= 8;
-  __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
-  Aux aux{nullptr, nullptr, 0u, p.hk};
-  if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
-
-  const int grp = threadIdx.x / G;
-  const int gl = threadIdx.x % G;
-  const int slot = blockIdx.x * SPB + grp;
-  if (slot >= p.n_sent) return;
-  const Bufs B = make_bufs(p);
-  const int s = p.order[slot];
-  const int n = p.sent_n[s];
-  const uint32_t nbase = (uint32_t)p.node_off[s];
-  const int32_t* __restrict__ ssp = p.span_start + p.span_off[s];
-  uint32_t* __restrict__ bp = p.bp + p.bp_off[s];
-  const int k = p.k;
-  const int bstride = p.bp_stride;
-  const uint32_t slots = p.slots, seed = p.seed;
-  const int has_tri = p.has_tri;
-  Entry (&R)[RING][KT] = ring[grp];
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int gbase = (int)(threadIdx.x & 63) - gl;      // first lane of this group in its wave
-  Counts cnt;
-
-  if (gl == 0) {                             // beam[0] = [BOS] (beam.py:21-23)
-    const Cand b0 = load_cand(B, nbase);
-    Entry e0;
-    e0.score = 0.0; e0.f6 = b0.f6;
-    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
-    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
-    R[0][0] = e0;
-    cntl[grp][0] = 1;
-  }
-  // span starts and staged candidate records of end position 1
-  int ss[MAX_SPAN + 1];
-#pragma unroll
-  for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = n >= 1 ? ssp[j] : 0;
-  dma_block<G>(B, nbase + (uint32_t)ss[0], n >= 1, stg[1][wv], gl);
-  __builtin_amdgcn_wave_barrier();
-
-  for (int e = 1; e <= n; ++e) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): this position's records landed
-    const uint4* const cst = stg[e & 1][wv];
-    const int dmax = min(e, p.max_len);
-    const int A0 = ss[0];
-    int pre[MAX_SPAN + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int j = 0; j < MAX_SPAN; ++j) {
-      const int d = MAX_SPAN - j;
-      const int c = (d <= dmax) ? cntl[grp][(e - d) % RING] : 0;
-      pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
-    }
-    const int X = pre[MAX_SPAN];
-
-    // prefetch of end position e+1: span starts (registers) and candidate
-    // records (DMA into the other parity buffer, last read a position ago)
-    int ssn[MAX_SPAN + 1];
-    const int en = min(e + 1, n);
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) ssn[j] = ssp[(en - 1) * MAX_SPAN + j];
-    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
-    dma_block<G>(B, nbase + (uint32_t)ss[MAX_SPAN], e < n, stg[(e + 1) & 1][wv], gl);
-    __builtin_amdgcn_sched_barrier(0);
-
-    // chunks of G*LCAP expansions merged into the running top-k (lanes < k)
-    double rs = -INFINITY;
-    uint32_t rg = INV;
-    int nsel = 0;
-    for (int base = 0; base < X; base += G * LCAP) {
-      double ls[LCAP + 1];
-      uint32_t lg[LCAP + 1];
-#pragma unroll
-      for (int q = 0; q <= LCAP; ++q) { ls[q] = -INFINITY; lg[q] = INV; }
-      for (int t = 0; t < LCAP; ++t) {
-        const int g = base + t * G + gl;
-        if (g >= X) break;
-        const Exp x = decode_g(g, pre, ss);
-        const int node = ss[x.j] + x.i;
-        const int so = node - A0;
-        const Cand c = so < STAGE ? read_block<G>(cst, gbase, so) : load_cand(B, nbase + (uint32_t)node);
-        const Hyp h = read_entry(R[(e - x.d) % RING][x.r]);
-        // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
-        if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (x.d < dmax)) continue;
-        const double tri = has_tri ? trigram<NARROW, COUNT>(B, slots, seed, h, c, cnt, aux) : 0.0;
-        const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
-        if (COUNT) ++cnt.exp;
-        list_insert<LCAP + 1>(ls, lg, sc, (uint32_t)g);
-      }
-      if (gl < k) list_insert<LCAP + 1>(ls, lg, rs, rg);   // running entry (earlier g)
-      // k rounds of group argmax over list heads (stable sort + [:k], beam.py:85)
-      double ns = -INFINITY;
-      uint32_t ng = INV;
-      nsel = 0;
-      for (int t = 0; t < k; ++t) {
-        double bs = ls[0];
-        uint32_t bg = lg[0];
-        group_argmax_fast<G>(bs, bg);
-        if (bg == INV) break;
-        if (lg[0] == bg) {
-#pragma unroll
-          for (int q = 0; q < LCAP; ++q) { ls[q] = ls[q + 1]; lg[q] = lg[q + 1]; }
-          ls[LCAP] = -INFINITY; lg[LCAP] = INV;
-        }
-        if (gl == t) { ns = bs; ng = bg; }
-        ++nsel;
-      }
-      rs = ns;
-      rg = ng;
-    }
-
-    // lanes t < nsel materialise beam[e][t] (Sequence.add, beam.py:112-116)
-    Entry ne;
-    uint32_t bpv = 0;
-    const bool writer = gl < nsel;
-    if (writer) {
-      const Exp x = decode_g((int)rg, pre, ss);
-      const int node = ss[x.j] + x.i;
-      const int so = node - A0;
-      const Cand c = so < STAGE ? read_block<G>(cst, gbase, so) : load_cand(B, nbase + (uint32_t)node);
-      const Entry& h = R[(e - x.d) % RING][x.r];
-      ne.score = rs; ne.f6 = c.f6;
-      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
-      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
-      ne.depth = h.depth + 1;
-      bpv = bp_pack((uint32_t)node, (uint32_t)x.d, (uint32_t)x.r);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (writer) {
-      R[e % RING][gl] = ne;
-      bp[(int64_t)e * bstride + gl] = bpv;
-    }
-    if (gl == 0) cntl[grp][e % RING] = nsel;
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) { pin(ssn[j]); ss[j] = ssn[j]; }
-    __builtin_amdgcn_wave_barrier();
-  }
-
-  // matures = beam[n] + EOS (beam.py:59-61); backtrace per mature rank
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const int nm = cntl[grp][n % RING];
-  if (gl == 0) p.out_count[s] = nm;
-  if (gl >= nm && gl < k) {                  // unused mature slots read as empty
-    p.out_score[(int64_t)s * k + gl] = 0.0;
-    p.out_len[(int64_t)s * k + gl] = 0;
-  }
-  if (gl < nm) {
-    const Entry& f = R[n % RING][gl];
-    const int64_t o = (int64_t)s * k + gl;
-    p.out_score[o] = f.score + 0.0;
-    p.out_len[o] = (int32_t)f.depth;
-    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)gl * n;
-    int pos = n, rank = gl;
-    for (int step = (int)f.depth - 1; step >= 0; --step) {
-      const uint32_t v = bp[(int64_t)pos * bstride + rank];
-      codes[step] = (int32_t)bp_node(v);
-      pos -= (int)bp_d(v);
-      rank = (int)bp_rank(v);
-    }
-  }
-  if (COUNT) {
-    const unsigned long long ex = group_sum<G>(cnt.exp), tu = group_sum<G>(cnt.tup),
-                             pb = group_sum<G>(cnt.probe);
-    if (gl == 0) {
-      atomicAdd(p.counters + 0, ex);
-      atomicAdd(p.counters + 1, tu);
-      atomicAdd(p.counters + 2, pb);
-    }
-  }
-}
-
-// k=1 kernel: packed lanes (default) or one 16-lane row per sentence
-// (LT_VITERBI=row16, kept for comparison).
-constexpr int P_W = 6;                  // sentences per wave, packed kernel
-
-static int viterbi_variant() {
-  static const int v = [] {
-    const char* e = std::getenv("LT_VITERBI");
-    if (e && std::strcmp(e, "row16") == 0) return 0;
-    if (e && std::strcmp(e, "pk4") == 0) return 4;
-    if (e && std::strcmp(e, "pk8") == 0) return 8;
-    if (e && std::strcmp(e, "pk5") == 0) return 5;
-    if (e && std::strcmp(e, "pk7") == 0) return 7;
-    return P_W;
-  }();
-  return v;
-}
+// k=1 kernel: W = 6 sentences per wave (4 and 5 measured within 5 % at
+// 8K-32K sentences, slower at 64K)
+constexpr int P_W = 6;
 
 template <int W, bool NARROW, bool COUNT>
-hipError_t launch_pk(const DecodeParams& p, hipStream_t st) {
+hipError_t launch_pk(const DecodeParams& p, const Launch& L) {
   constexpr int SPB = W * P_WPB;
   const int blocks = (p.n_sent + SPB - 1) / SPB;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_viterbi_pk<W, NARROW, COUNT>), dim3(blocks), dim3(256), 0, st, p);
+  hipExtLaunchKernelGGL((lt_viterbi_pk<W, NARROW, COUNT>), dim3(blocks), dim3(256), 0, L.st, L.e0, L.e1, 0, p);
   return hipGetLastError();
 }
 
@@ -1241,8 +754,8 @@ lt_beam_pk(DecodeParams p) {
   __shared__ uint32_t tgen[WPB][KT];
   constexpr bool USE_D3 = KT <= 4;              // (its 8 KiB would cost a block per CU above)
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
-  Aux aux{nullptr, nullptr, 0u, p.hk};
-  if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
+  Aux aux{nullptr, 0u, p.hk};
+  if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
@@ -1518,6 +1031,8 @@ lt_beam_pk(DecodeParams p) {
   if (lane >= nm && lane < k) {                 // unused mature slots read as empty
     p.out_score[(int64_t)s * k + lane] = 0.0;
     p.out_len[(int64_t)s * k + lane] = 0;
+    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)lane * n;
+    for (int j = 0; j < n; ++j) codes[j] = -1;
   }
   if (lane < nm) {
     const Entry& f = R[n % RING][lane];
@@ -1532,6 +1047,7 @@ lt_beam_pk(DecodeParams p) {
       pos -= (int)bp_d(v);
       rank = (int)bp_rank(v);
     }
+    for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;       // padded layout
   }
   if (COUNT) {
     const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
@@ -1545,20 +1061,11 @@ lt_beam_pk(DecodeParams p) {
 }
 
 template <int KT, int WPB, bool NARROW, bool COUNT>
-hipError_t launch_bp(const DecodeParams& p, hipStream_t st) {
+hipError_t launch_bp(const DecodeParams& p, const Launch& L) {
   const int blocks = (p.n_sent + WPB - 1) / WPB;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_beam_pk<KT, WPB, NARROW, COUNT>), dim3(blocks), dim3(64 * WPB), 0, st, p);
+  hipExtLaunchKernelGGL((lt_beam_pk<KT, WPB, NARROW, COUNT>), dim3(blocks), dim3(64 * WPB), 0, L.st, L.e0, L.e1, 0, p);
   return hipGetLastError();
-}
-
-// LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
-static bool beam_one_per_wave() {
-  static const bool v = [] {
-    const char* e = std::getenv("LT_BEAM");
-    return e && std::strcmp(e, "pk") == 0;
-  }();
-  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -1592,8 +1099,8 @@ lt_beam_hw(DecodeParams p) {
   __shared__ uint32_t tgen[WPB][S][KT];
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
-  Aux aux{nullptr, nullptr, 0u, p.hk};
-  if (USE_D3) aux = stage_aux<NARROW>(p, nullptr, d3l);
+  Aux aux{nullptr, 0u, p.hk};
+  if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
@@ -1901,6 +1408,8 @@ lt_beam_hw(DecodeParams p) {
     if (hl >= nm) {
       p.out_score[o] = 0.0;
       p.out_len[o] = 0;
+      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
+      for (int j = 0; j < n; ++j) codes[j] = -1;
     } else {
       const Entry& f = R[n % RING][hl];
       p.out_score[o] = f.score + 0.0;
@@ -1914,39 +1423,23 @@ lt_beam_hw(DecodeParams p) {
         pos -= (int)bp_d(v);
         rank = (int)bp_rank(v);
       }
+      for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;     // padded layout
     }
   }
 }
 
 template <int KT, int G, int WPB, bool NARROW>
-hipError_t launch_hw(const DecodeParams& p, hipStream_t st) {
+hipError_t launch_hw(const DecodeParams& p, const Launch& L) {
   constexpr int SPB = (64 / G) * WPB;
   const int blocks = (p.n_sent + SPB - 1) / SPB;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_beam_hw<KT, G, WPB, NARROW>), dim3(blocks), dim3(64 * WPB), 0, st, p);
+  hipExtLaunchKernelGGL((lt_beam_hw<KT, G, WPB, NARROW>), dim3(blocks), dim3(64 * WPB), 0, L.st, L.e0, L.e1, 0, p);
   return hipGetLastError();
 }
 
 // lanes per sentence of lt_beam_hw: 16 (four sentences per wave) where a
-// position has few expansions (k <= 3), else 32; LT_BEAM_G=16 / 32 forces one
-static int beam_group_lanes(int k) {
-  static const int forced = [] {
-    const char* e = std::getenv("LT_BEAM_G");
-    if (e && std::strcmp(e, "16") == 0) return 16;
-    if (e && std::strcmp(e, "32") == 0) return 32;
-    return 0;
-  }();
-  return forced ? forced : (k <= 3 ? 16 : 32);
-}
-
-
-static bool beam_v1() {
-  static const bool v = [] {
-    const char* e = std::getenv("LT_BEAM");
-    return e && std::strcmp(e, "v1") == 0;
-  }();
-  return v;
-}
+// position has few expansions (k <= 3), else 32
+static int beam_group_lanes(int k) { return k <= 3 ? 16 : 32; }
 
 // ===========================================================================
 // Batch evaluate (BeamScoreFunctions.evaluate, score_funcs.py:44-48)
@@ -1958,7 +1451,7 @@ static bool beam_v1() {
 template <bool NARROW>
 __global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
   __shared__ double d3l[D3_DIM * D3_DIM];
-  Aux aux{nullptr, nullptr, p.d3mul, p.hk};
+  Aux aux{nullptr, p.d3mul, p.hk};
   if (p.d3) {
     const uint4* src = reinterpret_cast<const uint4*>(p.d3);
     uint4* dst = reinterpret_cast<uint4*>(d3l);
@@ -2010,31 +1503,6 @@ __global__ void __launch_bounds__(256) lt_eval_paths_k(EvalParams p) {
   p.out[s] = total;
 }
 
-template <bool NARROW, bool COUNT>
-hipError_t launch_v(const DecodeParams& p, hipStream_t st) {
-  switch (viterbi_variant()) {
-    case 4: return launch_pk<4, NARROW, COUNT>(p, st);
-    case 5: return launch_pk<5, NARROW, COUNT>(p, st);
-    case 6: return launch_pk<6, NARROW, COUNT>(p, st);
-    case 7: return launch_pk<7, NARROW, COUNT>(p, st);
-    case 8: return launch_pk<8, NARROW, COUNT>(p, st);
-    default: break;
-  }
-  const int blocks = (p.n_sent + V_SPB - 1) / V_SPB;
-  if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_viterbi_k<NARROW, COUNT>), dim3(blocks), dim3(256), 0, st, p);
-  return hipGetLastError();
-}
-
-template <int KT, int G, bool NARROW, bool COUNT>
-hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
-  constexpr int SPB = 256 / G;
-  const int blocks = (p.n_sent + SPB - 1) / SPB;
-  if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_beam_k<KT, G, NARROW, COUNT>), dim3(blocks), dim3(256), 0, st, p);
-  return hipGetLastError();
-}
-
 #ifndef HW_WPB
 #define HW_WPB 4                        // waves per block of lt_beam_hw
 #endif
@@ -2046,42 +1514,31 @@ hipError_t launch_b(const DecodeParams& p, hipStream_t st) {
 #endif
 
 template <bool NARROW, bool COUNT>
-hipError_t launch_k(const DecodeParams& p, int kt, hipStream_t st) {
-  // lane groups (beam_group_lanes: 16 lanes for k <= 3, 32 above) for k = 2..8;
-  // LT_BEAM=pk: one sentence per wave for every beam (A/B runs)
-  if (!COUNT && !beam_v1() && !beam_one_per_wave() && kt <= 8) {
+hipError_t launch_k(const DecodeParams& p, int kt, const Launch& L) {
+  if (kt == 1) return launch_pk<P_W, NARROW, COUNT>(p, L);
+  // k = 2..8: lane groups (16 lanes for k <= 3, 32 above); the operation
+  // counts of those beams come from lt_beam_pk's COUNT variant (one sentence
+  // per wave, same enumeration), which lt_beam_hw does not have
+  if (!COUNT && kt <= 8) {
     if (beam_group_lanes(p.k) == 16) {
       switch (kt) {
-        case 2: return launch_hw<2, 16, HW_WPB, NARROW>(p, st);
-        case 4: return launch_hw<4, 16, HW_WPB, NARROW>(p, st);
-        case 8: return launch_hw<8, 16, HW_WPB, NARROW>(p, st);
+        case 2: return launch_hw<2, 16, HW_WPB, NARROW>(p, L);
+        case 4: return launch_hw<4, 16, HW_WPB, NARROW>(p, L);
         default: break;
       }
     }
     switch (kt) {
-      case 2: return launch_hw<2, 32, HW_WPB, NARROW>(p, st);
-      case 4: return launch_hw<4, 32, HW_WPB, NARROW>(p, st);
-      case 8: return launch_hw<8, 32, HW_WPB, NARROW>(p, st);
-      default: break;
-    }
-  }
-  if (kt > 1 && !beam_v1()) {
-    switch (kt) {
-      case 2: return launch_bp<2, 4, NARROW, COUNT>(p, st);
-      case 4: return launch_bp<4, 4, NARROW, COUNT>(p, st);
-      case 8: return launch_bp<8, 4, NARROW, COUNT>(p, st);
-      case 16: return launch_bp<16, BP16_WPB, NARROW, COUNT>(p, st);
-      case 32: return launch_bp<32, BP32_WPB, NARROW, COUNT>(p, st);
+      case 4: return launch_hw<4, 32, HW_WPB, NARROW>(p, L);
+      case 8: return launch_hw<8, 32, HW_WPB, NARROW>(p, L);
       default: return hipErrorInvalidValue;
     }
   }
   switch (kt) {
-    case 1: return launch_v<NARROW, COUNT>(p, st);
-    case 2: return launch_b<2, 32, NARROW, COUNT>(p, st);
-    case 4: return launch_b<4, 32, NARROW, COUNT>(p, st);
-    case 8: return launch_b<8, 64, NARROW, COUNT>(p, st);
-    case 16: return launch_b<16, 64, NARROW, COUNT>(p, st);
-    case 32: return launch_b<32, 64, NARROW, COUNT>(p, st);
+    case 2: return launch_bp<2, 4, NARROW, COUNT>(p, L);
+    case 4: return launch_bp<4, 4, NARROW, COUNT>(p, L);
+    case 8: return launch_bp<8, 4, NARROW, COUNT>(p, L);
+    case 16: return launch_bp<16, BP16_WPB, NARROW, COUNT>(p, L);
+    case 32: return launch_bp<32, BP32_WPB, NARROW, COUNT>(p, L);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2108,12 +1565,8 @@ hipError_t launch_evaluate(const EvalParams& p, hipStream_t st) {
 const char* kernel_name_for(int k) {
   const int kt = beam_template_for(k);
   if (kt < 0) return nullptr;
-  if (kt > 1) {
-    if (beam_v1()) return "lt_beam_k";
-    if (beam_one_per_wave()) return "lt_beam_pk";
-    return kt <= 8 ? "lt_beam_hw" : "lt_beam_pk";
-  }
-  return viterbi_variant() == 0 ? "lt_viterbi_k" : "lt_viterbi_pk";
+  if (kt == 1) return "lt_viterbi_pk";
+  return kt <= 8 ? "lt_beam_hw" : "lt_beam_pk";
 }
 
 int beam_template_for(int k) {
@@ -2126,11 +1579,19 @@ int beam_template_for(int k) {
   return -1;
 }
 
-hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count) {
+hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipEvent_t e0, hipEvent_t e1) {
   const int kt = beam_template_for(p.k);
+  // the timing events ride on the kernel's dispatch (no extra stream
+  // commands between back-to-back decodes); an empty batch launches nothing
+  if (p.n_sent == 0) {
+    hipError_t e = e0 ? hipEventRecord(e0, st) : hipSuccess;
+    if (e == hipSuccess && e1) e = hipEventRecord(e1, st);
+    return e;
+  }
+  const Launch L{st, e0, e1};
   if (p.narrow)
-    return count ? launch_k<true, true>(p, kt, st) : launch_k<true, false>(p, kt, st);
-  return count ? launch_k<false, true>(p, kt, st) : launch_k<false, false>(p, kt, st);
+    return count ? launch_k<true, true>(p, kt, L) : launch_k<true, false>(p, kt, L);
+  return count ? launch_k<false, true>(p, kt, L) : launch_k<false, false>(p, kt, L);
 }
 
 }  // namespace lt

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "lt_common.h"
+#include "lt_internal.h"
 
 // One batch's device buffers (one hipMalloc) and pinned result buffers (one
 // hipHostMalloc), carved into the lt_batch pointers.  lt_batch_destroy hands
@@ -23,10 +24,16 @@ struct lt_arena {
 
 struct lt_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;    // decodes, result copies, gathers
+  hipStream_t stream = nullptr;    // decodes, gather staging copies
   hipStream_t ustream = nullptr;   // lt_batch_create's uploads (a pipeline's upload
                                    // thread does not queue behind the decodes)
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipStream_t cstream = nullptr;   // result copies to the host: the D2H of decode i
+                                   // runs under decode i+1 (lt_result_fetch)
+  // start / end events of the last KRING decode launches (lt_kernel_ms_recent)
+  static constexpr int KRING = 64;
+  hipEvent_t kev0[KRING] = {}, kev1[KRING] = {};
+  int64_t n_launch = 0;            // timed decode launches (KRING index)
+  int64_t n_serial = 0;            // every decode-kernel launch (result slot freshness)
   unsigned long long* d_counters = nullptr;
   std::mutex mu;                   // spare (batches are created and destroyed on several threads)
   std::vector<lt_arena> spare;     // arenas of destroyed batches, kept for reuse
@@ -44,15 +51,40 @@ struct lt_batch {
   double* d_post = nullptr;
   // scratch + device results (sized for max_k)
   uint32_t* d_bp = nullptr;
+  // two result slots: decodes alternate between them, so the D2H of one
+  // decode's results (lt_result_fetch, copy stream) overlaps the next decode
+  struct Slot {
+    int32_t *count = nullptr, *len = nullptr, *codes = nullptr;
+    double* score = nullptr;
+    void* slab = nullptr;             // the slot's results packed (lt_results.hip)
+    int64_t packed_launch = -1;       // launch_serial of the decode the slab holds
+  } res[2];
+  int64_t launch_serial = -1;         // lt_ctx::n_serial of the last decode
+  uint64_t slab_cap = 0;              // slab capacity at max_k (+ pack scratch behind it)
+  char* h_slab = nullptr;             // pinned: the last lt_result_fetch_packed
+  int cur = 1;                        // slot of the last decode (the first decode takes slot 0)
+  hipEvent_t last_end = nullptr;      // end event of the last decode (a lt_ctx::kev1), or NULL
+  // readers of result slot i on other streams (RD_COPY: the ctx copy stream,
+  // RD_GATHER: a communicator's stream); a decode reusing slot i waits for them
+  static constexpr int RD_COPY = 0, RD_GATHER = 1;
+  hipEvent_t ev_rd[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  bool rd_pending[2][2] = {{false, false}, {false, false}};
+  // the last decode's slot (what lt_gather_launch and lt_result_fetch read)
   int32_t *d_count = nullptr, *d_len = nullptr, *d_codes = nullptr;
   double* d_score = nullptr;
   // pinned host results
   int32_t *h_count = nullptr, *h_len = nullptr, *h_codes = nullptr;
   double* h_score = nullptr;
-  // component frequencies of the batch's nodes (ids < 2^20) and the hot table
-  // built for the last model decoded with this batch
-  std::vector<uint32_t> f_word, f_tag, f_morph;
-  uint64_t hot_uid = 0;      // lt_model::uid the hot table was built for (0: none)
-  lt::SlotN* d_hot = nullptr;
   lt_arena arena;
 };
+
+namespace lt {
+// Bytes of a slab buffer for n_sent sentences, beam k, `chars` characters:
+// the slab's capacity plus the packing scratch behind it.
+uint64_t slab_alloc_bytes(int64_t n_sent, int k, int64_t chars);
+// Stream `st` (another stream of b's ctx) waits until the last decode of b
+// is complete, and starts reading its result slot: packs it into `slab`
+// (slab_alloc_bytes(b->n_sent, b->last_k, b->total_chars) bytes) and records
+// that `reader` (lt_batch::RD_*) is done with the slot at that point of st.
+hipError_t pack_last_results_on(lt_batch* b, int reader, void* slab, hipStream_t st);
+}  // namespace lt

@@ -12,7 +12,6 @@ struct DecodeParams {
   uint32_t slots;
   uint32_t seed;
   NarrowHash hk;                // narrow tables: slot hash constants (from seed)
-  const SlotN* hot;             // HOT_SLOTS-slot LDS hot table (narrow only) or NULL
   const double* d3;             // dense class-3 table (D3_DIM^2) or NULL
   uint32_t d3mul;
   int32_t narrow;               // 1: SlotN, 0: SlotW
@@ -67,8 +66,62 @@ struct EvalParams {
 };
 hipError_t launch_evaluate(const EvalParams& p, hipStream_t st);
 
+// ---- compact results ("slabs", lt_results.hip; lattice_decode.h) ----------
+struct SlabHeader {
+  int32_t n_sent;
+  int32_t k;
+  int64_t n_codes;              // path codes in the slab
+  int64_t bytes;                // used bytes (header included)
+  int64_t reserved;
+};
+static_assert(sizeof(SlabHeader) == 32, "slab header is 32 B");
+
+__host__ __device__ inline uint64_t al16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
+
+// Section offsets of a slab of n_sent sentences, beam k, and its capacity
+// for `chars` characters (a path of a sentence of n characters has <= n words).
+struct SlabLayout {
+  uint64_t count, len, score, codes, capacity;
+};
+__host__ __device__ inline SlabLayout slab_layout(int64_t n_sent, int k, int64_t chars) {
+  SlabLayout L;
+  L.count = sizeof(SlabHeader);
+  L.len = L.count + al16(4 * (uint64_t)n_sent);
+  L.score = L.len + al16(4 * (uint64_t)n_sent * k);
+  L.codes = L.score + al16(8 * (uint64_t)n_sent * k);
+  L.capacity = L.codes + al16(4 * (uint64_t)chars * k);
+  return L;
+}
+__host__ __device__ inline uint64_t slab_used_bytes(const SlabLayout& L, int64_t n_codes) {
+  return L.codes + al16(4 * (uint64_t)n_codes);
+}
+
+struct ResultsPackParams {
+  // the decode's padded results (device)
+  const int32_t* count;
+  const int32_t* len;
+  const double* score;
+  const int32_t* codes;
+  const int32_t* sent_n;
+  const int64_t* cum_n;
+  int32_t n_sent;
+  int32_t k;
+  int64_t n_entries;            // n_sent * k
+  int64_t n_blocks;             // pack_blocks(n_entries)
+  int64_t* block_sum;           // [n_blocks] scratch
+  SlabLayout lay;
+  void* slab;                   // device, lay.capacity bytes
+};
+int64_t pack_blocks(int64_t n_entries);
+hipError_t launch_pack_results(const ResultsPackParams& p, hipStream_t st);
+// Copies the used bytes of a device slab (its header says how many) into
+// pinned host memory of `capacity` bytes.
+hipError_t launch_slab_to_host(const void* slab, void* host, size_t capacity, hipStream_t st);
+
 int beam_template_for(int k);
 const char* kernel_name_for(int k);
-hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count);
+// e0 / e1 (may be NULL): events recorded at the start / end of the kernel.
+hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipEvent_t e0 = nullptr,
+                         hipEvent_t e1 = nullptr);
 
 }  // namespace lt

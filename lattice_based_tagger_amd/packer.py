@@ -62,20 +62,53 @@ class PackedBatch:
             out[f] = getattr(self, f)[n0:n1]
         return PackedBatch(**out)
 
-    def split(self, max_nodes):
-        """[(s0, s1)] sentence ranges of at most max_nodes nodes each (a single
-        larger sentence gets a range of its own)."""
+    # backpointer bytes of one launch: lt_batch_create takes sum_s (n_s + 1) * k
+    # 4-byte slots below 2^31 B
+    MAX_BP_BYTES = (1 << 31) - 1
+
+    def split(self, max_nodes, k=1):
+        """[(s0, s1)] sentence ranges that fit one launch each: at most
+        max_nodes nodes and fewer than 2^31 B of beam-k backpointers (a
+        single larger sentence gets a range of its own)."""
         S = self.n_sent
         if S == 0:
             return [(0, 0)]
         cuts, s0 = [], 0
         off = self.sent_node_off
+        bp = np.zeros(S + 1, dtype=np.int64)
+        np.cumsum((np.asarray(self.sent_n, dtype=np.int64) + 1) * (4 * max(int(k), 1)), out=bp[1:])
         while s0 < S:
             s1 = int(np.searchsorted(off, off[s0] + max_nodes, side='right')) - 1
-            s1 = min(max(s1, s0 + 1), S)
+            s1b = int(np.searchsorted(bp, bp[s0] + self.MAX_BP_BYTES, side='right')) - 1
+            s1 = min(max(min(s1, s1b), s0 + 1), S)
             cuts.append((s0, s1))
             s0 = s1
         return cuts
+
+    def take(self, order):
+        """Sentences ``order`` (indices, repeats allowed) as a new batch, in
+        that order (copies; offsets rebuilt)."""
+        order = np.asarray(order, dtype=np.int64)
+        n_nodes = np.diff(self.sent_node_off)[order]
+        n_span = np.diff(self.sent_span_off)[order]
+        node_off = np.zeros(len(order) + 1, dtype=np.int64)
+        np.cumsum(n_nodes, out=node_off[1:])
+        span_off = np.zeros(len(order) + 1, dtype=np.int64)
+        np.cumsum(n_span, out=span_off[1:])
+
+        def gather_index(src_off, counts, dst_off):
+            total = int(dst_off[-1])
+            seg = np.repeat(np.arange(len(order), dtype=np.int64), counts)
+            return src_off[order][seg] + (np.arange(total, dtype=np.int64) - dst_off[seg])
+        ni = gather_index(self.sent_node_off[:-1], n_nodes, node_off)
+        si = gather_index(self.sent_span_off[:-1], n_span, span_off)
+        out = dict(max_len=self.max_len, n_post=self.n_post, has_trigram=self.has_trigram,
+                   sent_n=self.sent_n[order], sent_node_off=node_off, sent_span_off=span_off,
+                   span_start=self.span_start[si],
+                   node_post=self.node_post[:, ni] if self.n_post else np.zeros((0, len(ni))))
+        for f in self.NODE_FIELDS:
+            out[f] = getattr(self, f)[ni]
+        return PackedBatch(**out)
 
 
 def _span_candidates(bindex_b, b, n, max_len):

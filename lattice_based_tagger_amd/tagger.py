@@ -105,7 +105,10 @@ class Tagger:
                     ``dictionary`` with its defaults, as the reference does
                     (`tagger.py:60`)
     ``score_funcs`` a ``BeamScoreFunctions`` composite (reference or mirror)
-    ``device``      HIP device ordinal of the decoder
+    ``device``      HIP device ordinal of the decoder, or a sequence of
+                    ordinals: ``tag_batch`` then deals its chunks to the
+                    devices in turn (one context per entry; results in
+                    input order)
     ``lexicon``     a prebuilt ``lookup.NativeLexicon`` (optional; used as
                     given -- the caller rebuilds it after changing the
                     dictionary)
@@ -209,7 +212,7 @@ class Tagger:
     def _tag_native(self, lex, sents, beam_size):
         from collections import deque
         from concurrent.futures import ThreadPoolExecutor
-        from .beam import Decoder, _check_beam, decode_batch, lowered_model
+        from .beam import _check_beam, decode_batch, decoders_for, device_list, lowered_model
         from .native_packer import packer_for
         k = _check_beam(beam_size)
         chunks = [sents[i:i + self.CHUNK] for i in range(0, len(sents), self.CHUNK)] or [[]]
@@ -224,10 +227,14 @@ class Tagger:
         lat0 = lookup(chunks[0])                   # (the reference raises before scoring)
         model = lowered_model(self.score_funcs)
         npk = packer_for(model)
-        dec = None
+        decs = None
         if npk is not None and k > 0:
-            dec = Decoder.get(self.device)
-            dec.device_model(model)                # built here, before any worker uses it
+            decs = decoders_for(device_list(self.device))
+            for dec in decs:                       # built here, before any worker uses it
+                dec.device_model(model)
+
+        def decoder(i):                            # chunk i's device
+            return decs[i % len(decs)] if decs else None
 
         def front(chunk, lat=None):
             lat = lat if lat is not None else lookup(chunk)
@@ -236,8 +243,9 @@ class Tagger:
             packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
             return lat, packed, views
 
-        def upload(fut):
+        def upload(i, fut):
             lat, packed, views = fut.result()
+            dec = decoder(i)
             dbs = dec.upload(model, packed, k) if dec is not None and packed is not None else None
             return lat, packed, views, dbs
 
@@ -246,12 +254,13 @@ class Tagger:
                 lattices = [(lat.bindex(s), lat.chars[s]) for s in range(len(chunks[i]))]
                 matures = beam_search_batch(lattices, self.score_funcs, beam_size=k, device=self.device)
             else:
-                matures = decode_batch(packed, views, lat.chars, model, k, self.device,
-                                       best_only=True, uploaded=dbs)
+                matures = decode_batch(packed, views, lat.chars, model, k, best_only=True,
+                                       uploaded=dbs, decoder=decoder(i))
             return [m[0] for m in matures]
 
         if len(chunks) == 1:                       # nothing to overlap (Tagger.tag): no worker threads
             lat, packed, views = front(chunks[0], lat0)
+            dec = decoder(0)
             dbs = dec.upload(model, packed, k) if dec is not None and packed is not None else None
             return finish(0, lat, packed, views, dbs)
 
@@ -261,8 +270,8 @@ class Tagger:
 
             def feed(i):
                 if i < len(chunks):
-                    stages.append(uploader.submit(upload, builder.submit(front, chunks[i],
-                                                                         lat0 if i == 0 else None)))
+                    stages.append(uploader.submit(upload, i, builder.submit(front, chunks[i],
+                                                                            lat0 if i == 0 else None)))
             feed(0)
             feed(1)
             try:

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     lib = _capi.load()
-    assert lib.lt_abi_version() == 1
+    assert lib.lt_abi_version() == 2
     assert lib.lt_device_count() >= 0
 
 
@@ -41,7 +41,11 @@ def test_kernels_are_gfx950_code_objects():
     lib = _build.build(verbose=False)
     blob = open(lib, 'rb').read()
     assert b'amdgcn-amd-amdhsa--gfx950' in blob
-    assert b'lt_viterbi_k' in blob and b'lt_beam_k' in blob
+    # the shipping kernels, and only those (the superseded lt_viterbi_k /
+    # lt_beam_k of round 1 are gone)
+    for name in (b'lt_viterbi_pk', b'lt_beam_hw', b'lt_beam_pk', b'lt_pack_write_k', b'lt_slab_to_host_k'):
+        assert name in blob, name
+    assert b'lt_viterbi_k' not in blob and b'lt_beam_k' not in blob
 
 
 def test_context_without_gpu_fails_loudly():
