@@ -404,8 +404,21 @@ def main():
         assert all(np.array_equal(x, y) for x, y in zip(mine_pk.padded(piece.sent_n), mine)), \
             'packed results differ from the padded results of the same decode'
     if root and got is not None and not a.no_check:
-        check = result_check(got, strong, d.world, comm is not None, packed, order, ctx, dm, k,
-                             a.sentences)
+        ref_db = _capi.DeviceBatch(ctx, packed, max_k=k)            # the whole (base) batch here
+        ref = ref_db.decode_packed(dm, k)
+        ref_db.close()
+        base_idx = np.arange(packed.n_sent) if order is None else order
+        if strong and comm:                  # every rank's shard: the whole batch
+            check_results(got, ref, base_idx)
+            what = 'all %d sentences of the batch, gathered from %d ranks over RCCL' % (a.sentences, d.world)
+        elif strong:                         # this rank's shard only (no gather)
+            check_results(got, ref, base_idx[lo:hi])
+            what = 'rank 0 shard [%d, %d) of the batch (no gather)' % (lo, hi)
+        else:                                # weak: rank 0's own batch, other blocks complete
+            check_results(got[:1], ref, base_idx, (got, a.sentences) if comm else None)
+            what = 'rank 0 batch of %d sentences%s' % (a.sentences, ', %d gathered blocks complete'
+                                                        % len(got) if comm else '')
+        check = {'what': what + ': equal to a single-process decode byte for byte', 'ok': True}
     count, length = mine[0], mine[1]
     kernel = (lib.lt_kernel_name(k) or b'?').decode()
     traffic = traffic_from_profiles(kernel, k, piece.n_sent, a.features, a.seed) \
@@ -529,41 +542,31 @@ def dict_nodes(raw, order, lo, hi):
     return int(per[lo:hi].sum() if order is None else per[order[lo:hi]].sum())
 
 
-def result_check(got, strong, world, gathered, packed, order, ctx, dm, k, total):
-    """Rank 0: the results delivered to the host by the timed region's last
-    step, against a single-process decode of the (base) batch on this GPU."""
-    ref_db = _capi.DeviceBatch(ctx, packed, max_k=k)
-    ref = ref_db.decode_packed(dm, k)
-    ref_db.close()
-    if strong:
-        from lattice_based_tagger_amd.beam import concat_results
-        whole = concat_results(got)
-        idx = np.arange(packed.n_sent) if order is None else order
-        assert whole.n_sent == total, 'gathered %d of %d sentences' % (whole.n_sent, total)
-        exp_count = ref.count[idx]
-        exp_len = ref.length[idx]
-        exp_score = ref.score[idx]
-        L = ref.length.ravel().astype(np.int64)
-        sel = (idx[:, None] * k + np.arange(k)[None, :]).ravel()
-        seg = np.repeat(sel, L[sel])
-        first = np.repeat(np.cumsum(L[sel]) - L[sel], L[sel])
-        within = np.arange(int(L[sel].sum())) - first
-        exp_codes = ref.codes[ref.off[seg] + within]
-        ok = (np.array_equal(whole.count, exp_count) and np.array_equal(whole.length, exp_len) and
-              np.array_equal(whole.score.view(np.uint64), exp_score.view(np.uint64)) and
-              np.array_equal(whole.codes, exp_codes))
-        assert ok, 'reassembled results differ from the single-process decode'
-        return {'what': 'all %d sentences from %d rank(s)%s equal a single-process decode of the '
-                        'batch byte for byte' % (total, world, ' (RCCL gather)' if gathered else ''),
-                'ok': True}
-    g0 = got[0]
-    ok = all(np.array_equal(x.view(np.uint8), y.view(np.uint8))
-             for x, y in zip((g0.count, g0.length, g0.score, g0.codes),
-                             (ref.count, ref.length, ref.score, ref.codes)))
-    assert ok, 'rank-0 results differ from its single-process decode'
-    assert all(g.n_sent == packed.n_sent for g in got), 'gathered result blocks incomplete'
-    return {'what': 'rank 0 results equal its single-process decode; %d complete blocks' % len(got),
-            'ok': True}
+def check_results(got, ref, idx, n_blocks_complete=None):
+    """Rank 0: results delivered to the host by the timed region's last step
+    -- ``got``: PackedResults blocks, consecutive in the batch -- against
+    ``ref``, a single-process decode of the generated (base) batch; ``idx``:
+    the base sentence of every row of the concatenated blocks.
+    ``n_blocks_complete``: (blocks, sentences each) that must be complete
+    besides (weak scaling: the other ranks' batches)."""
+    from lattice_based_tagger_amd.beam import concat_results
+    whole = concat_results(got)
+    idx = np.asarray(idx, dtype=np.int64)
+    assert whole.n_sent == len(idx), 'got %d of %d sentences' % (whole.n_sent, len(idx))
+    k = ref.k
+    L = ref.length.ravel().astype(np.int64)
+    sel = (idx[:, None] * k + np.arange(k)[None, :]).ravel()
+    seg = np.repeat(sel, L[sel])
+    first = np.repeat(np.cumsum(L[sel]) - L[sel], L[sel])
+    exp_codes = ref.codes[ref.off[seg] + np.arange(int(L[sel].sum())) - first]
+    ok = (np.array_equal(whole.count, ref.count[idx]) and np.array_equal(whole.length, ref.length[idx]) and
+          np.array_equal(whole.score.view(np.uint64), ref.score[idx].view(np.uint64)) and
+          np.array_equal(whole.codes, exp_codes))
+    assert ok, 'results differ from the single-process decode'
+    if n_blocks_complete:
+        blocks, each = n_blocks_complete
+        assert len(blocks) and all(b.n_sent == each for b in blocks), 'gathered result blocks incomplete'
+    return True
 
 
 if __name__ == '__main__':

@@ -141,6 +141,15 @@ lt_status lt_batch_create(lt_ctx* ctx, const lt_batch_desc* desc, int max_k, lt_
 lt_status lt_batch_destroy(lt_batch* batch);
 /* Total path-code slots of the results for beam k: k * sum_s n_s. */
 int64_t lt_batch_code_slots(const lt_batch* batch, int k);
+/* Kernel launches per decode of the batch: a batch of any size is decoded in
+ * consecutive sentence pieces whose node records and backpointers each stay
+ * below 2^31 B (32-bit buffer offsets in the kernels); all pieces write the
+ * one result array. */
+int32_t lt_batch_pieces(const lt_batch* batch);
+/* Test hook: launch pieces of batches created afterwards hold at most
+ * `bytes` of node records / backpointers (bytes < 1: the 2^31 - 1 default);
+ * returns the previous limit.  Process-wide. */
+int64_t lt_set_piece_bytes(int64_t bytes);
 
 /* ---- decode ---------------------------------------------------------------
  * Replaces beam_search(bindex, chars, score_functions, beam_size=k, max_len)

@@ -21,7 +21,7 @@ _STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED
 EXPORTED_SYMBOLS = (
     'lt_abi_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
     'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
-    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_decode_launch', 'lt_last_kernel_ms',
+    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_batch_pieces', 'lt_set_piece_bytes', 'lt_decode_launch', 'lt_last_kernel_ms',
     'lt_kernel_ms_recent', 'lt_kernel_name',
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
     'lt_result_fetch_packed', 'lt_result_view_packed', 'lt_slab_parse',
@@ -137,6 +137,8 @@ def load(path=None):
             'lt_batch_create': (i32, [vp, C.POINTER(BatchDesc), C.c_int, C.POINTER(vp)]),
             'lt_batch_destroy': (i32, [vp]),
             'lt_batch_code_slots': (i64, [vp, C.c_int]),
+            'lt_batch_pieces': (i32, [vp]),
+            'lt_set_piece_bytes': (i64, [i64]),
             'lt_decode_launch': (i32, [vp, vp, vp, C.c_int]),
             'lt_last_kernel_ms': (i32, [vp, C.POINTER(C.c_float)]),
             'lt_kernel_ms_recent': (i32, [vp, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
@@ -356,6 +358,11 @@ class DeviceBatch:
         self.handle = h
         self.ctx = ctx
         self.max_k = int(max_k)
+
+    @property
+    def pieces(self):
+        """Kernel launches per decode (lattice_decode.h lt_batch_pieces)."""
+        return int(self.ctx._lib.lt_batch_pieces(self.handle))
 
     def launch(self, model, k):
         check(self.ctx._lib.held.lt_decode_launch(self.ctx.handle, model.handle, self.handle, int(k)))

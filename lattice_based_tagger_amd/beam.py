@@ -144,60 +144,26 @@ class Decoder:
             model._device_models[self.key] = dm
         return dm
 
-    # node records per launch (lt_batch_create takes < 2^31 B of 48 B records)
-    MAX_NODES = 40_000_000
-
     def upload(self, model, packed, k):
-        """Device batches of a PackedBatch, one per launch piece
-        (``PackedBatch.split``), as (s0, s1, DeviceBatch).  Safe from a worker
-        thread while this thread's caller decodes (lt_batch_create only
-        queues copies on the context's upload stream), so uploads overlap
-        decodes."""
-        out = []
-        try:
-            for s0, s1 in packed.split(self.MAX_NODES, k):
-                piece = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
-                out.append((s0, s1, _capi.DeviceBatch(self.ctx, piece, max_k=k)))
-        except BaseException:
-            for _, _, db in out:
-                db.close()
-            raise
-        return out
+        """The PackedBatch on the device, as [(0, n_sent, DeviceBatch)] (a
+        batch of any size: the library decodes it in launch pieces).  Safe
+        from a worker thread while this thread's caller decodes
+        (lt_batch_create only queues copies on the context's upload
+        stream), so uploads overlap decodes."""
+        return [(0, packed.n_sent, _capi.DeviceBatch(self.ctx, packed, max_k=k))]
 
     def decode_packed(self, model, packed, k, uploaded=None):
-        """Decode a PackedBatch (in launch pieces of ``PackedBatch.split``, or
-        the pieces ``upload`` made of it); returns the batch's
-        ``_capi.PackedResults``.  Pieces pipeline: piece i+1 is uploaded
-        while piece i decodes."""
+        """Decode a PackedBatch (or the device batches ``upload`` made of
+        it); returns the batch's ``_capi.PackedResults``."""
         dm = self.device_model(model)
-        if uploaded is not None:
-            pieces = [db for _, _, db in uploaded]
-            todo = []
-        else:
-            pieces = []
-            todo = packed.split(self.MAX_NODES, k)
-
-        def up(rng):
-            s0, s1 = rng
-            sub = packed if (s0, s1) == (0, packed.n_sent) else packed.slice(s0, s1)
-            return _capi.DeviceBatch(self.ctx, sub, max_k=k)
+        dbs = [db for _, _, db in uploaded] if uploaded is not None else \
+            [_capi.DeviceBatch(self.ctx, packed, max_k=k)]
         parts = []
         try:
-            if todo:
-                pieces.append(up(todo[0]))
-            i = 0
-            while i < len(pieces):
-                db = pieces[i]
-                db.launch(dm, k)
-                db.fetch_packed()
-                if i + 1 < len(todo):
-                    pieces.append(up(todo[i + 1]))      # H2D under this decode
-                self.ctx.sync()
-                parts.append(db.results_packed())
-                db.close()
-                i += 1
+            for db in dbs:
+                parts.append(db.decode_packed(dm, k))
         finally:
-            for db in pieces:
+            for db in dbs:
                 db.close()
         return concat_results(parts)
 

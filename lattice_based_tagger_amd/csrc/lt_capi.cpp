@@ -467,9 +467,6 @@ static lt_status validate(const lt_batch_desc* d) {
                          !d->node_pre || !d->node_f4 || !d->node_f5 || !d->node_f6))
     return fail(LT_EINVAL, "batch: NULL node arrays");
   if (d->n_post > 0 && !d->node_post) return fail(LT_EINVAL, "batch: NULL node_post");
-  if (d->n_nodes * (int64_t)sizeof(NodeRec) >= ((int64_t)1 << 31))
-    return fail(LT_EUNSUPPORTED, "batch: %lld nodes exceed one launch (2^31 B of node records); split the batch",
-                (long long)d->n_nodes);
   if (d->n_span > 0 && !d->span_start) return fail(LT_EINVAL, "batch: NULL span_start");
   if (d->sent_node_off[0] != 0 || d->sent_span_off[0] != 0)
     return fail(LT_EINVAL, "batch: offsets must start at 0");
@@ -630,6 +627,32 @@ static T* at(char* base, size_t off) {
 }
 }  // extern "C++"
 
+// Launch pieces: consecutive sentence ranges whose node records and
+// backpointers each stay below 2^31 B (the kernels address them with 32-bit
+// buffer offsets).  A batch of any size is decoded as one launch per piece,
+// all writing one result array.
+static std::atomic<int64_t> g_piece_bytes{((int64_t)1 << 31) - 1};
+
+static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc* d, int max_k) {
+  const int64_t lim = g_piece_bytes.load();
+  std::vector<std::pair<int32_t, int32_t>> out;
+  int32_t s0 = 0;
+  int64_t nodes = 0, bp = 0;
+  for (int32_t s = 0; s < d->n_sent; ++s) {
+    const int64_t sn = (d->sent_node_off[s + 1] - d->sent_node_off[s]) * (int64_t)sizeof(NodeRec);
+    const int64_t sb = ((int64_t)d->sent_n[s] + 1) * max_k * 4;
+    if (s > s0 && (nodes + sn > lim || bp + sb > lim)) {
+      out.emplace_back(s0, s);
+      s0 = s;
+      nodes = bp = 0;
+    }
+    nodes += sn;
+    bp += sb;
+  }
+  if (d->n_sent > s0 || out.empty()) out.emplace_back(s0, d->n_sent);
+  return out;
+}
+
 lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch** out) {
   if (!c || !d || !out) return fail(LT_EINVAL, "lt_batch_create: NULL argument");
   *out = nullptr;
@@ -650,39 +673,64 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   b->n_span = d->n_span;
 
   const int32_t S = d->n_sent;
-  std::vector<int32_t> order(S);
-  std::vector<int64_t> bp_off(S + 1), cum_n(S + 1);
-  for (int32_t s = 0; s < S; ++s) order[s] = s;
-  // longest sentences first: the grid drains evenly
-  std::stable_sort(order.begin(), order.end(),
-                   [&](int32_t x, int32_t y) { return d->sent_n[x] > d->sent_n[y]; });
-  bp_off[0] = 0;
+  std::vector<int64_t> cum_n(S + 1);
   cum_n[0] = 0;
-  for (int32_t s = 0; s < S; ++s) {
-    bp_off[s + 1] = bp_off[s] + (int64_t)(d->sent_n[s] + 1) * max_k;
-    cum_n[s + 1] = cum_n[s] + d->sent_n[s];
-  }
+  for (int32_t s = 0; s < S; ++s) cum_n[s + 1] = cum_n[s] + d->sent_n[s];
   b->total_chars = cum_n[S];
-  b->bp_entries = bp_off[S];
-  if (b->bp_entries * 4 >= ((int64_t)1 << 31)) {
-    const long long slots = (long long)b->bp_entries;
-    delete b;
-    return fail(LT_EUNSUPPORTED, "lt_batch_create: %lld backpointer slots exceed one launch (2^31 B); split the batch",
-                slots);
+  const auto ranges = piece_ranges(d, max_k);
+  const size_t P = ranges.size();
+  b->pieces.resize(P);
+  // per piece: local sentence order (longest first: the grid drains
+  // evenly), offsets rebased to the piece
+  std::vector<std::vector<int32_t>> order(P);
+  std::vector<std::vector<int64_t>> node_off(P), span_off(P), bp_off(P), pcum(P);
+  for (size_t q = 0; q < P; ++q) {
+    lt_piece& pc = b->pieces[q];
+    const int32_t s0 = ranges[q].first, s1 = ranges[q].second, n = s1 - s0;
+    pc.s0 = s0;
+    pc.n_sent = n;
+    pc.node0 = d->sent_node_off[s0];
+    pc.span0 = d->sent_span_off[s0];
+    pc.n_nodes = d->sent_node_off[s1] - pc.node0;
+    pc.n_span = d->sent_span_off[s1] - pc.span0;
+    pc.chars0 = cum_n[s0];
+    order[q].resize(n);
+    node_off[q].resize(n + 1);
+    span_off[q].resize(n + 1);
+    bp_off[q].resize(n + 1);
+    pcum[q].resize(n + 1);
+    for (int32_t s = 0; s < n; ++s) order[q][s] = s;
+    std::stable_sort(order[q].begin(), order[q].end(),
+                     [&](int32_t x, int32_t y) { return d->sent_n[s0 + x] > d->sent_n[s0 + y]; });
+    bp_off[q][0] = 0;
+    for (int32_t s = 0; s <= n; ++s) {
+      node_off[q][s] = d->sent_node_off[s0 + s] - pc.node0;
+      span_off[q][s] = d->sent_span_off[s0 + s] - pc.span0;
+      pcum[q][s] = cum_n[s0 + s] - pc.chars0;
+      if (s < n) bp_off[q][s + 1] = bp_off[q][s] + (int64_t)(d->sent_n[s0 + s] + 1) * max_k;
+    }
+    pc.bp_entries = bp_off[q][n];
+    b->bp_entries += pc.bp_entries;
   }
 
   hipStream_t stm = c->ustream;     // complete when this returns (synchronised below)
   const size_t nres = (size_t)S * max_k;
   const size_t ncodes = (size_t)b->total_chars * max_k;
-  const size_t npost = (size_t)d->n_post * (size_t)d->n_nodes;
   // the batch's buffers as offsets into one arena
   Carve cv;
-  const size_t o_order = cv.dev((size_t)S * 4), o_sent_n = cv.dev((size_t)S * 4),
-               o_node_off = cv.dev(((size_t)S + 1) * 8), o_span_off = cv.dev(((size_t)S + 1) * 8),
-               o_bp_off = cv.dev(((size_t)S + 1) * 8), o_cum_n = cv.dev(((size_t)S + 1) * 8),
-               o_span_start = cv.dev((size_t)d->n_span * 4),
-               o_nodes = cv.dev((size_t)d->n_nodes * sizeof(NodeRec)), o_post = cv.dev(npost * 8),
-               o_bp = cv.dev((size_t)b->bp_entries * 4);
+  struct PieceOff {
+    size_t order, sent_n, node_off, span_off, bp_off, cum_n, span_start, nodes, post, bp;
+  };
+  std::vector<PieceOff> po(P);
+  for (size_t q = 0; q < P; ++q) {
+    const lt_piece& pc = b->pieces[q];
+    const size_t n = (size_t)pc.n_sent;
+    po[q] = PieceOff{cv.dev(n * 4), cv.dev(n * 4), cv.dev((n + 1) * 8), cv.dev((n + 1) * 8),
+                     cv.dev((n + 1) * 8), cv.dev((n + 1) * 8), cv.dev((size_t)pc.n_span * 4),
+                     cv.dev((size_t)pc.n_nodes * sizeof(NodeRec)),
+                     cv.dev((size_t)d->n_post * (size_t)pc.n_nodes * 8), cv.dev((size_t)pc.bp_entries * 4)};
+  }
+  const size_t o_sent_n = cv.dev((size_t)S * 4), o_cum_n = cv.dev(((size_t)S + 1) * 8);
   b->slab_cap = slab_layout(S, max_k, b->total_chars).capacity;
   const uint64_t slab_alloc = slab_alloc_bytes(S, max_k, b->total_chars);
   size_t o_count[2], o_len[2], o_score[2], o_codes[2], o_slab[2];
@@ -703,16 +751,21 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   }
   char* D = b->arena.d;
   char* H = b->arena.h;
-  b->d_order = at<int32_t>(D, o_order);
+  for (size_t q = 0; q < P; ++q) {
+    lt_piece& pc = b->pieces[q];
+    pc.d_order = at<int32_t>(D, po[q].order);
+    pc.d_sent_n = at<int32_t>(D, po[q].sent_n);
+    pc.d_node_off = at<int64_t>(D, po[q].node_off);
+    pc.d_span_off = at<int64_t>(D, po[q].span_off);
+    pc.d_bp_off = at<int64_t>(D, po[q].bp_off);
+    pc.d_cum_n = at<int64_t>(D, po[q].cum_n);
+    pc.d_span_start = at<int32_t>(D, po[q].span_start);
+    pc.d_nodes = at<NodeRec>(D, po[q].nodes);
+    pc.d_post = at<double>(D, po[q].post);
+    pc.d_bp = at<uint32_t>(D, po[q].bp);
+  }
   b->d_sent_n = at<int32_t>(D, o_sent_n);
-  b->d_node_off = at<int64_t>(D, o_node_off);
-  b->d_span_off = at<int64_t>(D, o_span_off);
-  b->d_bp_off = at<int64_t>(D, o_bp_off);
   b->d_cum_n = at<int64_t>(D, o_cum_n);
-  b->d_span_start = at<int32_t>(D, o_span_start);
-  b->d_nodes = at<NodeRec>(D, o_nodes);
-  b->d_post = at<double>(D, o_post);
-  b->d_bp = at<uint32_t>(D, o_bp);
   for (int i = 0; i < 2; ++i) {
     b->res[i].count = at<int32_t>(D, o_count[i]);
     b->res[i].len = at<int32_t>(D, o_len[i]);
@@ -730,13 +783,8 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     if (e == hipSuccess && count)
       e = hipMemcpyAsync(dst, src, count * sizeof(*src), hipMemcpyHostToDevice, stm);
   };
-  up(b->d_order, order.data(), (size_t)S);
   up(b->d_sent_n, d->sent_n, (size_t)S);
-  up(b->d_node_off, d->sent_node_off, (size_t)S + 1);
-  up(b->d_span_off, d->sent_span_off, (size_t)S + 1);
-  up(b->d_bp_off, bp_off.data(), (size_t)S + 1);
   up(b->d_cum_n, cum_n.data(), (size_t)S + 1);
-  up(b->d_span_start, d->span_start, (size_t)d->n_span);
   // device node records: AoS, mask + each node's span length d-1 (bits 24-26)
   std::unique_ptr<NodeRec[]> recs(new (std::nothrow) NodeRec[(size_t)std::max<int64_t>(d->n_nodes, 1)]);
   if (!recs) {
@@ -766,8 +814,20 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       }
     }
   }, 256);
-  up(b->d_nodes, recs.get(), (size_t)d->n_nodes);
-  up(b->d_post, d->node_post, npost);
+  for (size_t q = 0; q < P; ++q) {
+    const lt_piece& pc = b->pieces[q];
+    const size_t n = (size_t)pc.n_sent;
+    up(pc.d_order, order[q].data(), n);
+    up(pc.d_sent_n, d->sent_n + pc.s0, n);
+    up(pc.d_node_off, node_off[q].data(), n + 1);
+    up(pc.d_span_off, span_off[q].data(), n + 1);
+    up(pc.d_bp_off, bp_off[q].data(), n + 1);
+    up(pc.d_cum_n, pcum[q].data(), n + 1);
+    up(pc.d_span_start, d->span_start + pc.span0, (size_t)pc.n_span);
+    up(pc.d_nodes, recs.get() + pc.node0, (size_t)pc.n_nodes);
+    for (int32_t t = 0; t < d->n_post; ++t)
+      up(pc.d_post + (size_t)t * pc.n_nodes, d->node_post + (size_t)t * d->n_nodes + pc.node0, (size_t)pc.n_nodes);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(stm);
   if (e != hipSuccess) {
     batch_free(b);
@@ -776,6 +836,13 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   }
   *out = b;
   return LT_OK;
+}
+
+int32_t lt_batch_pieces(const lt_batch* b) { return b ? (int32_t)b->pieces.size() : 0; }
+
+int64_t lt_set_piece_bytes(int64_t bytes) {
+  const int64_t full = ((int64_t)1 << 31) - 1;
+  return g_piece_bytes.exchange(bytes < 1 || bytes > full ? full : bytes);
 }
 
 lt_status lt_batch_destroy(lt_batch* b) {
@@ -790,6 +857,8 @@ lt_status lt_batch_destroy(lt_batch* b) {
 int64_t lt_batch_code_slots(const lt_batch* b, int k) { return b ? b->total_chars * (int64_t)k : 0; }
 
 // --------------------------------------------------------------- decode --
+// Parameters of the model / batch / beam; the per-piece fields are set by
+// piece_params.
 static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, DecodeParams& p) {
   if (!c || !m || !b) return fail(LT_EINVAL, "decode: NULL argument");
   if (m->ctx != c || b->ctx != c) return fail(LT_EINVAL, "decode: handles from another context");
@@ -805,29 +874,35 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.d3mul = m->d3mul;
   p.narrow = m->narrow;
   p.has_tri = b->has_tri;
-  p.n_sent = b->n_sent;
   p.max_len = b->max_len;
   p.n_post = b->n_post;
   p.k = k;
   p.bp_stride = b->max_k;
-  p.n_nodes = b->n_nodes;
-  p.order = b->d_order;
-  p.sent_n = b->d_sent_n;
-  p.node_off = b->d_node_off;
-  p.span_off = b->d_span_off;
-  p.span_start = b->d_span_start;
-  p.nodes = b->d_nodes;
-  p.npost = b->d_post;
-  p.bp = b->d_bp;
-  p.bp_bytes = b->bp_entries * 4;
-  p.bp_off = b->d_bp_off;
-  p.cum_n = b->d_cum_n;
-  p.out_count = b->d_count;
-  p.out_len = b->d_len;
-  p.out_score = b->d_score;
-  p.out_codes = b->d_codes;
   p.counters = c->d_counters;
   return LT_OK;
+}
+
+// Piece q of b, writing the current result slot: its sentences' results
+// land at their places in the batch's result arrays.
+static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
+  const lt_piece& pc = b->pieces[q];
+  p.n_sent = pc.n_sent;
+  p.n_nodes = pc.n_nodes;
+  p.order = pc.d_order;
+  p.sent_n = pc.d_sent_n;
+  p.node_off = pc.d_node_off;
+  p.span_off = pc.d_span_off;
+  p.span_start = pc.d_span_start;
+  p.nodes = pc.d_nodes;
+  p.npost = pc.d_post;
+  p.bp = pc.d_bp;
+  p.bp_bytes = pc.bp_entries * 4;
+  p.bp_off = pc.d_bp_off;
+  p.cum_n = pc.d_cum_n;
+  p.out_count = b->d_count + pc.s0;
+  p.out_len = b->d_len + (int64_t)pc.s0 * k;
+  p.out_score = b->d_score + (int64_t)pc.s0 * k;
+  p.out_codes = b->d_codes + (int64_t)k * pc.chars0;
 }
 
 // The next decode writes the result slot the previous one did not: the D2H
@@ -851,12 +926,12 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
   if ((st = next_slot(c, b)) != LT_OK) return st;
-  p.out_count = b->d_count;
-  p.out_len = b->d_len;
-  p.out_score = b->d_score;
-  p.out_codes = b->d_codes;
   const int r = (int)(c->n_launch % lt_ctx::KRING);
-  HIP_TRY(launch_decode(p, c->stream, false, c->kev0[r], c->kev1[r]));
+  const size_t P = b->pieces.size();
+  for (size_t q = 0; q < P; ++q) {           // timing: start of the first piece .. end of the last
+    piece_params(b, q, k, p);
+    HIP_TRY(launch_decode(p, c->stream, false, q == 0 ? c->kev0[r] : nullptr, q + 1 == P ? c->kev1[r] : nullptr));
+  }
   b->last_end = c->kev1[r];          // other streams wait for this decode here
   b->launch_serial = c->n_serial++;
   ++c->n_launch;
@@ -1114,12 +1189,11 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
   if ((st = next_slot(c, b)) != LT_OK) return st;
-  p.out_count = b->d_count;
-  p.out_len = b->d_len;
-  p.out_score = b->d_score;
-  p.out_codes = b->d_codes;
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
-  HIP_TRY(launch_decode(p, c->stream, true));
+  for (size_t q = 0; q < b->pieces.size(); ++q) {
+    piece_params(b, q, k, p);
+    HIP_TRY(launch_decode(p, c->stream, true));
+  }
   b->launch_serial = c->n_serial++;
   b->last_end = nullptr;             // complete below
   unsigned long long h[4] = {0, 0, 0, 0};

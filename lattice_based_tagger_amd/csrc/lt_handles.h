@@ -39,18 +39,30 @@ struct lt_ctx {
   std::vector<lt_arena> spare;     // arenas of destroyed batches, kept for reuse
 };
 
+// One launch piece of a batch: sentences [s0, s0 + n_sent), its inputs with
+// offsets rebased to the piece, its backpointers.
+struct lt_piece {
+  int32_t s0 = 0, n_sent = 0;
+  int64_t node0 = 0, span0 = 0, chars0 = 0;      // first node / span entry / character
+  int64_t n_nodes = 0, n_span = 0, bp_entries = 0;
+  int32_t *d_order = nullptr, *d_sent_n = nullptr, *d_span_start = nullptr;
+  int64_t *d_node_off = nullptr, *d_span_off = nullptr, *d_bp_off = nullptr, *d_cum_n = nullptr;
+  lt::NodeRec* d_nodes = nullptr;
+  double* d_post = nullptr;
+  uint32_t* d_bp = nullptr;
+};
+
 struct lt_batch {
   lt_ctx* ctx = nullptr;
   int32_t n_sent = 0, max_len = 8, n_post = 0, has_tri = 0, max_k = 1;
   int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
   int last_k = 0;
-  // device inputs
-  int32_t *d_order = nullptr, *d_sent_n = nullptr, *d_span_start = nullptr;
-  int64_t *d_node_off = nullptr, *d_span_off = nullptr, *d_bp_off = nullptr, *d_cum_n = nullptr;
-  lt::NodeRec* d_nodes = nullptr;
-  double* d_post = nullptr;
-  // scratch + device results (sized for max_k)
-  uint32_t* d_bp = nullptr;
+  // device inputs, per launch piece (lt_batch_create: node records and
+  // backpointers of a piece stay below 2^31 B)
+  std::vector<lt_piece> pieces;
+  int32_t* d_sent_n = nullptr;        // whole batch (result packing)
+  int64_t* d_cum_n = nullptr;
+  // device results (sized for max_k)
   // two result slots: decodes alternate between them, so the D2H of one
   // decode's results (lt_result_fetch, copy stream) overlaps the next decode
   struct Slot {

@@ -103,3 +103,52 @@ def test_bench_dist_shares_the_communicator_id():
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = sorted(q.get(timeout=10) for _ in range(2))
     assert res == [(0, True, 1.0, 2.0), (1, True, 1.0, 2.0)]
+
+
+def _strong_worker(rank, world, port, total, out_q):
+    """bench.py's strong-scaling path on the CPU: the seeded batch (in
+    seeded permutations past the generated lattices, as config 4 builds
+    it), this rank's shard (``shard_of``), its decode (the C restatement
+    standing in for the device), the per-rank results gathered to rank 0
+    (gloo here, RCCL in bench.py) and rank 0's byte-for-byte check against
+    a single-process decode (``check_results``)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    from oracle import lt_oracle
+    d = bench.Dist(world)
+    k = 2
+    raw, lay, sm, packed, keys, coefs = bench.make_workload(64, 13, 5000)
+    order = bench.batch_order(total, packed.n_sent, 13)
+    lo, hi, piece = bench.shard_of(packed, order, k, world, rank)
+    res = lt_oracle.decode(piece, keys, coefs, k)[:4]
+    mine = bench.padded_as_packed(res, piece.sent_n, k)
+    g = dist.HostGroup.__new__(dist.HostGroup)
+    g.ranks, g.pg = dist.Ranks(), d.pg
+    parts = g.gather(mine)
+    if rank == 0:
+        ref = bench.padded_as_packed(lt_oracle.decode(packed, keys, coefs, k)[:4], packed.sent_n, k)
+        idx = np.arange(packed.n_sent) if order is None else order
+        ok = bench.check_results(parts, ref, idx)
+        try:                                   # a wrong reassembly is caught
+            bench.check_results(parts[::-1], ref, idx)
+            caught = False
+        except AssertionError:
+            caught = True
+        out_q.put((ok, caught, all(p.n_sent > 0 for p in parts), [p.n_sent for p in parts]))
+    d.close()
+
+
+@pytest.mark.parametrize('world,total', [(2, 64), (3, 200)])
+def test_bench_strong_split_reassembles(world, total):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strong_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ok, caught, nonempty, sizes = q.get(timeout=10)
+    assert ok and caught and nonempty and sum(sizes) == total

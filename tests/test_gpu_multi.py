@@ -147,19 +147,26 @@ def test_beam_search_batch_over_two_contexts(gpu_decoder):
 
 def test_config4_million_sentences_on_one_gpu(gpu_decoder):
     """1,048,576 sentences (the 64K generated lattices in 16 seeded
-    permutations, as bench.py --sentences 1048576 builds them) through
-    Decoder.decode_packed: several launch pieces, uploads overlapping
-    decodes; every sentence equals the C oracle's decode of its lattice."""
+    permutations, as bench.py --sentences 1048576 builds them) as one device
+    batch: the library decodes it in launch pieces (each below 2^31 B of
+    node records); every sentence equals the C oracle's decode of its
+    lattice, in the packed and the padded result layouts."""
     _, _, (base, keys, coefs) = _workload(65536, 5, 1_000_000)
     rng = np.random.default_rng(99)
     order = np.concatenate([rng.permutation(base.n_sent) for _ in range(16)])
     big = base.take(order)
     assert big.n_sent == 1 << 20
-    model = _model(keys, coefs)
-    pieces = big.split(Decoder.MAX_NODES, 1)
-    assert len(pieces) > 8
-    got = Decoder.get(0).decode_packed(model, big, 1)
+    dec = Decoder.get(0)
+    dm = dec.device_model(_model(keys, coefs))
+    db = _capi.DeviceBatch(dec.ctx, big, max_k=1)
     del big
+    try:
+        assert db.pieces > 8                    # launch pieces below 2^31 B of node records each
+        got = db.decode_packed(dm, 1)
+        padded = db.decode(dm, 1)               # the padded layout of the same batch
+    finally:
+        db.close()
+    assert _same(got.padded(base.sent_n[order]), padded)
     oc, ol, osc, ocodes, _, _ = lt_oracle.decode(base, keys, coefs, 1, nthreads=16)
     assert np.array_equal(got.count, oc[order])
     assert np.array_equal(got.length[:, 0], ol[order, 0])

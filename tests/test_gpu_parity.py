@@ -157,18 +157,39 @@ def test_ragged_and_empty_batch(gpu_decoder):
     assert beam_search_batch([], funcs, beam_size=3) == []
 
 
-def test_decode_in_several_launches(gpu_decoder, monkeypatch):
-    """A batch above the per-launch node budget is decoded in sentence-range
-    launches with the same results (Decoder.decode_packed)."""
-    from lattice_based_tagger_amd.beam import Decoder
+@pytest.mark.parametrize('k', [1, 2, 5, 16])
+def test_decode_in_several_launches(gpu_decoder, k):
+    """A batch above the per-launch budget is decoded as several launch
+    pieces writing one result array (lt_batch_pieces) -- forced here with
+    the piece-size test hook -- with the results of one launch."""
+    from lattice_based_tagger_amd import _capi as C
+    lib = C.load()
     cases = [c for c in load('base') if c.bindex]
     lats = [(c.bindex, c.chars) for c in cases]
-    whole = beam_search_batch(lats, cases[0].funcs, beam_size=5)
-    monkeypatch.setattr(Decoder, 'MAX_NODES', 3000)
-    pieces = beam_search_batch(lats, cases[0].funcs, beam_size=5)
+    whole = beam_search_batch(lats, cases[0].funcs, beam_size=k)
+    packed, keys, coefs = _synthetic(300, seed=7, n_features=20_000, eojeols=6)
+    one = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)[0]
+    old = lib.lt_set_piece_bytes(100_000)
+    try:
+        pieces = beam_search_batch(lats, cases[0].funcs, beam_size=k)
+        dm = C.DeviceModel(gpu_decoder.ctx, keys, coefs)
+        db = C.DeviceBatch(gpu_decoder.ctx, packed, max_k=k)
+        try:
+            assert db.pieces > 3
+            many = db.decode(dm, k)
+            pk = db.decode_packed(dm, k)
+        finally:
+            db.close()
+            dm.close()
+    finally:
+        lib.lt_set_piece_bytes(old)
     for a, b in zip(whole, pieces):
         assert [float(x.score).hex() for x in a] == [float(x.score).hex() for x in b]
         assert [[tuple(w) for w in x.sequences] for x in a] == [[tuple(w) for w in x.sequences] for x in b]
+    for x, y in zip(one, many):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    for x, y in zip(pk.padded(packed.sent_n), one):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
 
 
 def test_half_wave_beam_kernel_multi_chunk(gpu_decoder):

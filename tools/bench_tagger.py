@@ -64,8 +64,7 @@ def main():
         t0 = time.perf_counter()
         dec = Decoder.get(0)
         dm = dec.device_model(model)
-        pieces = packed.split(Decoder.MAX_NODES)
-        dbs = [_capi.DeviceBatch(dec.ctx, packed.slice(s0, s1), max_k=a.k) for s0, s1 in pieces]
+        dbs = [_capi.DeviceBatch(dec.ctx, packed, max_k=a.k)]
         t['batch_create_h2d'] = time.perf_counter() - t0
         t0 = time.perf_counter()
         kern = 0.0
