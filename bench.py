@@ -413,7 +413,8 @@ def main():
             what = 'all %d sentences of the batch, gathered from %d ranks over RCCL' % (a.sentences, d.world)
         elif strong:                         # this rank's shard only (no gather)
             check_results(got, ref, base_idx[lo:hi])
-            what = 'rank 0 shard [%d, %d) of the batch (no gather)' % (lo, hi)
+            what = ('all %d sentences of the batch' % a.sentences if d.world == 1 else
+                    'rank 0 shard [%d, %d) of the batch (no gather)' % (lo, hi))
         else:                                # weak: rank 0's own batch, other blocks complete
             check_results(got[:1], ref, base_idx, (got, a.sentences) if comm else None)
             what = 'rank 0 batch of %d sentences%s' % (a.sentences, ', %d gathered blocks complete'

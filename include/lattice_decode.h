@@ -32,7 +32,7 @@ extern "C" {
 
 #define LT_ABI_VERSION 2   /* 2: compact results (slabs), gathers of slabs */
 #define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
-#define LT_MAX_BEAM 32     /* largest beam_size compiled in */
+#define LT_MAX_BEAM 256    /* largest beam_size compiled in */
 
 typedef int32_t lt_status;
 enum {

@@ -70,24 +70,57 @@ class Beam:
 _model_cache = weakref.WeakKeyDictionary()
 
 
+def _digest_array(a):
+    """Content digest of a numpy array (in-place edits change it)."""
+    a = np.ascontiguousarray(a)
+    try:
+        import xxhash
+        return (a.dtype.str, a.shape, xxhash.xxh3_64_intdigest(a.data))
+    except ImportError:                 # pragma: no cover - xxhash ships with the image
+        return (a.dtype.str, a.shape, int(np.bitwise_xor.reduce(a.view(np.uint8).reshape(-1))))
+
+
+def _digest_table(t):
+    """Content digest of a preference table {tag: {string: value}}."""
+    try:
+        return hash(tuple((tag, id(inner), hash(frozenset(inner.items())) if isinstance(inner, dict) else id(inner))
+                          for tag, inner in t.items()))
+    except TypeError:                   # unhashable values: identity only
+        return id(t)
+
+
 def _fingerprint(score_functions):
+    """Everything the lowered model copies from the composite: the plugin
+    objects, the regularisation coefficients, the preference tables'
+    contents, the trigram's encoder / feature_dic (identity and size) and the
+    coefficient array's contents (the reference reads all of them live on
+    every call, score_funcs.py:63-105, 137-144).  A feature_dic edited in
+    place without a size change is not detected: call
+    ``invalidate_model_cache`` after that."""
     parts = []
     for f in getattr(score_functions, 'funcs', []):
         parts.append(id(f))
-        if type(f).__name__ == 'SimpleTrigramFeatureScore':
+        name = type(f).__name__
+        if name == 'RegularizationScore':
+            parts += [f.unknown_penalty, f.known_preference, f.syllable_penalty,
+                      type(f.unknown_penalty), type(f.known_preference), type(f.syllable_penalty)]
+        elif name == 'MorphemePreferenceScore':
+            parts += [id(f.tag_to_morph), _digest_table(f.tag_to_morph)]
+        elif name == 'WordPreferenceScore':
+            parts += [id(f.tag_to_word), _digest_table(f.tag_to_word)]
+        elif name == 'SimpleTrigramFeatureScore':
             enc = f.encoder
             dic = getattr(enc, 'feature_dic', None)
             coef = f.coefficients
             parts += [id(enc), id(dic), len(dic) if dic is not None else -1, id(coef),
-                      coef.ctypes.data if isinstance(coef, np.ndarray) else 0]
+                      _digest_array(coef) if isinstance(coef, np.ndarray) else None]
     return tuple(parts)
 
 
 def lowered_model(score_functions):
     """LoweredModel of a composite, cached while the composite is unchanged
-    (same plugin objects, same feature_dic object and size, same
-    coefficient array).  Call ``invalidate_model_cache`` after mutating a
-    feature_dic or coefficients in place."""
+    (``_fingerprint``).  Call ``invalidate_model_cache`` after editing a
+    feature_dic in place."""
     fp = _fingerprint(score_functions)
     try:
         hit = _model_cache.get(score_functions)
@@ -277,6 +310,59 @@ def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device
     return decode_batch(packed, objs, [ch for _, ch in sentences], model, k, device)
 
 
+# ---------------------------------------------------------------------------
+# score types: the reference's score is a Python sum whose type follows the
+# increments -- BOS starts at int 0 (beam.py:21), each increment is
+# ((0 + f1) + f2) + ... (score_funcs.py:50-54), the trigram term is int 0 for
+# an empty feature set and a numpy.float64 sum otherwise
+# (score_funcs.py:141-144), EOS adds int 0 (beam.py:60).  numpy.float64
+# absorbs int and float, float absorbs int.
+# ---------------------------------------------------------------------------
+from .lowering import F_HAS4, F_HAS5  # noqa: E402
+
+_TRI_LOCAL = F_HAS4 | F_HAS5          # a class-4/5 feature of wk: the trigram set is non-empty
+
+
+def path_score_type(model, path):
+    """Type of the reference score of ``path`` (BOS, words...; no EOS) under
+    the lowered composite: the increments' values replayed on the host
+    (node-local scorers evaluated, trigram presence from the encoder)."""
+    funcs = model.pre_funcs + ([model.trigram] if model.trigram is not None else []) + model.post_funcs
+    enc = model.trigram.encoder if model.trigram is not None else None
+    acc = 0
+    for q in range(1, len(path)):
+        wk, wj = path[q], path[q - 1]
+        wi = None if q == 1 else path[q - 2]
+        inc = 0
+        for f in funcs:
+            if f is model.trigram:
+                inc = inc + (np.float64(0.0) if enc.encode_word(wi, wj, wk) else 0)
+            else:
+                inc = inc + f.score(None, wk)
+        acc = acc + inc
+    return type(acc + 0)
+
+
+def typed_score(kind, value):
+    return kind(value) if kind is not float else float(value)
+
+
+def score_kinds(model, n_paths, path_masks_any, path_words, need=None):
+    """Types of n_paths scores.  ``path_masks_any[p]``: some word of path p
+    has a class-4/5 trigram feature (its increment, and so the score, is a
+    numpy.float64); the other paths are replayed (``path_words(p)``);
+    ``need[p]`` false: not wanted (float)."""
+    out = []
+    for p in range(n_paths):
+        if need is not None and not need[p]:
+            out.append(float)
+        elif model.trigram is not None and path_masks_any[p]:
+            out.append(np.float64)
+        else:
+            out.append(path_score_type(model, path_words(p)))
+    return out
+
+
 def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, uploaded=None,
                  decoder=None):
     """Decode a packed batch and re-materialise the matures: ``objs[s][i]`` is
@@ -299,8 +385,9 @@ def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, 
         res = decode_packed_devices(model, packed, k, devices)
     T = 1 if best_only else k
     if objs and hasattr(objs[0], 'src') and hasattr(objs[0], 'words'):      # native packer's views
-        return _materialise_bulk(packed, objs, chars_list, T, res)
+        return _materialise_bulk(packed, objs, chars_list, T, res, model)
     count, length, score, codes, off = res.count, res.length, res.score, res.codes, res.off
+    masks = np.asarray(packed.node_mask)
     out = []
     for s, chars in enumerate(chars_list):
         n = len(chars)
@@ -308,9 +395,15 @@ def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, 
         matures = []
         for t in range(min(int(count[s]), T)):
             a = int(off[s * k + t])
-            path = [nodes[0]] + [nodes[c] for c in codes[a:a + int(length[s, t])]] + [eos_word(n)]
-            sc = float(score[s, t]) if n > 0 else 0
-            matures.append(Sequence(path, sc, 0))
+            cs = codes[a:a + int(length[s, t])]
+            path = [nodes[0]] + [nodes[c] for c in cs]
+            if n > 0:
+                hit = bool(np.any(masks[packed.sent_node_off[s] + cs] & _TRI_LOCAL))
+                kind = score_kinds(model, 1, [hit], lambda _: path)[0]
+                sc = typed_score(kind, score[s, t])
+            else:
+                sc = 0
+            matures.append(Sequence(path + [eos_word(n)], sc, 0))
         out.append(matures)
     return out
 
@@ -330,7 +423,7 @@ def _materialise_bulk(*args):
             gc.enable()
 
 
-def _materialise_bulk_body(packed, objs, chars_list, T, res):
+def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
     count, length, score, codes, k = res.count, res.length, res.score, res.codes, res.k
     S = len(chars_list)
     n = np.asarray(packed.sent_n, dtype=np.int64)
@@ -365,20 +458,20 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res):
             flat[j] = Word(sub, sub, None, Unk, None, d, b, b + d, False)
     # the sentinels are immutable tuples: one BOS, one EOS per sentence length
     bos, eos = bos_word(), {}
+    vals = _typed_scores(model, packed, glob, seg, Lf, first, score[:, :T], n, T, bos, flat)
     if T == 1:                                          # best path only (Tagger.tag): one comprehension
         nl = n.tolist()
         for nch in set(nl):
             eos[nch] = eos_word(nch)
         L1 = L[:, 0]
         ends = np.cumsum(L1)
-        return [[Sequence([bos] + flat[a:z] + [eos[nch]], sc if nch > 0 else 0, 0)] if c else []
+        return [[Sequence([bos] + flat[a:z] + [eos[nch]], sc, 0)] if c else []
                 for a, z, nch, c, sc in zip((ends - L1).tolist(), ends.tolist(), nl,
-                                            (np.minimum(count, 1) > 0).tolist(), score[:, 0].tolist())]
+                                            (np.minimum(count, 1) > 0).tolist(), vals)]
     out = []
     pos = 0
     cnt = np.minimum(count, T).tolist()
     Ll = L.tolist()
-    sc = score.tolist()
     for s, nch in enumerate(n.tolist()):
         e = eos.get(nch)
         if e is None:
@@ -386,10 +479,33 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res):
         matures = []
         for tt in range(cnt[s]):
             ln = Ll[s][tt]
-            matures.append(Sequence([bos] + flat[pos:pos + ln] + [e], sc[s][tt] if nch > 0 else 0, 0))
+            matures.append(Sequence([bos] + flat[pos:pos + ln] + [e], vals[s * T + tt], 0))
             pos += ln
         out.append(matures)
     return out
+
+
+def _typed_scores(model, packed, glob, seg, Lf, first, score, n, T, bos, flat):
+    """Scores of the S x T paths (flattened) with the reference's types
+    (path_score_type): numpy.float64 for every path with a class-4/5 trigram
+    feature on some word (all of them in a trained model), the rest
+    replayed; int 0 for an empty sentence."""
+    P = Lf.size
+    hit = np.bincount(seg, weights=(np.asarray(packed.node_mask)[glob] & _TRI_LOCAL) != 0,
+                      minlength=P) > 0 if P else np.zeros(0, dtype=bool)
+    flat_sc = score.reshape(-1)
+    empty = np.repeat(n == 0, T)
+    need = Lf > 0                                       # a mature of a non-empty sentence
+    if model.trigram is not None and bool(np.all(hit | ~need)):
+        vals = list(flat_sc)                            # numpy.float64 scalars
+    else:
+        kinds = score_kinds(model, P, hit.tolist(),
+                            lambda p: [bos] + flat[int(first[p]):int(first[p] + Lf[p])], need.tolist())
+        vals = [typed_score(kd, v) for kd, v in zip(kinds, flat_sc.tolist())]
+    if empty.any():
+        for p in np.flatnonzero(empty).tolist():
+            vals[p] = 0
+    return vals
 
 
 def beam_search(bindex, chars, score_functions, beam_size=5, max_len=8, debug=False):

@@ -151,13 +151,13 @@ struct alignas(16) NodeRec {
   double pre, f4, f5, f6;
 };
 
-// Backpointer word: local node index (24 b) | span d-1 (3 b) | parent rank (5 b)
+// Backpointer word: local node index (21 b) | span d-1 (3 b) | parent rank (8 b)
 LT_HD uint32_t bp_pack(uint32_t node, uint32_t d, uint32_t r) {
-  return (node << 8) | ((d - 1u) << 5) | r;
+  return (node << 11) | ((d - 1u) << 8) | r;
 }
-LT_HD uint32_t bp_node(uint32_t v) { return v >> 8; }
-LT_HD uint32_t bp_d(uint32_t v) { return ((v >> 5) & 7u) + 1u; }
-LT_HD uint32_t bp_rank(uint32_t v) { return v & 31u; }
-constexpr int64_t MAX_LOCAL_NODES = (int64_t)1 << 24;
+LT_HD uint32_t bp_node(uint32_t v) { return v >> 11; }
+LT_HD uint32_t bp_d(uint32_t v) { return ((v >> 8) & 7u) + 1u; }
+LT_HD uint32_t bp_rank(uint32_t v) { return v & 255u; }
+constexpr int64_t MAX_LOCAL_NODES = (int64_t)1 << 21;     // nodes per sentence
 
 }  // namespace lt

@@ -21,8 +21,10 @@
 //    reference's generation order (begin ascending, hypothesis rank,
 //    candidate order), scored one per lane, ranked by counting within the
 //    group (Python's stable sort), the top k written to the ring.
-//  * lt_beam_pk<KT>    -- beam_size 9..32 (KT = 16, 32): one sentence per wave,
-//    the same enumeration and rank counting over several scoring rounds.
+//  * lt_beam_pk<KT>    -- beam_size 9..256 (KT = 16 .. 256): one sentence per
+//    wave, the same enumeration and rank counting over several scoring
+//    rounds (beams above 64: the running list, winners and matures in
+//    64-lane chunks).
 // All: the frontier (beams of the last 9 end positions) lives in LDS as a
 // ring whose entries cache the fields of the hypothesis' last two nodes;
 // trigram classes 4/5/6 arrive pre-resolved per node, class 3 (tag, tag)
@@ -740,6 +742,10 @@ template <int KT, int WPB, bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(64 * WPB)
 lt_beam_pk(DecodeParams p) {
   constexpr int RPC = KT <= 16 ? 2 : 4;         // scoring rounds per chunk
+  // beams above 64 (KT = 128, 256): more than one entry per lane in the
+  // running list, the winners and the matures -- loops over 64-lane chunks
+  constexpr bool BIG = KT > 64;
+  constexpr int KV = BIG ? KT / 64 : 1;
   constexpr int CH = 64 * RPC;                  // expansions per chunk
   constexpr int KTP = KT < 4 ? 4 : KT;          // running-list room (multiple of 4)
   constexpr int LN = KTP + CH;                  // ranked list: running top-k + chunk
@@ -812,8 +818,10 @@ lt_beam_pk(DecodeParams p) {
   for (int e = 1; e <= n; ++e) {
     // vmcnt(1): the prefetched records and span starts landed (VMEM
     // operations retire in order on gfx9; the one younger operation is the
-    // previous position's backpointer store)
-    __builtin_amdgcn_s_waitcnt(0x0F71);
+    // previous position's backpointer store).  Big beams store several
+    // backpointer chunks per position: vmcnt(0).
+    if constexpr (BIG) __builtin_amdgcn_s_waitcnt(0x0F70);
+    else __builtin_amdgcn_s_waitcnt(0x0F71);
     uint4* const cst = stg[wv];
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
@@ -897,8 +905,19 @@ lt_beam_pk(DecodeParams p) {
       // entry is the number of entries with a larger key, or an equal key and
       // a smaller generation index (0 keys -- skipped / idle -- never win).
       const int R0 = min(RPC, (M - base + 63) >> 6);         // rounds used (uniform)
-      const unsigned long long rk = lane < nrun ? LK[KTP - nrun + lane] : 0ull;
-      const uint32_t rg = lane < nrun ? LG[KTP - nrun + lane] : INV;
+      unsigned long long rk = lane < nrun ? LK[KTP - nrun + lane] : 0ull;
+      uint32_t rg = lane < nrun ? LG[KTP - nrun + lane] : INV;
+      unsigned long long rkv[KV];                 // big beams: running entry lane + 64 v
+      uint32_t rgv[KV];
+      if constexpr (BIG) {
+#pragma unroll
+        for (int v = 0; v < KV; ++v) {
+          const int q = lane + 64 * v;
+          rkv[v] = q < nrun ? LK[KTP - nrun + q] : 0ull;
+          rgv[v] = q < nrun ? LG[KTP - nrun + q] : INV;
+          if (v > 0 && rkv[v] > rk) rk = rkv[v];   // the lane's maximum (pruning below)
+        }
+      }
       int valid = nrun;
 #pragma unroll
       for (int t = 0; t < RPC; ++t)
@@ -950,7 +969,13 @@ lt_beam_pk(DecodeParams p) {
           if (c) { LK[at] = key; LG[at] = g; }
           nc += __builtin_popcountll(bal);
         };
-        if (nrun > 0) push(rk, rg);
+        if constexpr (BIG) {
+#pragma unroll
+          for (int v = 0; v < KV; ++v)
+            if (64 * v < nrun) push(rkv[v], rgv[v]);
+        } else {
+          if (nrun > 0) push(rk, rg);
+        }
 #pragma unroll
         for (int t = 0; t < RPC; ++t)
           if (t < R0) push(myk[t], myg[t]);
@@ -978,8 +1003,8 @@ lt_beam_pk(DecodeParams p) {
       // running list for the next chunk / beam[e]: at [KTP - nrun, KTP), zero
       // padding below it (in order behind the writes above)
       const int nrp2 = (nrun + 3) & ~3;
-      if (lane < nrp2) {
-        const int dst = KTP - nrp2 + lane, src = lane - (nrp2 - nrun);
+      for (int q = lane; q < nrp2; q += 64) {
+        const int dst = KTP - nrp2 + q, src = q - (nrp2 - nrun);
         LK[dst] = src >= 0 ? tkey[wv][src] : 0ull;
         LG[dst] = src >= 0 ? tgen[wv][src] : INV;
       }
@@ -995,17 +1020,19 @@ lt_beam_pk(DecodeParams p) {
     // block (a position with more than STAGE candidates) takes a separate,
     // uniform path with global loads, so the common path has no load to wait
     // for (and does not wait for the prefetch above).
+    for (int w0 = 0; w0 < (BIG ? nrun : 1); w0 += 64) {   // one pass unless the beam exceeds 64
+    const int wl = w0 + lane;                   // winner (rank) of this lane
     Entry ne;
     uint32_t bpv = 0;
-    const bool writer = lane < nrun;
+    const bool writer = wl < nrun;
     int wj = 0, wr = 0, wi = 0;
-    if (writer) decode((int)LG[KTP - nrun + lane], wj, wr, wi);
+    if (writer) decode((int)LG[KTP - nrun + wl], wj, wr, wi);
     const int wnode = ss[wj] + wi;
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
       const Entry& h = R[(e - d) % RING][wr];
-      ne.score = ord_score(LK[KTP - nrun + lane]); ne.f6 = c.f6;
+      ne.score = ord_score(LK[KTP - nrun + wl]); ne.f6 = c.f6;
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
       ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
       ne.depth = h.depth + 1;
@@ -1017,8 +1044,9 @@ lt_beam_pk(DecodeParams p) {
       build(far ? load_cand(B, nbase + (uint32_t)wnode) : read_block<64>(cst, 0, min(wnode - A0, STAGE - 1)));
     }
     __builtin_amdgcn_wave_barrier();
-    if (writer) R[em9][lane] = ne;
-    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + lane) * 4u : OOB, 0, 0);
+    if (writer) R[em9][wl] = ne;
+    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + wl) * 4u : OOB, 0, 0);
+    }
     if (lane == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
   }
@@ -1028,19 +1056,20 @@ lt_beam_pk(DecodeParams p) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const int nm = cnt9[n % RING];
   if (lane == 0) p.out_count[s] = nm;
-  if (lane >= nm && lane < k) {                 // unused mature slots read as empty
-    p.out_score[(int64_t)s * k + lane] = 0.0;
-    p.out_len[(int64_t)s * k + lane] = 0;
-    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)lane * n;
-    for (int j = 0; j < n; ++j) codes[j] = -1;
-  }
-  if (lane < nm) {
-    const Entry& f = R[n % RING][lane];
-    const int64_t o = (int64_t)s * k + lane;
+  for (int t = lane; t < k; t += 64) {          // mature rank t (one pass unless the beam exceeds 64)
+    if (t >= nm) {                              // unused mature slots read as empty
+      p.out_score[(int64_t)s * k + t] = 0.0;
+      p.out_len[(int64_t)s * k + t] = 0;
+      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
+      for (int j = 0; j < n; ++j) codes[j] = -1;
+      continue;
+    }
+    const Entry& f = R[n % RING][t];
+    const int64_t o = (int64_t)s * k + t;
     p.out_score[o] = f.score + 0.0;
     p.out_len[o] = (int32_t)f.depth;
-    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)lane * n;
-    int pos = n, rank = lane;
+    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
+    int pos = n, rank = t;
     for (int step = (int)f.depth - 1; step >= 0; --step) {
       const uint32_t v = bp[(int64_t)pos * bstride + rank];
       codes[step] = (int32_t)bp_node(v);
@@ -1539,6 +1568,10 @@ hipError_t launch_k(const DecodeParams& p, int kt, const Launch& L) {
     case 8: return launch_bp<8, 4, NARROW, COUNT>(p, L);
     case 16: return launch_bp<16, BP16_WPB, NARROW, COUNT>(p, L);
     case 32: return launch_bp<32, BP32_WPB, NARROW, COUNT>(p, L);
+    // beams above 32: one wave per block (the LDS ring of 9 x KT entries)
+    case 64: return launch_bp<64, 1, NARROW, COUNT>(p, L);
+    case 128: return launch_bp<128, 1, NARROW, COUNT>(p, L);
+    case 256: return launch_bp<256, 1, NARROW, COUNT>(p, L);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1571,11 +1604,8 @@ const char* kernel_name_for(int k) {
 
 int beam_template_for(int k) {
   if (k <= 1) return 1;
-  if (k <= 2) return 2;
-  if (k <= 4) return 4;
-  if (k <= 8) return 8;
-  if (k <= 16) return 16;
-  if (k <= 32) return 32;
+  for (int kt = 2; kt <= LT_MAX_BEAM_COMPILED; kt *= 2)
+    if (k <= kt) return kt;
   return -1;
 }
 

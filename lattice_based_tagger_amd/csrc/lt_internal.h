@@ -118,6 +118,7 @@ hipError_t launch_pack_results(const ResultsPackParams& p, hipStream_t st);
 // pinned host memory of `capacity` bytes.
 hipError_t launch_slab_to_host(const void* slab, void* host, size_t capacity, hipStream_t st);
 
+constexpr int LT_MAX_BEAM_COMPILED = 256;
 int beam_template_for(int k);
 const char* kernel_name_for(int k);
 // e0 / e1 (may be NULL): events recorded at the start / end of the kernel.

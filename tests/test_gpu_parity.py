@@ -40,8 +40,9 @@ def test_golden_vectors_on_gpu(gpu_decoder, name):
             for c, matures in zip(ok, got):
                 exp = c.expected[str(k)]['matures']
                 assert len(matures) == len(exp), (c.tag, k)
-                for m, (codes, shex, _) in zip(matures, exp):
+                for m, (codes, shex, kind) in zip(matures, exp):
                     assert float(m.score).hex() == shex, (c.tag, k)
+                    assert type(m.score).__name__ == kind, (c.tag, k, type(m.score), kind)
                     assert path_matches(c, codes, m.sequences[1:-1]), (c.tag, k)
                     checked += 1
     assert checked > 0
@@ -72,7 +73,8 @@ def _gpu_decode(ctx, packed, keys, coefs, k):
         dm.close()
 
 
-@pytest.mark.parametrize('k,n_sent', [(1, 65536), (5, 8192), (16, 4096), (2, 2048), (3, 2048), (8, 2048), (32, 512)])
+@pytest.mark.parametrize('k,n_sent', [(1, 65536), (5, 8192), (16, 4096), (2, 2048), (3, 2048), (8, 2048), (32, 512),
+                                       (33, 300), (64, 300), (100, 200), (256, 120)])
 def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
     packed, keys, coefs = _synthetic(n_sent, seed=100 + k, n_features=1_000_000)
     (count, length, score, codes), (ex, tu, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)

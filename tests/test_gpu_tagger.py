@@ -31,8 +31,9 @@ def test_tagger_native_lattices_match_reference(gpu_decoder, name, chunk, monkey
         best = tagger.tag_batch(sents, beam_size=k)
         for sent, seq in zip(sents, best):
             c = by_chars[sent.replace(' ', '')]
-            codes, shex, _ = c.expected[str(k)]['matures'][0]
+            codes, shex, kind = c.expected[str(k)]['matures'][0]
             assert float(seq.score).hex() == shex, (sent, k)
+            assert type(seq.score).__name__ == kind, (sent, k)
             words = seq.sequences[1:-1]
             assert len(words) == len(codes), (sent, k)
             for code, w in zip(codes, words):

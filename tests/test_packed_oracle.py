@@ -122,3 +122,31 @@ def test_batch_split_and_slice_preserve_results():
         got = np.concatenate([p[i] for p in parts])
         assert np.array_equal(got.view(np.uint8), np.asarray(full[i]).view(np.uint8))
     assert packed.split(1) == [(s, s + 1) for s in range(packed.n_sent)]
+
+
+@pytest.mark.parametrize('k', [33, 64, 100, 256])
+def test_c_oracle_matches_python_oracle_at_large_beams(k):
+    """Beams above the golden vectors' k = 16: the C restatement equals the
+    pure-Python one (pinned to the reference by the golden vectors, and
+    generic in k like beam.py:64-86) on every mature, so the device's
+    big-beam kernels have an oracle."""
+    raw = synth.make_lattices(10, seed=21 + k, eojeols=4)
+    sm = synth.make_model(raw, seed=21, n_features=3000)
+    sents, dic, coef = synth.to_words(raw, sm)
+    funcs = SF.BeamScoreFunctions(SF.RegularizationScore(),
+                                  SF.SimpleTrigramFeatureScore(FE.SimpleTrigramEncoder(dic), coef))
+    lm = lowering.LoweredModel(funcs)
+    pk, objs = packer.pack(sents, lm)
+    count, length, score, codes, _, _ = lt_oracle.decode(pk, lm.keys, lm.coefs, k)
+    cum = np.concatenate([[0], np.cumsum(pk.sent_n.astype(np.int64))])
+    n_full = 0
+    for s, (b, c) in enumerate(sents):
+        got = ref_beam.beam_search(b, c, funcs, k)
+        assert int(count[s]) == len(got)
+        n_full += len(got) == k
+        for t, (path, sc) in enumerate(got):
+            assert float(sc).hex() == float(score[s, t]).hex()
+            L = int(length[s, t])
+            off = k * cum[s] + t * len(c)
+            assert [tuple(w) for w in path[1:-1]] == [tuple(objs[s][x]) for x in codes[off:off + L]]
+    assert n_full > 0
