@@ -176,15 +176,17 @@ def algorithmic_bytes(piece, n_dict, tuples, length, count, k):
     return 32 * n_dict + int(np.sum(8 * (8 * n + 1) + 4 * 8 * n)) + 24 * tuples + 8 * T * n_dict + out
 
 
-def kernel_bytes(piece, probes, k):
+def kernel_bytes(piece, table_loads, k):
     """Bytes the decode kernel itself issues per launch (not the §8(d)
     algorithm count): every node record once (48 B), the span starts and
-    per-sentence offsets, 32 B per cuckoo-table probe (both 16 B slots),
-    the backpointer and padded result writes."""
+    per-sentence offsets, 16 B per feature-table slot load (counted by the
+    counting launch: the primary slot of every probe past the pre-filter,
+    the secondary only at flagged slots), the backpointer and padded result
+    writes."""
     S = piece.n_sent
     n = np.asarray(piece.sent_n, dtype=np.int64)
     chars = int(n.sum())
-    return (48 * piece.n_nodes + 4 * int(len(piece.span_start)) + 36 * S + 32 * probes
+    return (48 * piece.n_nodes + 4 * int(len(piece.span_start)) + 36 * S + 16 * table_loads
             + 4 * int(((n + 1) * k).sum()) + 4 * chars * k + 12 * S * k + 4 * S)
 
 
@@ -337,7 +339,7 @@ def main():
     t_up = time.perf_counter()
     db = _capi.DeviceBatch(ctx, piece, max_k=k)          # H2D, outside the timed region
     t_up = time.perf_counter() - t_up
-    expansions, tuples, probes = db.count_ops(dm, k)
+    expansions, tuples, probes, table_loads = db.count_ops(dm, k)
 
     # result gather to rank 0 over RCCL/xGMI (the path's one exchange step)
     gather = d.world > 1 if a.gather is None else bool(a.gather)
@@ -427,7 +429,7 @@ def main():
     avg_kernel_s = float(np.mean(kern)) / 1e3
     nd = dict_nodes(raw, order, lo, hi)
     B = algorithmic_bytes(piece, nd, tuples, length, count, k)
-    KB = kernel_bytes(piece, probes, k)
+    KB = kernel_bytes(piece, table_loads, k)
     achieved = B / avg_kernel_s / 1e9
     al = lambda x: (x + 15) // 16 * 16                      # noqa: E731
     if comm:
@@ -485,7 +487,7 @@ def main():
                 'launch': 'rank 0 shard' if d.world > 1 else 'whole batch',
             },
             'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
-                               'table_probes': probes},
+                               'table_probes': probes, 'table_slot_loads': table_loads},
             'kernel_only_sentences_per_s': piece.n_sent / avg_kernel_s,
             'd2h': {'bytes_per_step': d2h, 'in_timed_region': True,
                     'how': ('rank 0: every rank\'s packed results (gathered slabs), used bytes to '

@@ -155,7 +155,7 @@ def load(path=None):
             'lt_slab_parse': (i32, [vp, C.c_uint64, C.POINTER(PackedView)]),
             'lt_decode': (i32, [vp, vp, vp, C.c_int, C.POINTER(Result)]),
             'lt_count_ops': (i32, [vp, vp, vp, C.c_int, C.POINTER(i64), C.POINTER(i64),
-                                   C.POINTER(i64)]),
+                                   C.POINTER(i64), C.POINTER(i64)]),
             'lt_comm_library': (C.c_char_p, []),
             'lt_comm_unique_id': (i32, [C.c_char_p]),
             'lt_comm_create': (i32, [vp, C.c_int, C.c_int, C.c_char_p, C.POINTER(vp)]),
@@ -406,10 +406,11 @@ class DeviceBatch:
         return self.results_packed()
 
     def count_ops(self, model, k):
-        x, p, q = C.c_int64(), C.c_int64(), C.c_int64()
+        """(expansions, feature tuples, probes, table loads) of beam k."""
+        x, p, q, t = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
         check(self.ctx._lib.lt_count_ops(self.ctx.handle, model.handle, self.handle, int(k),
-                                         C.byref(x), C.byref(p), C.byref(q)))
-        return x.value, p.value, q.value
+                                         C.byref(x), C.byref(p), C.byref(q), C.byref(t)))
+        return x.value, p.value, q.value, t.value
 
     def close(self):
         if self.handle:

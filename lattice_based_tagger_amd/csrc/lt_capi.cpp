@@ -99,7 +99,8 @@ struct KeyRec {
 
 struct lt_model {
   lt_ctx* ctx = nullptr;
-  void* d_table = nullptr;
+  void* d_table = nullptr;      // with overflow flags (beam 1: primary first)
+  void* d_plain = nullptr;      // the same slots, flags cleared (beams > 1 load both slots)
   int64_t slots = 0;
   uint32_t seed = 0;
   int narrow = 0;          // 16 B SlotN (all ids < 2^20) or 32 B SlotW
@@ -129,21 +130,29 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
   std::vector<int32_t> who(slots, -1);          // key index held by each slot
   uint64_t rng = 0x9E3779B97F4A7C15ull ^ seed;
   const int max_kicks = 2000;
-  for (int32_t i = 0; i < (int32_t)keys.size(); ++i) {
+  // Phase 1: every key whose primary slot is still free takes it (the fewest
+  // keys end up at a secondary: only those whose primary another key took).
+  // Phase 2: the rest by cuckoo insertion.
+  std::vector<uint32_t> prim(keys.size()), sec(keys.size());
+  std::vector<int32_t> rest;
+  for (size_t i = 0; i < keys.size(); ++i) {
+    table_slots<SlotT>(keys[i], seed, hk, slots, prim[i], sec[i]);
+    if (who[prim[i]] < 0) who[prim[i]] = (int32_t)i;
+    else rest.push_back((int32_t)i);
+  }
+  auto same = [&](int32_t w, const KeyRec& k) {
+    return w >= 0 && keys[(size_t)w].a == k.a && keys[(size_t)w].b == k.b && keys[(size_t)w].c == k.c &&
+           keys[(size_t)w].cls == k.cls;
+  };
+  for (int32_t i : rest) {
+    // a key equal to this one (placed earlier) sits at one of its two slots
+    const KeyRec& ki = keys[(size_t)i];
+    if (same(who[prim[(size_t)i]], ki) || same(who[sec[(size_t)i]], ki)) {
+      *dup = i;
+      return false;
+    }
     int32_t cur = i;
     uint32_t i1, i2;
-    {
-      const KeyRec& k = keys[(size_t)i];
-      table_slots<SlotT>(k, seed, hk, slots, i1, i2);
-      for (uint32_t x : {i1, i2}) {
-        const int32_t w = who[x];
-        if (w >= 0 && keys[(size_t)w].a == k.a && keys[(size_t)w].b == k.b &&
-            keys[(size_t)w].c == k.c && keys[(size_t)w].cls == k.cls) {
-          *dup = i;
-          return false;
-        }
-      }
-    }
     uint32_t pos = 0;
     bool placed = false;
     for (int kick = 0; kick < max_kicks; ++kick) {
@@ -165,15 +174,39 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
     }
     if (!placed) return false;
   }
+  // Primary first: move keys that sit at their secondary slot back to their
+  // primary when it is free, or when its holder sits at its own secondary and
+  // can go back to a free primary.  Fewer secondaries = fewer flagged slots =
+  // fewer second loads per lookup (lt_common.h).
+  for (int pass = 0; pass < 4; ++pass) {
+    int64_t moved = 0;
+    for (uint32_t x = 0; x < slots; ++x) {
+      const int32_t kx = who[x];
+      if (kx < 0 || prim[(size_t)kx] == x) continue;
+      const uint32_t p = prim[(size_t)kx];
+      const int32_t y = who[p];
+      if (y < 0) {
+        who[p] = kx; who[x] = -1; ++moved;
+      } else if (prim[(size_t)y] != p && who[prim[(size_t)y]] < 0) {
+        who[prim[(size_t)y]] = y; who[p] = kx; who[x] = -1; ++moved;
+      }
+    }
+    if (!moved) break;
+  }
   for (uint32_t x = 0; x < slots; ++x) {
     if (who[x] < 0) continue;
     const KeyRec& k = keys[(size_t)who[x]];
     SlotT& sl = tab[x];
     if constexpr (sizeof(SlotT) == sizeof(SlotN)) {
-      sl.key = narrow_key(k.a, k.b, k.c, k.cls);
+      sl.key |= narrow_key(k.a, k.b, k.c, k.cls);
       sl.coef = k.coef;
     } else {
-      sl.a = k.a; sl.b = k.b; sl.c = k.c; sl.cls1 = k.cls + 1; sl.coef = k.coef;
+      sl.a = k.a; sl.b = k.b; sl.c = k.c; sl.cls1 |= k.cls + 1; sl.coef = k.coef;
+    }
+    const uint32_t p = prim[(size_t)who[x]];
+    if (p != x) {                                // at its secondary: flag the primary
+      if constexpr (sizeof(SlotT) == sizeof(SlotN)) tab[p].key |= FLAG_N;
+      else tab[p].cls1 |= FLAG_W;
     }
   }
   return true;
@@ -400,6 +433,8 @@ static lt_status model_upload(lt_ctx* c, const lt_model_image* v, lt_model** out
   hipError_t e = hipMalloc(&m->d_table, (size_t)v->table_bytes);
   if (e == hipSuccess)
     e = hipMemcpyAsync(m->d_table, v->table, (size_t)v->table_bytes, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMalloc(&m->d_plain, (size_t)v->table_bytes);
+  if (e == hipSuccess) e = launch_strip_flags(m->d_plain, m->d_table, v->table_bytes, m->narrow != 0, c->stream);
   if (e == hipSuccess && v->d3mul) {
     m->d3mul = v->d3mul;
     e = dalloc_copy(&m->d_d3, v->d3, (size_t)D3_DIM * D3_DIM, c->stream);
@@ -407,6 +442,7 @@ static lt_status model_upload(lt_ctx* c, const lt_model_image* v, lt_model** out
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     dfree(m->d_table);
+    dfree(m->d_plain);
     dfree(m->d_d3);
     delete m;
     return fail(LT_EHIP, "lt_model_create: %s", hipGetErrorString(e));
@@ -448,6 +484,7 @@ lt_status lt_model_destroy(lt_model* m) {
   if (!m) return LT_OK;
   (void)hipSetDevice(m->ctx->device);
   dfree(m->d_table);
+  dfree(m->d_plain);
   dfree(m->d_d3);
   delete m;
   return LT_OK;
@@ -866,7 +903,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
     return fail(LT_EUNSUPPORTED, "decode: beam %d not in 1..%d (batch max_k)", k, b->max_k);
   if (beam_template_for(k) < 0) return fail(LT_EUNSUPPORTED, "decode: beam %d not compiled", k);
   p = DecodeParams{};
-  p.table = m->d_table;
+  p.table = k == 1 ? m->d_table : m->d_plain;     // beam 1 probes primary first (flags)
   p.slots = (uint32_t)m->slots;
   p.seed = m->seed;
   p.hk = narrow_hash(m->seed);
@@ -1183,7 +1220,7 @@ lt_status lt_decode(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_result*
 }
 
 lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t* expansions,
-                       int64_t* feature_tuples, int64_t* probes) {
+                       int64_t* feature_tuples, int64_t* probes, int64_t* table_loads) {
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
@@ -1203,6 +1240,7 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   if (expansions) *expansions = (int64_t)h[0];
   if (feature_tuples) *feature_tuples = (int64_t)h[1];
   if (probes) *probes = (int64_t)h[2];
+  if (table_loads) *table_loads = (int64_t)h[3];
   return LT_OK;
 }
 

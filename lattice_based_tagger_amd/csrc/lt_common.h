@@ -39,22 +39,31 @@ constexpr int MAX_SPAN = 8;
 constexpr int RING = MAX_SPAN + 1;     // frontier positions e-8 .. e
 
 // -- feature hash table ----------------------------------------------------
-// Narrow slot (16 B): exact 64-bit key cls<<60 | a<<40 | b<<20 | c, valid
-// when every interned id is < 2^20.  key 0 = empty (ids are >= 1).
+// Narrow slot (16 B): exact 64-bit key c3<<60 | a<<40 | b<<20 | c (c3 = the
+// class in 3 bits, cls_code), valid when every interned id is < 2^20; bit 63
+// is the slot's overflow flag (below).  key 0 = empty (ids are >= 1).
 constexpr int NARROW_ID_BITS = 20;
 struct alignas(16) SlotN {
   uint64_t key;
   double coef;
 };
-// Wide slot (32 B): {a, b, c, class+1}; cls1 0 = empty.
+// Wide slot (32 B): {a, b, c, class+1 | overflow flag in bit 31}; 0 = empty.
 struct alignas(32) SlotW {
   uint32_t a, b, c, cls1;
   double coef;
   uint64_t pad;
 };
 
+// Overflow flag ("primary first" cuckoo): every key lives in one of its two
+// candidate slots i1 (primary) / i2 (secondary), and slot i1 carries the flag
+// iff some key whose primary is i1 lives at its secondary.  A lookup loads i1;
+// only on a miss at a flagged slot does it load i2 -- about 1.1 loads per
+// probe instead of 2 (the probes are bound by random cache-line requests).
+constexpr uint64_t FLAG_N = 1ull << 63;
+constexpr uint32_t FLAG_W = 1u << 31;
+LT_HD uint32_t cls_code(uint32_t cls) { return cls == 8 ? 4u : cls; }   // {0,1,2,3,7,8} -> 3 bits
 LT_HD uint64_t narrow_key(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
-  return ((uint64_t)cls << 60) | ((uint64_t)a << 40) | ((uint64_t)b << 20) | (uint64_t)c;
+  return ((uint64_t)cls_code(cls) << 60) | ((uint64_t)a << 40) | ((uint64_t)b << 20) | (uint64_t)c;
 }
 
 // Cuckoo hashing: every key lives in one of its two candidate slots, so a
@@ -108,7 +117,7 @@ LT_HD void cuckoo_slots(KeyBase kb, uint32_t seed, uint32_t slots, uint32_t& i1,
 // reseeds, which changes every constant).  No 32-bit multiply per lookup
 // besides the range reduction (v_mul_u32_u24 is full rate; v_mul_lo_u32 is
 // quarter rate).
-constexpr uint32_t HASH_VERSION = 2;
+constexpr uint32_t HASH_VERSION = 3;     // 3: overflow flags, 3-bit class code
 struct NarrowHash {
   uint32_t k1a, k1b, k1c, k1s, k2a, k2b, k2c, k2s;
 };
@@ -126,12 +135,28 @@ LT_HD NarrowHash narrow_hash(uint32_t seed) {
   }
   return NarrowHash{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
 }
+LT_HD uint32_t narrow_slot1(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
+                            uint32_t slots) {
+  return slot_of(mul24(a, h.k1a) ^ mul24(b, h.k1b) ^ mul24(c, h.k1c) ^ (cls * h.k1s), slots);
+}
+LT_HD uint32_t narrow_slot2(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
+                            uint32_t slots) {
+  return slot_of(mul24(a, h.k2a) ^ mul24(b, h.k2b) ^ mul24(c, h.k2c) ^ (cls * h.k2s), slots);
+}
 LT_HD void narrow_slots(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
                         uint32_t slots, uint32_t& i1, uint32_t& i2) {
-  const uint32_t b1 = mul24(a, h.k1a) ^ mul24(b, h.k1b) ^ mul24(c, h.k1c) ^ (cls * h.k1s);
-  const uint32_t b2 = mul24(a, h.k2a) ^ mul24(b, h.k2b) ^ mul24(c, h.k2c) ^ (cls * h.k2s);
-  i1 = slot_of(b1, slots);
-  i2 = slot_of(b2, slots);
+  i1 = narrow_slot1(h, a, b, c, cls, slots);
+  i2 = narrow_slot2(h, a, b, c, cls, slots);
+}
+// Wide tables: the primary / secondary slot alone (as cuckoo_slots).
+LT_HD uint32_t wide_slot1(uint32_t a, uint32_t b, uint32_t c, uint32_t cls, uint32_t seed, uint32_t slots) {
+  return slot_of(mix1(((a * 0x9E3779B1u) ^ (b * 0x85EBCA77u) ^ (c * 0xC2B2AE3Du) ^ (cls * 0x27D4EB2Fu)) ^ seed),
+                 slots);
+}
+LT_HD uint32_t wide_slot2(uint32_t a, uint32_t b, uint32_t c, uint32_t cls, uint32_t seed, uint32_t slots) {
+  return slot_of(mix1(((a * 0x7FEB352Du) ^ (b * 0x846CA68Bu) ^ (c * 0xD35A2D97u) ^ (cls * 0x165667B1u)) ^
+                      (seed * 0x9E3779B1u + 0x632BE5ABu)),
+                 slots);
 }
 
 // Dense class-3 table: the (t_j, t_k) keys of a model whose class-3 tag values

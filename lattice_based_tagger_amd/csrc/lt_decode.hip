@@ -35,6 +35,7 @@
 // order.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <math.h>
@@ -171,7 +172,15 @@ __device__ __forceinline__ double numpy_sum9(const double (&v)[9], const bool (&
   return s;
 }
 
-// Slot access per table format.
+// LDS-resident parts of the model a block stages at its start.
+struct Aux {
+  const double* d3;       // dense class-3 table (D3_DIM^2) or nullptr
+  uint32_t d3mul;
+  NarrowHash hk;          // narrow table slot hash
+};
+
+// Slot access per table format.  A slot's key carries the overflow flag of
+// the "primary first" cuckoo table (lt_common.h); query keys never do.
 template <bool NARROW>
 struct Tab;
 
@@ -183,18 +192,23 @@ struct Tab<true> {
   __device__ static Key key(uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
     return narrow_key(a, b, c, cls);
   }
-  __device__ static bool hit(const S& s, Key k) { return s.key == k; }
+  __device__ static bool hit(const S& s, Key k) { return (s.key & ~FLAG_N) == k; }
+  __device__ static bool hit_plain(const S& s, Key k) { return s.key == k; }
+  __device__ static bool flagged(const S& s) { return (s.key & FLAG_N) != 0; }
+  __device__ static uint32_t slot1(const Aux& x, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
+                                   uint32_t, uint32_t slots) {
+    return narrow_slot1(x.hk, a, b, c, cls, slots);
+  }
+  __device__ static uint32_t slot2(const Aux& x, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
+                                   uint32_t, uint32_t slots) {
+    return narrow_slot2(x.hk, a, b, c, cls, slots);
+  }
   __device__ static S load(rsrc_t t, uint32_t off) {
     const u32x4 v = ld128(t, off);
     S s;
     s.key = ((uint64_t)v.y << 32) | v.x;
     s.coef = __builtin_bit_cast(double, (u32x2){v.z, v.w});
     return s;
-  }
-  // 0 = empty, 1 = hit, 2 = other key (continue)
-  __device__ static int test(const S& s, uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
-    if (s.key == narrow_key(a, b, c, cls)) return 1;
-    return s.key == 0 ? 0 : 2;
   }
 };
 
@@ -207,7 +221,19 @@ struct Tab<false> {
     return Key{a, b, c, cls + 1};
   }
   __device__ static bool hit(const S& s, Key k) {
+    return (s.cls1 & ~FLAG_W) == k.cls1 && s.a == k.a && s.b == k.b && s.c == k.c;
+  }
+  __device__ static bool flagged(const S& s) { return (s.cls1 & FLAG_W) != 0; }
+  __device__ static bool hit_plain(const S& s, Key k) {
     return s.cls1 == k.cls1 && s.a == k.a && s.b == k.b && s.c == k.c;
+  }
+  __device__ static uint32_t slot1(const Aux&, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
+                                   uint32_t seed, uint32_t slots) {
+    return wide_slot1(a, b, c, cls, seed, slots);
+  }
+  __device__ static uint32_t slot2(const Aux&, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
+                                   uint32_t seed, uint32_t slots) {
+    return wide_slot2(a, b, c, cls, seed, slots);
   }
   __device__ static S load(rsrc_t t, uint32_t off) {
     const u32x4 k = ld128(t, off);
@@ -217,34 +243,33 @@ struct Tab<false> {
     s.coef = __builtin_bit_cast(double, v);
     return s;
   }
-  __device__ static int test(const S& s, uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
-    if (s.cls1 == cls + 1 && s.a == a && s.b == b && s.c == c) return 1;
-    return s.cls1 == 0 ? 0 : 2;
-  }
 };
 
 struct Counts {
-  unsigned long long exp = 0, tup = 0, probe = 0;
+  unsigned long long exp = 0, tup = 0, probe = 0, load = 0;
 };
 
 // Trigram score of appending candidate c after hypothesis h
 // (score_funcs.py:137-144 over feature.py:76-121), in two phases so that
 // other loads can be issued while the probes are in flight:
-//   probe_issue   -- keys, hashes, one buffer load per needed probe
-//   probe_finish  -- match / collision chains, numpy-order sum
-template <bool NARROW>
+//   probe_issue   -- keys, hashes, the primary slot load of each needed probe
+//                    (BOTH: the secondary slot too)
+//   probe_second  -- primary hit, or a miss at a flagged slot: load the
+//                    secondary (nothing to load under BOTH)
+//   probe_finish  -- secondary hits, numpy-order sum
+// BOTH: load the secondary slot together with the primary (one memory round
+// trip, two loads per probe) instead of only at flagged primaries (about 1.2
+// loads per probe, a second round trip).  The beam kernels, whose waits are
+// ordered around register-prefetched records, take BOTH.
+template <bool NARROW, bool BOTH = false>
 struct Probe {
-  typename Tab<NARROW>::S s1[6], s2[6];   // the two cuckoo candidates (valid where needed)
+  typename Tab<NARROW>::S s1[6];          // the primary slots (valid where needed)
+  typename Tab<NARROW>::S s2[6];          // the secondary slots (valid where loaded)
   uint32_t need;                           // bit q: probe q is needed
   uint32_t gneed;                          // bit q: probe q went to the global table
   uint32_t lpres;                          // bit q: resolved from LDS and present (coef in s1)
-};
-
-// LDS-resident parts of the model a block stages at its start.
-struct Aux {
-  const double* d3;       // dense class-3 table (D3_DIM^2) or nullptr
-  uint32_t d3mul;
-  NarrowHash hk;          // narrow table slot hash
+  uint32_t hit1;                           // bit q: found at the primary slot
+  uint32_t need2;                          // bit q: secondary slot loaded
 };
 
 // Key components of probe q for (h, c); recomputed where needed instead of
@@ -306,8 +331,8 @@ __device__ __forceinline__ Aux stage_aux(const DecodeParams& p, double* d3l) {
   return a;
 }
 
-template <bool NARROW>
-__device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uint32_t slots,
+template <bool NARROW, bool BOTH>
+__device__ __forceinline__ void probe_issue(Probe<NARROW, BOTH>& P, const Bufs& B, uint32_t slots,
                                             uint32_t seed, const Hyp& h, const Cand& c,
                                             uint32_t need, const Aux& aux) {
   using T = Tab<NARROW>;
@@ -329,21 +354,45 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW>& P, const Bufs& B, uin
     // (slots stay undefined when not needed; probe_finish reads them only
     // under the same predicate)
     if ((gneed >> q) & 1u) {
-      uint32_t i1, i2;
-      if constexpr (NARROW) narrow_slots(aux.hk, K.a[q], K.b[q], K.c[q], PCLS[q], slots, i1, i2);
-      else cuckoo_slots(key_base<false>(K.a[q], K.b[q], K.c[q], PCLS[q]), seed, slots, i1, i2);
-      P.s1[q] = T::load(B.tab, i1 * T::SZ);
-      P.s2[q] = T::load(B.tab, i2 * T::SZ);
+      P.s1[q] = T::load(B.tab, T::slot1(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+      if constexpr (BOTH)
+        P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
     }
   }
 }
 
-template <bool NARROW, bool COUNT>
-__device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp& h,
+template <bool NARROW, bool BOTH>
+__device__ __forceinline__ void probe_second(Probe<NARROW, BOTH>& P, const Bufs& B, uint32_t slots,
+                                             uint32_t seed, const Aux& aux, const Hyp& h,
+                                             const Cand& c) {
+  using T = Tab<NARROW>;
+  // keys recomputed from (h, c), which stay live anyway
+  const Keys K = make_keys(h, c, use_j8_of(h, c));
+  uint32_t hit1 = 0, need2 = 0;
+  if constexpr (!BOTH) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      if ((P.gneed >> q) & 1u) {
+        const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
+        if (T::hit(P.s1[q], key)) {
+          hit1 |= 1u << q;
+        } else if (T::flagged(P.s1[q])) {         // all second loads before any wait
+          need2 |= 1u << q;
+          P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+        }
+      }
+    }
+  }
+  P.hit1 = hit1;
+  P.need2 = need2;
+}
+
+template <bool NARROW, bool COUNT, bool BOTH>
+__device__ __forceinline__ double probe_finish(const Probe<NARROW, BOTH>& P, const Hyp& h,
                                                const Cand& c, Counts& cnt) {
   using T = Tab<NARROW>;
   const uint32_t jm = h.jmask, km = c.mask, im = h.imask;
-  // keys recomputed from (h, c), which stay live anyway
+  const uint32_t hit1 = P.hit1, need2 = P.need2;
   const Keys K = make_keys(h, c, use_j8_of(h, c));
   bool pr6[6];
   double cf[6];
@@ -351,12 +400,25 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
   for (int q = 0; q < 6; ++q) {
     pr6[q] = false;
     cf[q] = 0.0;
-    if ((P.gneed >> q) & 1u) {
+    if constexpr (BOTH) {                       // both slots loaded: branch-free selects
+      if ((P.gneed >> q) & 1u) {
+        const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
+        // BOTH kernels probe the flag-free copy of the table (lt_model.d_plain)
+        const bool m1 = T::hit_plain(P.s1[q], key);
+        const bool m2 = T::hit_plain(P.s2[q], key);
+        pr6[q] = m1 || m2;
+        cf[q] = m1 ? P.s1[q].coef : P.s2[q].coef;
+      } else if ((P.lpres >> q) & 1u) {
+        pr6[q] = true;
+        cf[q] = P.s1[q].coef;
+      }
+    } else if ((hit1 >> q) & 1u) {
+      pr6[q] = true;
+      cf[q] = P.s1[q].coef;
+    } else if ((need2 >> q) & 1u) {
       const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
-      const bool m1 = T::hit(P.s1[q], key);
-      const bool m2 = T::hit(P.s2[q], key);
-      pr6[q] = m1 || m2;
-      cf[q] = m1 ? P.s1[q].coef : P.s2[q].coef;
+      pr6[q] = T::hit(P.s2[q], key);
+      cf[q] = P.s2[q].coef;
     } else if ((P.lpres >> q) & 1u) {          // resolved from LDS
       pr6[q] = true;
       cf[q] = P.s1[q].coef;
@@ -377,6 +439,7 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW>& P, const Hyp
     const bool use_i8 = (km & F_CTX) && !(jm & F_CTX) && has_i && (im & F_CTX);
     cnt.tup += 6 + ((jm & F_UNK) ? 1 : 0) + (has_i ? 1 : 0) + ((use_j8 || use_i8) ? 1 : 0);
     cnt.probe += __builtin_popcount(P.need);
+    cnt.load += BOTH ? 2 * __builtin_popcount(P.gneed) : __builtin_popcount(P.gneed) + __builtin_popcount(need2);
   }
   return numpy_sum9(v, pr);
 }
@@ -387,7 +450,8 @@ __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_
                                           const Aux& aux) {
   Probe<NARROW> P;
   probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c), aux);
-  return probe_finish<NARROW, COUNT>(P, h, c, cnt);
+  probe_second<NARROW>(P, B, slots, seed, aux, h, c);
+  return probe_finish<NARROW, COUNT, false>(P, h, c, cnt);
 }
 
 // inc = ((0 + pre...) + tri) + post...   (score_funcs.py:50-54)
@@ -603,18 +667,21 @@ lt_viterbi_pk(DecodeParams p) {
     Probe<NARROW> P;
     probe_issue<NARROW>(P, B, slots, seed, h0, cur,
                         (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, aux);
-    // the next macro-step's records are DMA'd only now: an LDS read issued
-    // after a buffer->LDS DMA waits for it (vmcnt), so the probes' own LDS
-    // reads (dense class-3 table) must come first
+    // primary slots back: hits, and the secondary loads of misses at flagged
+    // slots -- issued before the next macro-step's records are DMA'd, so the
+    // DMA's latency hides under theirs.  The DMA comes after every LDS read of
+    // this step's scoring: an LDS read issued after a buffer->LDS DMA waits
+    // for it (vmcnt).
+    const Hyp h1 = read_hyp(R[msr][act ? bm0 : 0]);
+    if (!skip0 && has_tri) probe_second<NARROW>(P, B, slots, seed, aux, h1, cur);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
     dma_packed(B, gn1, wst, lane);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    const Hyp h1 = read_hyp(R[msr][act ? bm0 : 0]);
     double best_s = -INFINITY;
     if (!skip0) {
-      const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h1, cur, cnt) : 0.0;
+      const double tri = has_tri ? probe_finish<NARROW, COUNT, false>(P, h1, cur, cnt) : 0.0;
       if (COUNT) ++cnt.exp;
       best_s = h1.score + increment(p, cur, tri, gn0);              // beam.py:115
     }
@@ -684,11 +751,12 @@ lt_viterbi_pk(DecodeParams p) {
   }
   if (COUNT) {
     const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
-                             pb = group_sum<64>(cnt.probe);
+                             pb = group_sum<64>(cnt.probe), ld = group_sum<64>(cnt.load);
     if (lane == 0) {
       atomicAdd(p.counters + 0, ex);
       atomicAdd(p.counters + 1, tu);
       atomicAdd(p.counters + 2, pb);
+      atomicAdd(p.counters + 3, ld);
     }
   }
 }
@@ -887,12 +955,13 @@ lt_beam_pk(DecodeParams p) {
         const Hyp h0 = read_entry(R[hb][hr]);
         // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
         const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));
-        Probe<NARROW> P;
+        Probe<NARROW, true> P;
         probe_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
         asm volatile("" ::: "memory");
         const Hyp h1 = read_entry(R[hb][hr]);
         if (!skip) {
-          const double tri = has_tri ? probe_finish<NARROW, COUNT>(P, h1, c, cnt) : 0.0;
+          const double tri = has_tri ? (probe_second<NARROW>(P, B, slots, seed, aux, h1, c),
+                                         probe_finish<NARROW, COUNT, true>(P, h1, c, cnt)) : 0.0;
           if (COUNT) ++cnt.exp;
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
           myk[t] = ord_key(sc);
@@ -1080,11 +1149,12 @@ lt_beam_pk(DecodeParams p) {
   }
   if (COUNT) {
     const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
-                             pb = group_sum<64>(cnt.probe);
+                             pb = group_sum<64>(cnt.probe), ld = group_sum<64>(cnt.load);
     if (lane == 0) {
       atomicAdd(p.counters + 0, ex);
       atomicAdd(p.counters + 1, tu);
       atomicAdd(p.counters + 2, pb);
+      atomicAdd(p.counters + 3, ld);
     }
   }
 }
@@ -1289,12 +1359,13 @@ lt_beam_hw(DecodeParams p) {
         const int hr = act ? r : 0;
         const Hyp h0 = read_entry(R[hb][hr]);
         const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
-        Probe<NARROW> P;
+        Probe<NARROW, true> P;
         probe_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
         asm volatile("" ::: "memory");
         const Hyp h1 = read_entry(R[hb][hr]);
         if (!skip) {
-          const double tri = has_tri ? probe_finish<NARROW, false>(P, h1, c, cnt) : 0.0;
+          const double tri = has_tri ? (probe_second<NARROW>(P, B, slots, seed, aux, h1, c),
+                                         probe_finish<NARROW, false, true>(P, h1, c, cnt)) : 0.0;
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
@@ -1624,4 +1695,36 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipE
   return count ? launch_k<false, true>(p, kt, L) : launch_k<false, false>(p, kt, L);
 }
 
+}  // namespace lt
+
+// ---------------------------------------------------------------------------
+// the flag-free copy of a feature table (lt_model.d_plain)
+// ---------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void lt_strip_flags_k(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                        int64_t n16, uint32_t hi_mask, uint32_t w_mask) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+    uint4 v = src[i];
+    v.y &= hi_mask;           // narrow slot: key high word (bit 63)
+    v.w &= w_mask;            // wide slot, first 16 B: cls1 (bit 31); second 16 B: coef / pad untouched
+    dst[i] = v;
+  }
+}
+}  // namespace
+
+namespace lt {
+hipError_t launch_strip_flags(void* dst, const void* src, int64_t bytes, bool narrow, hipStream_t st) {
+  const int64_t n16 = bytes / 16;
+  if (n16 <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n16 + 255) / 256, 4096);
+  if (narrow) {
+    hipLaunchKernelGGL(lt_strip_flags_k, dim3(blocks), dim3(256), 0, st, (uint4*)dst, (const uint4*)src, n16,
+                       ~(FLAG_N >> 32) & 0xFFFFFFFFu, 0xFFFFFFFFu);
+    return hipGetLastError();
+  }
+  // wide slots are 32 B: even 16 B chunks hold {a, b, c, cls1}; odd ones coef + pad
+  hipLaunchKernelGGL(lt_strip_flags_k, dim3(blocks), dim3(256), 0, st, (uint4*)dst, (const uint4*)src, n16,
+                     0xFFFFFFFFu, ~FLAG_W);
+  return hipGetLastError();
+}
 }  // namespace lt

@@ -118,6 +118,10 @@ hipError_t launch_pack_results(const ResultsPackParams& p, hipStream_t st);
 // pinned host memory of `capacity` bytes.
 hipError_t launch_slab_to_host(const void* slab, void* host, size_t capacity, hipStream_t st);
 
+// dst = the table src with every slot's overflow flag cleared (the copy the
+// beam kernels probe: they load both candidate slots and compare keys plainly)
+hipError_t launch_strip_flags(void* dst, const void* src, int64_t bytes, bool narrow, hipStream_t st);
+
 constexpr int LT_MAX_BEAM_COMPILED = 256;
 int beam_template_for(int k);
 const char* kernel_name_for(int k);

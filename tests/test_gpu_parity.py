@@ -77,7 +77,7 @@ def _gpu_decode(ctx, packed, keys, coefs, k):
                                        (33, 300), (64, 300), (100, 200), (256, 120)])
 def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
     packed, keys, coefs = _synthetic(n_sent, seed=100 + k, n_features=1_000_000)
-    (count, length, score, codes), (ex, tu, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
+    (count, length, score, codes), (ex, tu, _, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
     o_count, o_len, o_score, o_codes, o_ex, o_tu = lt_oracle.decode(packed, keys, coefs, k,
                                                                     nthreads=16)
     assert np.array_equal(count, o_count)
@@ -96,7 +96,7 @@ def test_dense_lattices_with_ties_match_c_oracle(gpu_decoder, k):
     chunks per position.  Bit-exact against the C restatement."""
     packed, keys, coefs = _synthetic(4096 if k == 1 else 1024, seed=300 + k, n_features=200_000,
                                      eojeols=6, extra_lambda=3.0, dup_rate=0.5)
-    (count, length, score, codes), (ex, tu, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
+    (count, length, score, codes), (ex, tu, _, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
     o_count, o_len, o_score, o_codes, o_ex, o_tu = lt_oracle.decode(packed, keys, coefs, k,
                                                                     nthreads=16)
     assert np.array_equal(count, o_count)

@@ -25,12 +25,14 @@ for K in ${KS:-1 2 5 16}; do
   done
   python3 $R/tools/pmc_table.py $O/k$K lt_ > $O/k$K.txt
 done
-if [ -x $R/tools/fetch_calib ]; then
+if [ "${CALIB:-1}" = 1 ] && [ -x $R/tools/fetch_calib ]; then
   i=0
   for G in "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum" "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum" "TA_TA_BUSY_sum GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $G -T --output-format csv -d $O/calib/p$i -o run -- $R/tools/fetch_calib > $O/calib_p$i.log 2>&1 || { echo CALIB_FAIL $i; tail -5 $O/calib_p$i.log; exit 1; }
   done
   timeout -s KILL 120 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/calib/trace -o run -- $R/tools/fetch_calib > $O/calib_trace.log 2>&1 || { echo CALIB_TRACE_FAIL; exit 1; }
+  python3 $R/tools/pmc_table.py $O/calib calib_ dispatch > $O/calib.txt
+  cp $O/calib_p1.log $O/calib_dispatches.jsonl
 fi
 echo COUNTERS_DONE
