@@ -231,6 +231,26 @@ lt_status lt_count_ops(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int 
                        int64_t* expansions, int64_t* feature_tuples, int64_t* probes,
                        int64_t* table_loads);
 
+/* Trace of a decode for beam_search(debug=True) (beam.py:53-57: the growns
+ * of every end position, in generation order, and each position's beam):
+ * a separate, untuned launch with the decoders' scoring code.  Positions of
+ * sentence s are pos_off[s] + e, e = 0..n_s; the caller sizes every array:
+ * position q's expansion slots are [exp_off[q], exp_off[q + 1]) (a position
+ * has at most k x (its candidates) expansions; too few slots -> LT_EINVAL).
+ * The batch must be one launch piece. */
+typedef struct {
+  const int64_t* pos_off;   /* [n_sent + 1] */
+  const int64_t* exp_off;   /* [pos_off[n_sent] + 1], exp_off[pos_off[n_sent]] == n_exp */
+  int64_t n_exp;            /* expansion slots */
+  int32_t* beam_count;      /* [pos_off[n_sent]]: |beam[e]| */
+  uint32_t* beam_gen;       /* [pos_off[n_sent] * k]: expansion index of beam[e][r] */
+  int32_t* exp_count;       /* [pos_off[n_sent]]: expansions enumerated at e */
+  double* exp_score;        /* [n_exp]: score of the grown sequence (0 if skipped) */
+  uint32_t* exp_node;       /* [n_exp]: local node << 11 | (span - 1) << 8 | parent rank */
+  uint8_t* exp_skip;        /* [n_exp]: 1 = skipped (unknown after unknown, beam.py:43-45) */
+} lt_trace;
+lt_status lt_decode_trace(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k, lt_trace* trace);
+
 /* ---- multi-GPU result gather --------------------------------
  * One process per GPU decodes its own shard of sentences: sentences are
  * independent (beam_search keeps no cross-sentence state, beam.py:5-61, and

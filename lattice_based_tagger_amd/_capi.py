@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = (
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
     'lt_result_fetch_packed', 'lt_result_view_packed', 'lt_slab_parse',
     'lt_image_build', 'lt_image_view', 'lt_image_destroy', 'lt_model_create_from_image',
-    'lt_evaluate',
+    'lt_evaluate', 'lt_decode_trace',
     'lt_comm_library', 'lt_comm_unique_id', 'lt_comm_create', 'lt_comm_destroy', 'lt_gather_prepare',
     'lt_gather_launch', 'lt_gather_sync', 'lt_gather_fetch', 'lt_gather_view', 'lt_last_gather_ms',
 )
@@ -148,6 +148,7 @@ def load(path=None):
             'lt_image_destroy': (i32, [vp]),
             'lt_model_create_from_image': (i32, [vp, vp, C.POINTER(vp)]),
             'lt_evaluate': (i32, [vp, vp, vp, vp]),
+            'lt_decode_trace': (i32, [vp, vp, vp, C.c_int, vp]),
             'lt_result_fetch': (i32, [vp, vp]),
             'lt_result_view': (i32, [vp, C.POINTER(Result)]),
             'lt_result_fetch_packed': (i32, [vp, vp]),
@@ -329,6 +330,12 @@ class DeviceModel:
             pass
 
 
+class TraceDesc(C.Structure):
+    _fields_ = [('pos_off', C.c_void_p), ('exp_off', C.c_void_p), ('n_exp', C.c_int64),
+                ('beam_count', C.c_void_p), ('beam_gen', C.c_void_p), ('exp_count', C.c_void_p),
+                ('exp_score', C.c_void_p), ('exp_node', C.c_void_p), ('exp_skip', C.c_void_p)]
+
+
 class DeviceBatch:
     """A packed batch resident on the device (lt_batch)."""
 
@@ -347,6 +354,7 @@ class DeviceBatch:
         post = np.ascontiguousarray(packed.node_post, dtype=np.float64) if n_post else None
         self.n_sent = int(arr['sent_n'].shape[0])
         self.sent_n = arr['sent_n']
+        self._span_start, self._span_off = arr['span_start'], arr['sent_span_off']
         self.cum_n = np.zeros(self.n_sent + 1, dtype=np.int64)
         np.cumsum(self.sent_n, out=self.cum_n[1:])
         desc = BatchDesc(
@@ -404,6 +412,37 @@ class DeviceBatch:
         self.fetch_packed()
         self.ctx.sync()
         return self.results_packed()
+
+    def trace(self, model, k):
+        """Every expansion of every end position (lt_decode_trace), as a dict
+        of arrays: pos_off (positions of sentence s: pos_off[s] + e),
+        exp_off, beam_count, beam_gen [positions, k], exp_count, exp_score,
+        exp_node (bp words), exp_skip."""
+        n = self.sent_n.astype(np.int64)
+        pos_off = np.zeros(self.n_sent + 1, dtype=np.int64)
+        np.cumsum(n + 1, out=pos_off[1:])
+        P = int(pos_off[-1])
+        # slots of position e of sentence s: k x (candidates ending at e)
+        span = np.ascontiguousarray(self._span_start, dtype=np.int64)
+        span_off = self._span_off
+        bound = np.zeros(P, dtype=np.int64)
+        for s in range(self.n_sent):
+            ns = int(n[s])
+            if ns:
+                a = span[span_off[s]:span_off[s] + 8 * ns + 1]
+                bound[pos_off[s] + 1:pos_off[s] + 1 + ns] = (a[8::8] - a[0:-1:8]) * int(k)
+        exp_off = np.zeros(P + 1, dtype=np.int64)
+        np.cumsum(bound, out=exp_off[1:])
+        n_exp = int(exp_off[-1])
+        out = {'pos_off': pos_off, 'exp_off': exp_off,
+               'beam_count': np.zeros(P, dtype=np.int32), 'beam_gen': np.zeros((P, int(k)), dtype=np.uint32),
+               'exp_count': np.zeros(P, dtype=np.int32), 'exp_score': np.zeros(max(n_exp, 1), dtype=np.float64),
+               'exp_node': np.zeros(max(n_exp, 1), dtype=np.uint32), 'exp_skip': np.zeros(max(n_exp, 1), dtype=np.uint8)}
+        desc = TraceDesc(*[_ptr(out[f]) for f in ('pos_off', 'exp_off')], n_exp,
+                         *[_ptr(out[f]) for f in ('beam_count', 'beam_gen', 'exp_count', 'exp_score',
+                                                 'exp_node', 'exp_skip')])
+        check(self.ctx._lib.lt_decode_trace(self.ctx.handle, model.handle, self.handle, int(k), C.byref(desc)))
+        return out
 
     def count_ops(self, model, k):
         """(expansions, feature tuples, probes, table loads) of beam k."""

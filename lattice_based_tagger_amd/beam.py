@@ -509,8 +509,68 @@ def _typed_scores(model, packed, glob, seg, Lf, first, score, n, T, bos, flat):
 
 
 def beam_search(bindex, chars, score_functions, beam_size=5, max_len=8, debug=False):
-    """Drop-in for the reference ``beam_search`` (`beam.py:5-61`)."""
+    """Drop-in for the reference ``beam_search`` (`beam.py:5-61`).  With
+    ``debug=True`` the growns of every end position are printed as the
+    reference prints them (`beam.py:53-57`), from the device trace."""
     if debug:
-        raise NotImplementedError('debug=True (per-position hypothesis dump) is not available '
-                                  'from the device decoder')
+        debug_dump(bindex, chars, score_functions, beam_size, max_len)
     return beam_search_batch([(bindex, chars)], score_functions, beam_size, max_len)[0]
+
+
+def debug_dump(bindex, chars, score_functions, beam_size=5, max_len=8, device=0, file=None):
+    """Print, for each end position e, every hypothesis grown there -- sorted
+    by score, ties in generation order -- exactly as the reference's
+    ``debug=True`` branch (`beam.py:53-57`) does.  The expansions and beams
+    come from the device trace (``lt_decode_trace``: the decoders' scoring
+    code, every expansion kept); paths are rebuilt here from the beams'
+    parent links."""
+    import sys
+    out = file or sys.stdout
+    k = _check_beam(beam_size)
+    model = lowered_model(score_functions)
+    packed, objs = pack([(bindex, chars)], model, max_len)      # the Word objects, not views
+    if len(chars) == 0:
+        return
+    # beam_size 0 keeps no hypothesis past BOS (beam.py:85 slices to []): the
+    # growns of e are BOS's expansions (b = 0), which a beam-1 trace also
+    # enumerates with the same scores and order
+    kt = max(k, 1)
+    dec = Decoder.get(device)
+    dm = dec.device_model(model)
+    db = _capi.DeviceBatch(dec.ctx, packed, max_k=kt)
+    try:
+        tr = db.trace(dm, kt)
+    finally:
+        db.close()
+    nodes = objs[0]
+    n = len(chars)
+    paths = {(0, 0): (nodes[0],)}
+    off = tr['exp_off']
+    node_of = lambda v: v >> 11                     # noqa: E731  (csrc/lt_common.h bp_pack)
+    span_of = lambda v: ((v >> 8) & 7) + 1           # noqa: E731
+    rank_of = lambda v: v & 255                      # noqa: E731
+
+    def path(pos, rank):
+        got = paths.get((pos, rank))
+        if got is None:
+            v = int(tr['exp_node'][off[pos] + tr['beam_gen'][pos, rank]])
+            got = path(pos - span_of(v), rank_of(v)) + (nodes[node_of(v)],)
+            paths[(pos, rank)] = got
+        return got
+
+    for e in range(1, n + 1):
+        a, m = int(off[e]), int(tr['exp_count'][e])
+        growns = [g for g in range(m) if not tr['exp_skip'][a + g]
+                  and (k > 0 or span_of(int(tr['exp_node'][a + g])) == e)]
+        print('\n{}\nEnd point = {}, len(growns) = {}\n'.format('-' * 40, e, len(growns)), file=out)
+        sc = tr['exp_score']
+        for g in sorted(growns, key=lambda g: -sc[a + g]):      # stable: generation order on ties
+            v = int(tr['exp_node'][a + g])
+            words = list(path(e - span_of(v), rank_of(v)) + (nodes[node_of(v)],))
+            kind = path_score_type(model, words)
+            num_unk = 0
+            for w in reversed(words[1:]):
+                if w.tag0 != Unk:
+                    break
+                num_unk += 1
+            print(Sequence(words, typed_score(kind, sc[a + g]), num_unk), end='\n\n', file=out)

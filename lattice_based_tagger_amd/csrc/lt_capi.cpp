@@ -1219,6 +1219,69 @@ lt_status lt_decode(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_result*
   return LT_OK;
 }
 
+lt_status lt_decode_trace(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_trace* t) {
+  DecodeParams p;
+  lt_status st = fill_params(c, m, b, k, p);
+  if (st != LT_OK) return st;
+  if (!t || !t->pos_off || !t->exp_off || !t->beam_count || !t->beam_gen || !t->exp_count ||
+      (t->n_exp > 0 && (!t->exp_score || !t->exp_node || !t->exp_skip)) || t->n_exp < 0)
+    return fail(LT_EINVAL, "lt_decode_trace: bad trace arrays");
+  if (b->pieces.size() != 1) return fail(LT_EUNSUPPORTED, "lt_decode_trace: batch of several launch pieces");
+  const int64_t S = b->n_sent;
+  if (t->pos_off[0] != 0) return fail(LT_EINVAL, "lt_decode_trace: pos_off[0] != 0");
+  const int64_t P = t->pos_off[S];
+  // (a position whose expansions exceed its slots stops its sentence on the
+  // device and is reported below)
+  for (int64_t s = 0; s < S; ++s)
+    if (t->pos_off[s + 1] <= t->pos_off[s]) return fail(LT_EINVAL, "lt_decode_trace: pos_off not increasing");
+  for (int64_t q = 1; q <= P; ++q)
+    if (t->exp_off[q] < t->exp_off[q - 1]) return fail(LT_EINVAL, "lt_decode_trace: exp_off not increasing");
+  if (t->exp_off[0] < 0 || t->exp_off[P] != t->n_exp)
+    return fail(LT_EINVAL, "lt_decode_trace: exp_off[0] < 0 or exp_off[positions] != n_exp");
+  HIP_TRY(hipSetDevice(c->device));
+  piece_params(b, 0, k, p);
+  p.table = m->d_table;                  // the trace probes primary first (flags)
+  TraceParams tp{};
+  int64_t *d_pos = nullptr, *d_exp = nullptr;
+  void* d_ent = nullptr;
+  int32_t *d_bc = nullptr, *d_ec = nullptr;
+  uint32_t *d_bg = nullptr, *d_node = nullptr;
+  double* d_score = nullptr;
+  uint8_t* d_skip = nullptr;
+  const size_t ne = (size_t)std::max<int64_t>(t->n_exp, 1);
+  hipError_t e = dalloc_copy(&d_pos, t->pos_off, (size_t)S + 1, c->stream);
+  if (e == hipSuccess) e = dalloc_copy(&d_exp, t->exp_off, (size_t)P + 1, c->stream);
+  if (e == hipSuccess) e = hipMalloc(&d_ent, (size_t)P * k * TRACE_ENTRY_BYTES);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_bc, (size_t)P * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_ec, (size_t)P * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_bg, (size_t)P * k * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_node, ne * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_score, ne * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_skip, ne);
+  if (e == hipSuccess) {
+    tp.pos_off = d_pos; tp.exp_off = d_exp; tp.ent = d_ent;
+    tp.beam_count = d_bc; tp.beam_gen = d_bg; tp.exp_count = d_ec;
+    tp.exp_score = d_score; tp.exp_node = d_node; tp.exp_skip = d_skip;
+    e = launch_trace(p, tp, c->stream);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(t->beam_count, d_bc, (size_t)P * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(t->exp_count, d_ec, (size_t)P * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(t->beam_gen, d_bg, (size_t)P * k * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && t->n_exp > 0) {
+    e = hipMemcpyAsync(t->exp_score, d_score, (size_t)t->n_exp * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(t->exp_node, d_node, (size_t)t->n_exp * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(t->exp_skip, d_skip, (size_t)t->n_exp, hipMemcpyDeviceToHost, c->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(d_pos); dfree(d_exp); dfree(d_ent); dfree(d_bc); dfree(d_ec); dfree(d_bg);
+  dfree(d_node); dfree(d_score); dfree(d_skip);
+  if (e != hipSuccess) return fail(LT_EHIP, "lt_decode_trace: %s", hipGetErrorString(e));
+  for (int64_t q = 0; q < P; ++q)
+    if (t->exp_count[q] < 0) return fail(LT_EINVAL, "lt_decode_trace: position %lld has more expansions than slots",
+                                         (long long)q);
+  return LT_OK;
+}
+
 lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t* expansions,
                        int64_t* feature_tuples, int64_t* probes, int64_t* table_loads) {
   DecodeParams p;

@@ -1697,6 +1697,115 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipE
 
 }  // namespace lt
 
+// ===========================================================================
+// trace (beam_search debug=True, beam.py:53-57): one thread per sentence walks
+// the reference loops literally -- b ascending, each hypothesis of beam[b],
+// each candidate of span (b, e) (beam.py:31-48) -- scoring with the decoders'
+// own code, records every expansion, and keeps beam[e] as Beam.append does
+// (stable by score, beam.py:85) by selection.  Diagnostic path: no tuning.
+// ===========================================================================
+namespace {
+template <bool NARROW>
+__global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) {
+  static_assert(sizeof(Entry) == TRACE_ENTRY_BYTES, "trace entry layout");
+  const int s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= p.n_sent) return;
+  const Bufs B = make_bufs(p);
+  const Aux aux{nullptr, 0u, p.hk};             // class 3 from the table itself
+  const int k = p.k;
+  const int n = p.sent_n[s];
+  const uint32_t nbase = (uint32_t)p.node_off[s];
+  const int32_t* ssp = p.span_start + p.span_off[s];
+  const int64_t po = t.pos_off[s];
+  Entry* ent = reinterpret_cast<Entry*>(t.ent) + po * k;
+  Counts cnt;
+  {
+    const Cand b0 = load_cand(B, nbase);        // beam[0] = [BOS] (beam.py:21-23)
+    Entry e0;
+    e0.score = 0.0; e0.f6 = b0.f6;
+    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
+    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+    ent[0] = e0;
+    t.beam_count[po] = 1;
+    t.beam_gen[po * k] = 0u;
+    t.exp_count[po] = 0;
+  }
+  for (int e = 1; e <= n; ++e) {
+    const int dmax = min(e, p.max_len);
+    const int64_t xo = t.exp_off[po + e], xe = t.exp_off[po + e + 1];
+    uint32_t g = 0;
+    for (int j = 0; j < MAX_SPAN; ++j) {        // span j: length d = 8 - j, begin b = e - d
+      const int d = MAX_SPAN - j;
+      if (d > dmax) continue;
+      const int b = e - d;
+      const int lo = ssp[(e - 1) * MAX_SPAN + j], hi = ssp[(e - 1) * MAX_SPAN + j + 1];
+      const int nb = t.beam_count[po + b];
+      for (int r = 0; r < nb; ++r) {
+        const Hyp h = read_entry(ent[(int64_t)b * k + r]);
+        for (int node = lo; node < hi; ++node, ++g) {
+          if (xo + g >= xe) {                   // the caller's slots are too few: report, stop
+            t.exp_count[po + e] = -1;
+            return;
+          }
+          const Cand c = load_cand(B, nbase + (uint32_t)node);
+          const bool skip = (h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax);   // beam.py:43-45
+          double sc = 0.0;
+          if (!skip) {
+            const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux) : 0.0;
+            sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);      // beam.py:115
+          }
+          t.exp_score[xo + g] = sc;
+          t.exp_node[xo + g] = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+          t.exp_skip[xo + g] = skip ? 1 : 0;
+        }
+      }
+    }
+    const uint32_t M = g;
+    t.exp_count[po + e] = (int32_t)M;
+    // beam[e]: the k first of the stable order (score desc, generation asc)
+    int kept = 0;
+    unsigned long long pk = ~0ull;
+    uint32_t pg = 0;
+    bool first = true;
+    for (; kept < k; ++kept) {
+      unsigned long long bk = 0ull;
+      uint32_t bg = INV;
+      for (uint32_t q = 0; q < M; ++q) {
+        if (t.exp_skip[xo + q]) continue;
+        const unsigned long long kk = ord_key(t.exp_score[xo + q]);
+        const bool after = first || kk < pk || (kk == pk && q > pg);
+        if (after && (bg == INV || kk > bk || (kk == bk && q < bg))) { bk = kk; bg = q; }
+      }
+      if (bg == INV) break;
+      first = false;
+      pk = bk; pg = bg;
+      const uint32_t v = t.exp_node[xo + bg];
+      const int d = (int)bp_d(v), r = (int)bp_rank(v), node = (int)bp_node(v);
+      const Entry& h = ent[(int64_t)(e - d) * k + r];
+      const Cand c = load_cand(B, nbase + (uint32_t)node);
+      Entry ne;
+      ne.score = t.exp_score[xo + bg]; ne.f6 = c.f6;
+      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
+      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
+      ne.depth = h.depth + 1;
+      ent[(int64_t)e * k + kept] = ne;
+      t.beam_gen[(po + e) * k + kept] = bg;
+    }
+    t.beam_count[po + e] = kept;
+  }
+}
+}  // namespace
+
+namespace lt {
+hipError_t launch_trace(const DecodeParams& p, const TraceParams& t, hipStream_t st) {
+  const int blocks = (p.n_sent + 63) / 64;
+  if (blocks == 0) return hipSuccess;
+  if (p.narrow) hipLaunchKernelGGL(lt_trace_k<true>, dim3(blocks), dim3(64), 0, st, p, t);
+  else hipLaunchKernelGGL(lt_trace_k<false>, dim3(blocks), dim3(64), 0, st, p, t);
+  return hipGetLastError();
+}
+}  // namespace lt
+
 // ---------------------------------------------------------------------------
 // the flag-free copy of a feature table (lt_model.d_plain)
 // ---------------------------------------------------------------------------

@@ -118,6 +118,24 @@ hipError_t launch_pack_results(const ResultsPackParams& p, hipStream_t st);
 // pinned host memory of `capacity` bytes.
 hipError_t launch_slab_to_host(const void* slab, void* host, size_t capacity, hipStream_t st);
 
+// Trace of a decode (beam_search(debug=True), beam.py:53-57): every expansion
+// of every end position in generation order, and each position's beam.  One
+// thread per sentence over global memory; the same scoring code as the
+// decoders.  Positions of sentence s: pos_off[s] + e (e = 0..n_s).
+constexpr int TRACE_ENTRY_BYTES = 48;
+struct TraceParams {
+  const int64_t* pos_off;       // [n_sent + 1]
+  const int64_t* exp_off;       // [positions + 1]: expansion slots of position q: [exp_off[q], exp_off[q+1])
+  void* ent;                    // [positions * k] hypothesis entries (scratch)
+  int32_t* beam_count;          // [positions]
+  uint32_t* beam_gen;           // [positions * k]: generation index of beam[e][r]
+  int32_t* exp_count;           // [positions]: expansions enumerated at the position (-1: slots too few)
+  double* exp_score;            // [expansion slots]
+  uint32_t* exp_node;           // [expansion slots]: bp_pack(node, span, parent rank)
+  uint8_t* exp_skip;            // [expansion slots]: 1 = skipped (beam.py:43-45)
+};
+hipError_t launch_trace(const DecodeParams& p, const TraceParams& t, hipStream_t st);
+
 // dst = the table src with every slot's overflow flag cleared (the copy the
 // beam kernels probe: they load both candidate slots and compare keys plainly)
 hipError_t launch_strip_flags(void* dst, const void* src, int64_t bytes, bool narrow, hipStream_t st);
