@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -97,8 +98,15 @@ struct KeyRec {
 
 }  // namespace
 
+// Infinite score terms: +inf and -inf may each occur, but not both in one
+// decode -- their sum is a NaN, and the reference ranks by Python's sort,
+// whose order over NaN (every comparison false) is not reproduced.  Bit 0:
+// some +inf, bit 1: some -inf.
+static inline int inf_sign_bits(double v) { return std::isinf(v) ? (v > 0 ? 1 : 2) : 0; }
+
 struct lt_model {
   lt_ctx* ctx = nullptr;
+  int inf_signs = 0;            // inf_sign_bits of the coefficients
   void* d_table = nullptr;      // with overflow flags (beam 1: primary first)
   void* d_plain = nullptr;      // the same slots, flags cleared (beams > 1 load both slots)
   int64_t slots = 0;
@@ -367,8 +375,8 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
     const bool two = (cls == 1 || cls == 3 || cls == 8);
     if (a == 0 || b == 0 || (two ? cc != 0 : cc == 0))
       return fail(LT_EINVAL, "lt_model_create: key %lld has a bad component id", (long long)i);
-    if (!std::isfinite(d->coefs[i]))
-      return fail(LT_EUNSUPPORTED, "lt_model_create: non-finite coefficient at key %lld", (long long)i);
+    if (std::isnan(d->coefs[i]))
+      return fail(LT_EUNSUPPORTED, "lt_model_create: NaN coefficient at key %lld", (long long)i);
     keys[(size_t)i] = KeyRec{a, b, cc, cls, d->coefs[i]};
     max_id = std::max(max_id, std::max(a, std::max(b, cc)));
   }
@@ -430,6 +438,17 @@ static lt_status model_upload(lt_ctx* c, const lt_model_image* v, lt_model** out
   m->slots = v->slots;
   m->seed = v->seed;
   m->narrow = v->narrow ? 1 : 0;
+  {
+    const int64_t sb = m->narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
+    const char* t = static_cast<const char*>(v->table);
+    for (int64_t i = 0; i < v->slots && m->inf_signs != 3; ++i) {
+      double cf;
+      std::memcpy(&cf, t + i * sb + (m->narrow ? offsetof(SlotN, coef) : offsetof(SlotW, coef)), 8);
+      m->inf_signs |= inf_sign_bits(cf);
+    }
+    if (v->d3mul && v->d3)
+      for (int i = 0; i < D3_DIM * D3_DIM; ++i) m->inf_signs |= inf_sign_bits(v->d3[i]);
+  }
   hipError_t e = hipMalloc(&m->d_table, (size_t)v->table_bytes);
   if (e == hipSuccess)
     e = hipMemcpyAsync(m->d_table, v->table, (size_t)v->table_bytes, hipMemcpyHostToDevice, c->stream);
@@ -493,7 +512,7 @@ lt_status lt_model_destroy(lt_model* m) {
 int64_t lt_model_slots(const lt_model* m) { return m ? m->slots : 0; }
 
 // ---------------------------------------------------------------- batch --
-static lt_status validate(const lt_batch_desc* d) {
+static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
   if (d->n_sent < 0 || d->n_nodes < 0 || d->n_span < 0 || d->n_post < 0)
     return fail(LT_EINVAL, "batch: negative size");
   if (d->max_len < 1 || d->max_len > LT_MAX_SPAN)
@@ -522,6 +541,7 @@ static lt_status validate(const lt_batch_desc* d) {
     return nullptr;
   };
   std::vector<Bad> bad(32);
+  std::vector<int> sgn(32, 0);            // inf_sign_bits of the node terms, per worker
   auto note = [](Bad& b, int64_t at, lt_status st, const char* fmt, long long a, long long c, long long e) {
     char buf[256];
     snprintf(buf, sizeof buf, fmt, a, c, e);
@@ -563,15 +583,24 @@ static lt_status validate(const lt_batch_desc* d) {
     for (int64_t i = lo; i < hi; ++i) {
       if (d->node_word[i] < 0 || d->node_morph0[i] < 0 || d->node_tag[i] < 0)
         return note(bad[t], i, LT_EINVAL, "batch: node %lld has a negative id%.0lld%.0lld", i, 0, 0);
-      if (!std::isfinite(d->node_pre[i]) || !std::isfinite(d->node_f4[i]) ||
-          !std::isfinite(d->node_f5[i]) || !std::isfinite(d->node_f6[i]))
-        return note(bad[t], i, LT_EUNSUPPORTED, "batch: node %lld has a non-finite score term%.0lld%.0lld", i, 0, 0);
+      if (std::isnan(d->node_pre[i]) || std::isnan(d->node_f4[i]) || std::isnan(d->node_f5[i]) ||
+          std::isnan(d->node_f6[i]))
+        return note(bad[t], i, LT_EUNSUPPORTED, "batch: node %lld has a NaN score term%.0lld%.0lld", i, 0, 0);
+      sgn[t] |= inf_sign_bits(d->node_pre[i]) | inf_sign_bits(d->node_f4[i]) | inf_sign_bits(d->node_f5[i]) |
+                inf_sign_bits(d->node_f6[i]);
     }
   });
   if (const Bad* x = first_bad(bad)) return fail(x->st, "%s", x->msg.c_str());
-  for (int64_t i = 0; i < (int64_t)d->n_post * d->n_nodes; ++i)
-    if (!std::isfinite(d->node_post[i]))
-      return fail(LT_EUNSUPPORTED, "batch: non-finite post term %lld", (long long)i);
+  int signs = 0;
+  for (int v : sgn) signs |= v;
+  for (int64_t i = 0; i < (int64_t)d->n_post * d->n_nodes; ++i) {
+    if (std::isnan(d->node_post[i])) return fail(LT_EUNSUPPORTED, "batch: NaN post term %lld", (long long)i);
+    signs |= inf_sign_bits(d->node_post[i]);
+  }
+  if (signs == 3)
+    return fail(LT_EUNSUPPORTED, "batch: both +inf and -inf among the node score terms (their sum is a NaN, "
+                                 "whose place in Python's sort is not reproduced)");
+  *inf_signs = signs;
   return LT_OK;
 }
 
@@ -695,12 +724,14 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   *out = nullptr;
   if (max_k < 1 || max_k > LT_MAX_BEAM)
     return fail(LT_EUNSUPPORTED, "lt_batch_create: max_k %d not in 1..%d", max_k, LT_MAX_BEAM);
-  lt_status st = validate(d);
+  int inf_signs = 0;
+  lt_status st = validate(d, &inf_signs);
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
   lt_batch* b = new (std::nothrow) lt_batch;
   if (!b) return fail(LT_ENOMEM, "lt_batch_create: out of host memory");
   b->ctx = c;
+  b->inf_signs = inf_signs;
   b->n_sent = d->n_sent;
   b->max_len = d->max_len;
   b->n_post = d->n_post;
@@ -902,6 +933,9 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   if (k < 1 || k > b->max_k)
     return fail(LT_EUNSUPPORTED, "decode: beam %d not in 1..%d (batch max_k)", k, b->max_k);
   if (beam_template_for(k) < 0) return fail(LT_EUNSUPPORTED, "decode: beam %d not compiled", k);
+  if ((m->inf_signs | b->inf_signs) == 3)
+    return fail(LT_EUNSUPPORTED, "decode: both +inf and -inf among the model's and the batch's score terms "
+                                 "(their sum is a NaN, whose place in Python's sort is not reproduced)");
   p = DecodeParams{};
   p.table = k == 1 ? m->d_table : m->d_plain;     // beam 1 probes primary first (flags)
   p.slots = (uint32_t)m->slots;
@@ -1003,7 +1037,7 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
       return fail(LT_EINVAL, "lt_evaluate: word %lld has a bad predecessor", (long long)w);
   }
   for (int64_t x = 0; x < (int64_t)d->n_terms * d->n_words; ++x)
-    if (!std::isfinite(d->terms[x])) return fail(LT_EUNSUPPORTED, "lt_evaluate: non-finite term");
+    if (std::isnan(d->terms[x])) return fail(LT_EUNSUPPORTED, "lt_evaluate: NaN term");
   HIP_TRY(hipSetDevice(c->device));
   std::vector<NodeRec> recs((size_t)d->n_words);
   for (int64_t w = 0; w < d->n_words; ++w) {

@@ -56,6 +56,7 @@ struct lt_batch {
   lt_ctx* ctx = nullptr;
   int32_t n_sent = 0, max_len = 8, n_post = 0, has_tri = 0, max_k = 1;
   int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
+  int inf_signs = 0;                  // +inf (1) / -inf (2) among the node score terms
   int last_k = 0;
   // device inputs, per launch piece (lt_batch_create: node records and
   // backpointers of a piece stay below 2^31 B)

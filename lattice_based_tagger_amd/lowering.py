@@ -22,9 +22,15 @@ Feature tuples are matched exactly as Python tuple membership does
 values receive the same id iff they compare (and hash) equal.  Id 0 means "occurs
 in no key", which makes every feature containing it absent.
 
+User plugins: a ``BeamScoreFunction`` subclass whose score depends on the
+appended node only may declare ``node_local = True``; its ``score(None, w)``
+is then evaluated once per lattice node (like the three built-in node-local
+scorers) and summed in constructor order.  A plugin that declares it but reads
+``seq`` gets ``None`` and fails loudly.
+
 Unsupported composites (a plugin of any other class, two trigram scorers,
-non-float64 coefficients) raise ``NotImplementedError``: there is no CPU
-fallback decoder.
+non-float64 or NaN coefficients, +inf and -inf terms together) raise: there
+is no CPU fallback decoder.
 """
 
 import numpy as np
@@ -110,11 +116,12 @@ class LoweredModel:
                 if self.trigram is not None:
                     raise NotImplementedError('at most one SimpleTrigramFeatureScore is supported')
                 self.trigram = f
-            elif name in NODE_LOCAL_SCORERS:
+            elif name in NODE_LOCAL_SCORERS or getattr(f, 'node_local', False) is True:
                 (self.post_funcs if self.trigram is not None else self.pre_funcs).append(f)
             else:
                 raise NotImplementedError(
-                    'scorer %s has no device lowering (supported: %s, %s)'
+                    'scorer %s has no device lowering (supported: %s, %s, and any '
+                    'BeamScoreFunction that declares node_local = True)'
                     % (name, ', '.join(NODE_LOCAL_SCORERS), TRIGRAM_SCORER))
         self.vocab = {}
         self.vmask = np.zeros(1, dtype=np.uint32)
@@ -148,6 +155,12 @@ class LoweredModel:
         coef = tri.coefficients
         if not isinstance(coef, np.ndarray) or coef.dtype != np.float64 or coef.ndim != 1:
             raise NotImplementedError('coefficients must be a 1-D float64 numpy array')
+        if np.isnan(coef).any():
+            raise NotImplementedError('NaN coefficients: the order Python\'s sort gives NaN scores '
+                                      'is not reproduced')
+        if np.isposinf(coef).any() and np.isneginf(coef).any():
+            raise NotImplementedError('+inf and -inf coefficients together: their sum is a NaN, whose '
+                                      'order in Python\'s sort is not reproduced')
         dic = enc.feature_dic
         self.feature_dic = dic
         self.coefficients = coef

@@ -198,6 +198,8 @@ class NativePacker:
         kinds, reg, ptag, pkey, pscorer, pval = [], [], [], [], [], []
         for s, f in enumerate(funcs):
             name = type(f).__name__
+            if name not in KIND:                    # a node-local plugin of the user's: Python packer
+                raise Unsupported('scorer %s is evaluated per node in Python' % name)
             kinds.append(KIND[name])
             if name == 'RegularizationScore':
                 reg += [_number(f.unknown_penalty), _number(f.known_preference), _number(f.syllable_penalty)]

@@ -23,7 +23,15 @@ from .tagset import BOS, EOS, Noun, Unk
 
 
 class BeamScoreFunction:
-    """Protocol for one additive term of the expansion score."""
+    """Protocol for one additive term of the expansion score.
+
+    A subclass whose ``score(seq, word_k)`` depends on ``word_k`` only may set
+    ``node_local = True``: the decoder then evaluates ``score(None, w)`` once
+    per lattice node (host side) and adds it on the device in constructor
+    order, as it does for the built-in node-local scorers.  Any other user
+    subclass has no device lowering (``NotImplementedError``)."""
+
+    node_local = False
 
     def __call__(self, sequence, word_k):
         return self.score(sequence, word_k)

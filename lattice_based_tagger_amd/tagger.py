@@ -178,8 +178,9 @@ class Tagger:
         return bindex, chars
 
     def tag(self, sent, beam_size=5, ensure_normalize=True, debug=False):
-        if debug:
-            raise NotImplementedError('debug=True is not available from the device decoder')
+        if debug:                                   # tagger.py:75-76 passes debug to beam_search
+            bindex, chars = self.lattice(sent)
+            return beam_search(bindex, chars, self.score_funcs, beam_size=beam_size, debug=True)[0]
         return self.tag_batch([sent], beam_size=beam_size)[0]
 
     # sentences per pipeline chunk of tag_batch

@@ -110,6 +110,8 @@ def _scorer_value(func, path, wk):
             return 0
         coef = func.coefficients
         return numpy_pairwise_sum([float(coef[i]) for i in idx])
+    if getattr(func, 'node_local', False) is True:           # a user plugin: the reference calls it
+        return func.score(path, wk)                          # (score_funcs.py:50-54); it reads wk only
     raise TypeError('oracle has no restatement of scorer %r' % name)
 
 
