@@ -32,7 +32,12 @@ extern "C" {
 
 #define LT_ABI_VERSION 2   /* 2: compact results (slabs), gathers of slabs */
 #define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
-#define LT_MAX_BEAM 256    /* largest beam_size compiled in */
+#define LT_MAX_BEAM 256    /* largest beam_size of the tuned kernels */
+/* Any other configuration -- max_len > 8 (span slots = max_len) or a beam
+ * above LT_MAX_BEAM -- decodes on the general kernel (lt_beam_wide): beams up
+ * to LT_MAX_BEAM_ANY, span lengths up to LT_MAX_LEN_ANY. */
+#define LT_MAX_BEAM_ANY (1 << 20)
+#define LT_MAX_LEN_ANY (1 << 20)
 
 typedef int32_t lt_status;
 enum {
@@ -106,13 +111,14 @@ int64_t lt_model_slots(const lt_model* model);
  * Replaces the `bindex` / `chars` arguments of beam_search (beam.py:5,
  * consumed at beam.py:25-38).  Layout: DESIGN.md "Data layout in HBM".
  *   sentence s owns local nodes [sent_node_off[s], sent_node_off[s+1]) (node 0 = BOS)
- *   and span entries [sent_span_off[s], sent_span_off[s+1]) (= 8*n_s + 1 entries);
- *   span_start[sent_span_off[s] + (e-1)*8 + (8-d)] = local index of the first
+ *   and span entries [sent_span_off[s], sent_span_off[s+1]) (= S*n_s + 1 entries,
+ *   S = 8 for max_len <= 8, else S = max_len);
+ *   span_start[sent_span_off[s] + (e-1)*S + (S-d)] = local index of the first
  *   candidate of span (e-d, e).
  */
 typedef struct {
   int32_t n_sent;
-  int32_t max_len;        /* 1..8 (beam_search max_len, beam.py:5,30) */
+  int32_t max_len;        /* 1..LT_MAX_LEN_ANY (beam_search max_len, beam.py:5,30) */
   int32_t n_post;         /* node-local terms that follow the trigram term */
   int32_t has_trigram;
   int64_t n_nodes;

@@ -79,7 +79,10 @@ typedef struct {
 /* Packed batch.  The arrays belong to `owner`, one block per pack, valid
  * until lt_packed_release (independent of the packer and of later packs, so
  * a pipeline can hold several).  node_src: >= 0 dictionary word index, -1
- * BOS, -2 - (8 b + d - 1) Unknown node of span (b, b + d). */
+ * BOS, -2 - (b * 2^32 + d - 1) Unknown node of span (b, b + d).
+ * batch.max_len is the effective one: min(max_len, max(8, longest sentence))
+ * -- spans never exceed the sentence, so the decode is the same -- and the
+ * span table has S = max(8, batch.max_len) slots per end position. */
 typedef struct {
   lt_batch_desc batch;
   const int64_t* node_src;
@@ -89,7 +92,7 @@ typedef struct {
 typedef struct lt_packer lt_packer;
 lt_status lt_packer_create(const lt_packer_desc* desc, lt_packer** out);
 lt_status lt_packer_destroy(lt_packer* packer);
-/* max_len as beam_search's (1..8).  Host only; no GPU needed. */
+/* max_len as beam_search's (>= 1).  Host only; no GPU needed. */
 lt_status lt_packer_pack(lt_packer* packer, const lt_lattice_desc* lattices, int max_len, lt_packed* out);
 /* Frees one pack's arrays and zeroes *out (NULL or an already released
  * lt_packed: no-op). */

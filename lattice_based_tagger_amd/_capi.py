@@ -14,7 +14,8 @@ from ._build import LIB
 
 LT_OK = 0
 ABI_VERSION = 2           # include/lattice_decode.h LT_ABI_VERSION
-LT_MAX_BEAM = 256
+LT_MAX_BEAM = 256          # tuned kernels (lattice_decode.h)
+LT_MAX_BEAM_ANY = 1 << 20  # the general kernel lt_beam_wide
 LT_EUNSUPPORTED = -4
 _STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED', -5: 'LT_ERCCL'}
 

@@ -292,8 +292,8 @@ def _check_beam(beam_size):
     k = int(beam_size)
     if k < 0:
         raise NotImplementedError('negative beam_size is not supported')
-    if k > _capi.LT_MAX_BEAM:
-        raise NotImplementedError('beam_size > %d is not compiled in' % _capi.LT_MAX_BEAM)
+    if k > _capi.LT_MAX_BEAM_ANY:
+        raise NotImplementedError('beam_size > %d is not supported' % _capi.LT_MAX_BEAM_ANY)
     return k
 
 
@@ -306,6 +306,17 @@ def beam_search_batch(sentences, score_functions, beam_size=5, max_len=8, device
     sentences = list(sentences)
     k = _check_beam(beam_size)
     model = lowered_model(score_functions)
+    if int(max_len) < 1:
+        # b_min = e - max_len >= e: no span, no expansion, beam[e] = [] for
+        # e >= 1 (beam.py:29-31) and bindex is never read; an empty sentence
+        # keeps [BOS] + EOS, which is its decode at any max_len
+        out = [[] for _ in sentences]
+        empty = [i for i, (_, ch) in enumerate(sentences) if len(ch) == 0]
+        if empty:
+            for i, m in zip(empty, beam_search_batch([sentences[i] for i in empty], score_functions,
+                                                     beam_size, 1, device)):
+                out[i] = m
+        return out
     packed, objs = pack_lattices(sentences, model, max_len)
     return decode_batch(packed, objs, [ch for _, ch in sentences], model, k, device)
 
@@ -452,7 +463,7 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
     unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
     if unk.size:
         code = -2 - src[unk]
-        for j, b, d, s in zip(unk.tolist(), (code // 8).tolist(), (code % 8 + 1).tolist(),
+        for j, b, d, s in zip(unk.tolist(), (code >> 32).tolist(), ((code & 0xFFFFFFFF) + 1).tolist(),
                               (seg[unk] // T).tolist()):
             sub = chars_list[s][b:b + d]
             flat[j] = Word(sub, sub, None, Unk, None, d, b, b + d, False)

@@ -274,6 +274,7 @@ lt_status lt_ctx_destroy(lt_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   dfree(c->d_counters);
+  dfree(c->d_wide);
   for (lt_arena& a : c->spare) {
     dfree(a.d);
     if (a.h) (void)hipHostFree(a.h);
@@ -515,8 +516,9 @@ int64_t lt_model_slots(const lt_model* m) { return m ? m->slots : 0; }
 static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
   if (d->n_sent < 0 || d->n_nodes < 0 || d->n_span < 0 || d->n_post < 0)
     return fail(LT_EINVAL, "batch: negative size");
-  if (d->max_len < 1 || d->max_len > LT_MAX_SPAN)
-    return fail(LT_EUNSUPPORTED, "batch: max_len %d not in 1..%d", d->max_len, LT_MAX_SPAN);
+  if (d->max_len < 1 || d->max_len > LT_MAX_LEN_ANY)
+    return fail(LT_EUNSUPPORTED, "batch: max_len %d not in 1..%d", d->max_len, LT_MAX_LEN_ANY);
+  const int SS = span_slots(d->max_len);
   if (!d->sent_n || !d->sent_node_off || !d->sent_span_off)
     return fail(LT_EINVAL, "batch: NULL sentence arrays");
   if (d->n_nodes > 0 && (!d->node_word || !d->node_morph0 || !d->node_tag || !d->node_mask ||
@@ -555,7 +557,7 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
       const int64_t n = d->sent_n[s];
       const int64_t nodes = d->sent_node_off[s + 1] - d->sent_node_off[s];
       const int64_t spans = d->sent_span_off[s + 1] - d->sent_span_off[s];
-      if (n < 0 || spans != LT_MAX_SPAN * n + 1)
+      if (n < 0 || spans != SS * n + 1)
         return note(bad[t], s, LT_EINVAL, "batch: sentence %lld has %lld span entries for %lld chars", s, spans, n);
       if (nodes < 1 || nodes >= MAX_LOCAL_NODES)
         return note(bad[t], s, LT_EINVAL, "batch: sentence %lld has %lld nodes%.0lld", s, nodes, 0);
@@ -564,10 +566,10 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
         return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span table does not cover its nodes%.0lld%.0lld", s, 0, 0);
       for (int64_t e = 1; e <= n; ++e) {
         const int64_t dmax = std::min<int64_t>(e, d->max_len);
-        for (int j = 0; j < LT_MAX_SPAN; ++j) {
-          const int64_t idx = (e - 1) * LT_MAX_SPAN + j;
+        for (int j = 0; j < SS; ++j) {
+          const int64_t idx = (e - 1) * SS + j;
           const int32_t cnt = ss[idx + 1] - ss[idx];
-          const int dd = LT_MAX_SPAN - j;
+          const int dd = SS - j;
           if (cnt < 0)
             return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span table not monotone%.0lld%.0lld", s, 0, 0);
           if (dd <= dmax && cnt == 0)
@@ -699,6 +701,9 @@ static T* at(char* base, size_t off) {
 // all writing one result array.
 static std::atomic<int64_t> g_piece_bytes{((int64_t)1 << 31) - 1};
 
+// Backpointer words per (position, rank): two for the general kernel.
+static int bp_words(int max_len, int max_k) { return decode_is_wide(max_len, max_k) ? 2 : 1; }
+
 static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc* d, int max_k) {
   const int64_t lim = g_piece_bytes.load();
   std::vector<std::pair<int32_t, int32_t>> out;
@@ -706,7 +711,7 @@ static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc
   int64_t nodes = 0, bp = 0;
   for (int32_t s = 0; s < d->n_sent; ++s) {
     const int64_t sn = (d->sent_node_off[s + 1] - d->sent_node_off[s]) * (int64_t)sizeof(NodeRec);
-    const int64_t sb = ((int64_t)d->sent_n[s] + 1) * max_k * 4;
+    const int64_t sb = ((int64_t)d->sent_n[s] + 1) * max_k * 4 * bp_words(d->max_len, max_k);
     if (s > s0 && (nodes + sn > lim || bp + sb > lim)) {
       out.emplace_back(s0, s);
       s0 = s;
@@ -722,8 +727,8 @@ static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc
 lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch** out) {
   if (!c || !d || !out) return fail(LT_EINVAL, "lt_batch_create: NULL argument");
   *out = nullptr;
-  if (max_k < 1 || max_k > LT_MAX_BEAM)
-    return fail(LT_EUNSUPPORTED, "lt_batch_create: max_k %d not in 1..%d", max_k, LT_MAX_BEAM);
+  if (max_k < 1 || max_k > LT_MAX_BEAM_ANY)
+    return fail(LT_EUNSUPPORTED, "lt_batch_create: max_k %d not in 1..%d", max_k, LT_MAX_BEAM_ANY);
   int inf_signs = 0;
   lt_status st = validate(d, &inf_signs);
   if (st != LT_OK) return st;
@@ -775,7 +780,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       node_off[q][s] = d->sent_node_off[s0 + s] - pc.node0;
       span_off[q][s] = d->sent_span_off[s0 + s] - pc.span0;
       pcum[q][s] = cum_n[s0 + s] - pc.chars0;
-      if (s < n) bp_off[q][s + 1] = bp_off[q][s] + (int64_t)(d->sent_n[s0 + s] + 1) * max_k;
+      if (s < n) bp_off[q][s + 1] = bp_off[q][s] + (int64_t)(d->sent_n[s0 + s] + 1) * max_k * bp_words(d->max_len, max_k);
     }
     pc.bp_entries = bp_off[q][n];
     b->bp_entries += pc.bp_entries;
@@ -875,9 +880,11 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
         r.f5 = d->node_f5[i];
         r.f6 = d->node_f6[i];
       }
+      // (the general kernel of max_len > 8 takes the span from the table)
       const int32_t* ss = d->span_start + d->sent_span_off[s];
-      for (int64_t x = 0; x < (int64_t)LT_MAX_SPAN * d->sent_n[s]; ++x) {
-        const uint32_t dd = (uint32_t)(LT_MAX_SPAN - (x % LT_MAX_SPAN));
+      const int SS = span_slots(d->max_len);
+      for (int64_t x = 0; x < (int64_t)SS * d->sent_n[s]; ++x) {
+        const uint32_t dd = (uint32_t)std::min<int64_t>(MAX_SPAN, SS - (x % SS));
         for (int32_t v = ss[x]; v < ss[x + 1]; ++v) recs[(size_t)(base + v)].mask |= (dd - 1u) << D_SHIFT;
       }
     }
@@ -932,7 +939,8 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   if (m->ctx != c || b->ctx != c) return fail(LT_EINVAL, "decode: handles from another context");
   if (k < 1 || k > b->max_k)
     return fail(LT_EUNSUPPORTED, "decode: beam %d not in 1..%d (batch max_k)", k, b->max_k);
-  if (beam_template_for(k) < 0) return fail(LT_EUNSUPPORTED, "decode: beam %d not compiled", k);
+  if (!decode_is_wide(b->max_len, k) && beam_template_for(k) < 0)
+    return fail(LT_EUNSUPPORTED, "decode: beam %d not compiled", k);
   if ((m->inf_signs | b->inf_signs) == 3)
     return fail(LT_EUNSUPPORTED, "decode: both +inf and -inf among the model's and the batch's score terms "
                                  "(their sum is a NaN, whose place in Python's sort is not reproduced)");
@@ -950,6 +958,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.k = k;
   p.bp_stride = b->max_k;
   p.counters = c->d_counters;
+  p.span_slots = span_slots(b->max_len);
   return LT_OK;
 }
 
@@ -991,17 +1000,59 @@ static lt_status next_slot(lt_ctx* c, lt_batch* b) {
   return LT_OK;
 }
 
+// Scratch of the general kernel for beam k over b's pieces: one block per
+// thread, threads = the largest piece's sentences, fewer when the blocks of
+// that many would pass WIDE_BUDGET (each thread then walks several
+// sentences).  Grown on demand; decodes on the ctx stream share it in order.
+constexpr size_t WIDE_BUDGET = (size_t)1 << 30;
+static lt_status wide_scratch(lt_ctx* c, const lt_batch* b, int k, DecodeParams& p) {
+  int32_t most = 0;
+  for (const lt_piece& pc : b->pieces) most = std::max(most, pc.n_sent);
+  const int64_t blk = wide_scratch_bytes(span_slots(b->max_len), k);
+  const int64_t fit = std::max<int64_t>(1, (int64_t)WIDE_BUDGET / blk);
+  const int32_t threads = (int32_t)std::max<int64_t>(1, std::min<int64_t>(most, fit));
+  const size_t need = (size_t)threads * (size_t)blk;
+  if (need > c->wide_bytes) {
+    if (c->d_wide) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      dfree(c->d_wide);
+      c->d_wide = nullptr;
+      c->wide_bytes = 0;
+    }
+    hipError_t e = hipMalloc((void**)&c->d_wide, need);
+    if (e != hipSuccess) {
+      c->d_wide = nullptr;
+      return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "decode: general-kernel scratch of %zu B: %s",
+                  need, hipGetErrorString(e));
+    }
+    c->wide_bytes = need;
+  }
+  p.wide_threads = threads;
+  p.wide_block = blk;
+  p.wide_scratch = c->d_wide;
+  return LT_OK;
+}
+
 lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
+  const bool wide = decode_is_wide(b->max_len, k);
+  if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
   if ((st = next_slot(c, b)) != LT_OK) return st;
   const int r = (int)(c->n_launch % lt_ctx::KRING);
   const size_t P = b->pieces.size();
+  const int32_t wide_threads = p.wide_threads;
   for (size_t q = 0; q < P; ++q) {           // timing: start of the first piece .. end of the last
     piece_params(b, q, k, p);
-    HIP_TRY(launch_decode(p, c->stream, false, q == 0 ? c->kev0[r] : nullptr, q + 1 == P ? c->kev1[r] : nullptr));
+    hipEvent_t e0 = q == 0 ? c->kev0[r] : nullptr, e1 = q + 1 == P ? c->kev1[r] : nullptr;
+    if (wide) {
+      p.wide_threads = std::max(1, std::min(wide_threads, p.n_sent));
+      HIP_TRY(launch_wide(p, c->stream, e0, e1));
+    } else {
+      HIP_TRY(launch_decode(p, c->stream, false, e0, e1));
+    }
   }
   b->last_end = c->kev1[r];          // other streams wait for this decode here
   b->launch_serial = c->n_serial++;
@@ -1010,7 +1061,7 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   return LT_OK;
 }
 
-const char* lt_kernel_name(int k) { return kernel_name_for(k); }
+const char* lt_kernel_name(int k) { return k > LT_MAX_BEAM_COMPILED ? "lt_beam_wide" : kernel_name_for(k); }
 
 // ------------------------------------------------------------- evaluate --
 lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, double* scores) {
@@ -1261,6 +1312,8 @@ lt_status lt_decode_trace(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_t
       (t->n_exp > 0 && (!t->exp_score || !t->exp_node || !t->exp_skip)) || t->n_exp < 0)
     return fail(LT_EINVAL, "lt_decode_trace: bad trace arrays");
   if (b->pieces.size() != 1) return fail(LT_EUNSUPPORTED, "lt_decode_trace: batch of several launch pieces");
+  if (decode_is_wide(b->max_len, k))
+    return fail(LT_EUNSUPPORTED, "lt_decode_trace: max_len > %d or beam > %d", MAX_SPAN, LT_MAX_BEAM_COMPILED);
   const int64_t S = b->n_sent;
   if (t->pos_off[0] != 0) return fail(LT_EINVAL, "lt_decode_trace: pos_off[0] != 0");
   const int64_t P = t->pos_off[S];
@@ -1321,6 +1374,9 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
+  if (decode_is_wide(b->max_len, k))
+    return fail(LT_EUNSUPPORTED, "lt_count_ops: not collected by the general kernel (max_len > %d or beam > %d)",
+                MAX_SPAN, LT_MAX_BEAM_COMPILED);
   HIP_TRY(hipSetDevice(c->device));
   if ((st = next_slot(c, b)) != LT_OK) return st;
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));

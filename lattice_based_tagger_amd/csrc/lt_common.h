@@ -37,6 +37,9 @@ constexpr uint32_t F_WI = 1u << 31;
 
 constexpr int MAX_SPAN = 8;
 constexpr int RING = MAX_SPAN + 1;     // frontier positions e-8 .. e
+// span slots per end position of a batch with this max_len: 8 (the tuned
+// kernels' layout) up to max_len 8, else max_len (the general kernel)
+LT_HD int span_slots(int max_len) { return max_len <= MAX_SPAN ? MAX_SPAN : max_len; }
 
 // -- feature hash table ----------------------------------------------------
 // Narrow slot (16 B): exact 64-bit key c3<<60 | a<<40 | b<<20 | c (c3 = the
@@ -184,5 +187,13 @@ LT_HD uint32_t bp_node(uint32_t v) { return v >> 11; }
 LT_HD uint32_t bp_d(uint32_t v) { return ((v >> 8) & 7u) + 1u; }
 LT_HD uint32_t bp_rank(uint32_t v) { return v & 255u; }
 constexpr int64_t MAX_LOCAL_NODES = (int64_t)1 << 21;     // nodes per sentence
+// General-kernel backpointer (two words): local node (21 b) | span d-1 (21 b)
+// | parent rank (22 b) -- spans and beams above the tuned kernels' 3 / 8 bits
+LT_HD uint64_t bpw_pack(uint32_t node, uint32_t d, uint32_t r) {
+  return (uint64_t)node | ((uint64_t)(d - 1u) << 21) | ((uint64_t)r << 42);
+}
+LT_HD uint32_t bpw_node(uint64_t v) { return (uint32_t)(v & 0x1FFFFFu); }
+LT_HD uint32_t bpw_d(uint64_t v) { return (uint32_t)((v >> 21) & 0x1FFFFFu) + 1u; }
+LT_HD uint32_t bpw_rank(uint64_t v) { return (uint32_t)(v >> 42); }
 
 }  // namespace lt

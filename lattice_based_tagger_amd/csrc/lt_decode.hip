@@ -1806,6 +1806,176 @@ hipError_t launch_trace(const DecodeParams& p, const TraceParams& t, hipStream_t
 }
 }  // namespace lt
 
+namespace {
+// ===========================================================================
+// General kernel (lt_beam_wide): max_len > 8 or beam_size > 256 -- what the
+// tuned kernels' layouts (8 span slots, 3-bit span and 8-bit rank fields,
+// LDS rings) do not hold.  One thread per sentence, grid-stride over the
+// piece; the beams of the last S + 1 end positions and a selection heap of k
+// items live in the thread's block of HBM scratch.  The reference loops
+// (beam.py:27-48: b ascending, hypothesis rank, candidate) run literally and
+// score with the decoders' own code.  Beam.append (beam.py:83-86, stable top
+// k by score) is a heap on the order (score desc, generation asc) whose root
+// is the worst item kept: expansions arrive in generation order, so a new one
+// displaces the root only with a strictly larger score; heap sort then puts
+// the k kept best first.  Backpointers are two words (bpw_pack).
+// ===========================================================================
+struct WItem {
+  unsigned long long key;                      // ord_key(score)
+  uint32_t g, node, d, r;                      // generation index, local node, span, parent rank
+};
+static_assert(sizeof(WItem) == WIDE_ITEM_BYTES, "wide heap item");
+static_assert(sizeof(Entry) == WIDE_ENTRY_BYTES, "wide beam entry");
+
+// a ranks after b in the stable order of Beam.append
+__device__ __forceinline__ bool ranks_after(const WItem& a, const WItem& b) {
+  return a.key < b.key || (a.key == b.key && a.g > b.g);
+}
+__device__ void wheap_down(WItem* H, int n, int i) {
+  const WItem x = H[i];
+  for (;;) {
+    int c = 2 * i + 1;
+    if (c >= n) break;
+    if (c + 1 < n && ranks_after(H[c + 1], H[c])) ++c;
+    if (!ranks_after(H[c], x)) break;
+    H[i] = H[c];
+    i = c;
+  }
+  H[i] = x;
+}
+__device__ void wheap_up(WItem* H, int i) {
+  const WItem x = H[i];
+  while (i > 0) {
+    const int par = (i - 1) >> 1;
+    if (!ranks_after(x, H[par])) break;
+    H[i] = H[par];
+    i = par;
+  }
+  H[i] = x;
+}
+
+template <bool NARROW>
+__global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
+  const int tid = (int)(blockIdx.x * 64 + threadIdx.x);
+  if (tid >= p.wide_threads) return;
+  const int S = p.span_slots, RW = S + 1, k = p.k;
+  const int64_t bstride = p.bp_stride;
+  const Bufs B = make_bufs(p);
+  const Aux aux{nullptr, 0u, p.hk};             // class 3 from the table itself
+  char* const blk = p.wide_scratch + (int64_t)tid * p.wide_block;
+  Entry* const R = reinterpret_cast<Entry*>(blk);                     // [RW][k]
+  int32_t* const cnt = reinterpret_cast<int32_t*>(blk + (int64_t)RW * k * WIDE_ENTRY_BYTES);
+  WItem* const H = reinterpret_cast<WItem*>(reinterpret_cast<char*>(cnt) + (((int64_t)RW * 4 + 15) & ~(int64_t)15));
+  Counts cn;
+  for (int i = tid; i < p.n_sent; i += p.wide_threads) {
+    const int s = p.order[i];
+    const int n = p.sent_n[s];
+    const uint32_t nbase = (uint32_t)p.node_off[s];
+    const int32_t* const ssp = p.span_start + p.span_off[s];
+    uint64_t* const bp = reinterpret_cast<uint64_t*>(p.bp + p.bp_off[s]);
+    {
+      const Cand b0 = load_cand(B, nbase);      // beam[0] = [BOS] (beam.py:21-23)
+      Entry e0;
+      e0.score = 0.0; e0.f6 = b0.f6;
+      e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
+      e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+      R[0] = e0;
+      cnt[0] = 1;
+    }
+    for (int e = 1; e <= n; ++e) {
+      const int dmax = min(e, p.max_len);
+      int hn = 0;
+      uint32_t g = 0;
+      for (int j = S - dmax; j < S; ++j) {      // span j: d = S - j, b = e - d ascending
+        const int d = S - j, b = e - d;
+        const int lo = ssp[(int64_t)(e - 1) * S + j], hi = ssp[(int64_t)(e - 1) * S + j + 1];
+        const int bs = b % RW;
+        const int nb = cnt[bs];
+        for (int r = 0; r < nb; ++r) {
+          const Hyp h = read_entry(R[(int64_t)bs * k + r]);
+          for (int node = lo; node < hi; ++node, ++g) {
+            const Cand c = load_cand(B, nbase + (uint32_t)node);
+            if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;    // beam.py:43-45
+            const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cn, aux) : 0.0;
+            const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
+            const WItem it{ord_key(sc), g, (uint32_t)node, (uint32_t)d, (uint32_t)r};
+            if (hn < k) {
+              H[hn] = it;
+              wheap_up(H, hn);
+              ++hn;
+            } else if (it.key > H[0].key) {
+              H[0] = it;
+              wheap_down(H, k, 0);
+            }
+          }
+        }
+      }
+      for (int m = hn - 1; m > 0; --m) {        // heap sort: best first
+        const WItem t = H[0];
+        H[0] = H[m];
+        H[m] = t;
+        wheap_down(H, m, 0);
+      }
+      const int es = e % RW;                    // not the slot of any b in [e - S, e - 1]
+      for (int t = 0; t < hn; ++t) {
+        const WItem it = H[t];
+        const Entry& h = R[(int64_t)((e - (int)it.d) % RW) * k + it.r];
+        const Cand c = load_cand(B, nbase + it.node);
+        Entry ne;
+        ne.score = ord_score(it.key); ne.f6 = c.f6;
+        ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
+        ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
+        ne.depth = h.depth + 1;
+        R[(int64_t)es * k + t] = ne;
+        bp[(int64_t)e * bstride + t] = bpw_pack(it.node, it.d, it.r);
+      }
+      cnt[es] = hn;
+    }
+    // matures = beam[n] + EOS (beam.py:59-61)
+    const int nm = cnt[n % RW];
+    p.out_count[s] = nm;
+    for (int t = 0; t < k; ++t) {
+      const int64_t o = (int64_t)s * k + t;
+      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
+      if (t >= nm) {                            // unused mature slots read as empty
+        p.out_score[o] = 0.0;
+        p.out_len[o] = 0;
+        for (int j = 0; j < n; ++j) codes[j] = -1;
+        continue;
+      }
+      const Entry& f = R[(int64_t)(n % RW) * k + t];
+      p.out_score[o] = f.score + 0.0;
+      p.out_len[o] = (int32_t)f.depth;
+      int pos = n;
+      uint32_t rank = (uint32_t)t;
+      for (int step = (int)f.depth - 1; step >= 0; --step) {
+        const uint64_t v = bp[(int64_t)pos * bstride + rank];
+        codes[step] = (int32_t)bpw_node(v);
+        pos -= (int)bpw_d(v);
+        rank = bpw_rank(v);
+      }
+      for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;      // padded layout
+    }
+  }
+}
+}  // namespace
+
+namespace lt {
+hipError_t launch_wide(const DecodeParams& p, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const int blocks = (p.wide_threads + 63) / 64;
+  if (p.n_sent == 0 || blocks == 0) {
+    hipError_t e = e0 ? hipEventRecord(e0, st) : hipSuccess;
+    if (e == hipSuccess && e1) e = hipEventRecord(e1, st);
+    return e;
+  }
+  if (p.narrow)
+    hipExtLaunchKernelGGL(lt_beam_wide<true>, dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
+  else
+    hipExtLaunchKernelGGL(lt_beam_wide<false>, dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
+  return hipGetLastError();
+}
+}  // namespace lt
+
 // ---------------------------------------------------------------------------
 // the flag-free copy of a feature table (lt_model.d_plain)
 // ---------------------------------------------------------------------------

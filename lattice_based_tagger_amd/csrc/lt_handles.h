@@ -35,6 +35,8 @@ struct lt_ctx {
   int64_t n_launch = 0;            // timed decode launches (KRING index)
   int64_t n_serial = 0;            // every decode-kernel launch (result slot freshness)
   unsigned long long* d_counters = nullptr;
+  char* d_wide = nullptr;          // lt_beam_wide scratch (grown on demand, decode stream only)
+  size_t wide_bytes = 0;
   std::mutex mu;                   // spare (batches are created and destroyed on several threads)
   std::vector<lt_arena> spare;     // arenas of destroyed batches, kept for reuse
 };

@@ -40,6 +40,11 @@ struct DecodeParams {
   double* out_score;
   int32_t* out_codes;
   unsigned long long* counters; // [3] expansions, feature tuples, probes
+  // general kernel (lt_beam_wide: max_len > 8 or k > LT_MAX_BEAM_COMPILED)
+  int32_t span_slots;           // span_slots(max_len)
+  int32_t wide_threads;         // threads of the launch (each owns a scratch block)
+  int64_t wide_block;           // scratch bytes per thread (wide_scratch_bytes)
+  char* wide_scratch;           // [wide_threads * wide_block]
 };
 
 // Batch evaluate (lt_evaluate): word increments, then per-path sums.
@@ -141,6 +146,19 @@ hipError_t launch_trace(const DecodeParams& p, const TraceParams& t, hipStream_t
 hipError_t launch_strip_flags(void* dst, const void* src, int64_t bytes, bool narrow, hipStream_t st);
 
 constexpr int LT_MAX_BEAM_COMPILED = 256;
+// A decode goes to the general kernel when its max_len or beam is beyond the
+// tuned kernels' (backpointers of two words, bpw_pack).
+inline bool decode_is_wide(int max_len, int k) { return max_len > MAX_SPAN || k > LT_MAX_BEAM_COMPILED; }
+// Scratch of one lt_beam_wide thread: the beams of the last S + 1 end
+// positions (48 B entries), their sizes, and the selection heap of k items.
+constexpr int WIDE_ENTRY_BYTES = 48, WIDE_ITEM_BYTES = 24;
+inline int64_t wide_scratch_bytes(int span_slots, int k) {
+  const int64_t ring = (int64_t)(span_slots + 1) * k * WIDE_ENTRY_BYTES;
+  const int64_t cnt = ((int64_t)(span_slots + 1) * 4 + 15) & ~(int64_t)15;
+  const int64_t heap = ((int64_t)k * WIDE_ITEM_BYTES + 15) & ~(int64_t)15;
+  return ring + cnt + heap;
+}
+hipError_t launch_wide(const DecodeParams& p, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 int beam_template_for(int k);
 const char* kernel_name_for(int k);
 // e0 / e1 (may be NULL): events recorded at the start / end of the kernel.

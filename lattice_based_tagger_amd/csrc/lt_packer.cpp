@@ -314,13 +314,21 @@ double lookup(std::string& kb, const ViewMap<double>& m, std::string_view t, std
 
 lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt_packed* out) {
   if (!p || !L || !out) return set_error(LT_EINVAL, "lt_packer_pack: NULL argument");
-  if (max_len < 1 || max_len > LT_MAX_SPAN)
-    return set_error(LT_EUNSUPPORTED, "lt_packer_pack: max_len %d not in 1..%d", max_len, LT_MAX_SPAN);
+  if (max_len < 1) return set_error(LT_EUNSUPPORTED, "lt_packer_pack: max_len %d < 1", max_len);
   if (L->n_sent < 0 || L->n_words < 0) return set_error(LT_EINVAL, "lt_packer_pack: negative size");
   const int32_t S = L->n_sent;
   const int64_t T = S ? L->char_off[S] : 0;
-  for (int32_t s = 0; s < S; ++s)
+  int64_t longest = 0;
+  for (int32_t s = 0; s < S; ++s) {
     if (L->char_off[s + 1] < L->char_off[s]) return set_error(LT_EINVAL, "lt_packer_pack: char offsets decrease");
+    longest = std::max<int64_t>(longest, L->char_off[s + 1] - L->char_off[s]);
+  }
+  // a span never exceeds its sentence: max_len beyond max(8, longest) decodes
+  // as that (beam.py:29-30), which keeps the span table small
+  max_len = (int)std::min<int64_t>(max_len, std::max<int64_t>(MAX_SPAN, longest));
+  if (max_len > LT_MAX_LEN_ANY)
+    return set_error(LT_EUNSUPPORTED, "lt_packer_pack: max_len %d > %d", max_len, LT_MAX_LEN_ANY);
+  const int SS = span_slots(max_len);           // span slots per end position
   for (int64_t g = 0; g < T; ++g)
     if (L->slot_off[g + 1] < L->slot_off[g] || L->slot_off[g + 1] > L->n_words)
       return set_error(LT_EINVAL, "lt_packer_pack: bad begin-slot offsets");
@@ -337,7 +345,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
   if (!o) return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
   o->pool = p->pool;
   // pass 1: nodes per sentence (threads over sentences) -> offsets
-  // (span entries: 8 n + 1 per sentence)
+  // (span entries: SS n + 1 per sentence)
   if (!o->sent_n.alloc(S) || !o->sent_node_off.alloc((int64_t)S + 1) || !o->sent_span_off.alloc((int64_t)S + 1))
     return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
   parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
@@ -349,7 +357,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
         for (int d = 1; d <= max_len && d <= e; ++d) cnt += span_count(c0 + e - d, e);
       o->sent_n[s] = n;
       o->sent_node_off[s + 1] = cnt;
-      o->sent_span_off[s + 1] = 8 * (int64_t)n + 1;
+      o->sent_span_off[s + 1] = SS * (int64_t)n + 1;
     }
   }, 256);
   o->sent_node_off[0] = 0;
@@ -444,7 +452,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       add_node(base, bos, -1);
       int32_t local = 1;
       for (int32_t e = 1; e <= n; ++e) {
-        for (int d = LT_MAX_SPAN; d >= 1; --d) {
+        for (int d = SS; d >= 1; --d) {
           *ss++ = local;
           const int32_t b = e - d;
           if (d > max_len || b < 0) continue;
@@ -470,7 +478,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
             unk.clear();
             for (int32_t x = b; x < e; ++x) utf8_append(unk, L->chars[c0 + x]);
             NodeView u{unk, unk, kUnk, {}, {}, false, false, (int64_t)d, 0};
-            add_node(base + local, u, -2 - (8 * (int64_t)b + d - 1));
+            add_node(base + local, u, -2 - (((int64_t)b << 32) | (int64_t)(d - 1)));
             ++local;
           }
         }

@@ -287,7 +287,7 @@ class NativePacker:
         N, S, nspan, npost = b.n_nodes, b.n_sent, b.n_span, b.n_post
         arr = block.view
         batch = PackedBatch(
-            max_len=int(max_len), n_post=int(npost), has_trigram=int(self.model.has_trigram),
+            max_len=int(b.max_len), n_post=int(npost), has_trigram=int(self.model.has_trigram),
             sent_n=arr(b.sent_n, C.c_int32, S, np.int32),
             sent_node_off=arr(b.sent_node_off, C.c_int64, S + 1, np.int64),
             sent_span_off=arr(b.sent_span_off, C.c_int64, S + 1, np.int64),
@@ -342,7 +342,7 @@ class _NodeView:
         if v == -1:
             return bos_word()
         code = -2 - v
-        b, d = code // 8, code % 8 + 1
+        b, d = code >> 32, (code & 0xFFFFFFFF) + 1
         sub = self.chars[b:b + d]
         return Word(sub, sub, None, Unk, None, d, b, b + d, False)
 

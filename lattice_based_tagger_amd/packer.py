@@ -11,8 +11,11 @@ layout described in DESIGN.md §Data layout:
   ``b = e-d`` in ascending order (d = max_len..1) the span's candidates in
   ``bindex[b]`` order filtered by ``w.e == e`` (`beam.py:31-33`), or the
   synthesised Unknown node when that filter is empty (`beam.py:36-38`).
-* ``span_start[(e-1)*8 + (8-d)]`` is the local index of the first node of
-  span (e-d, e); entry ``8n`` closes the sentence.
+* ``span_start[(e-1)*S + (S-d)]`` is the local index of the first node of
+  span (e-d, e); entry ``S*n`` closes the sentence.  ``S = span_slots(max_len)``:
+  8 up to max_len 8 (the tuned kernels' layout), else max_len (the general
+  kernel).  ``max_len`` is first clamped to ``max(8, longest sentence)``: a
+  span never exceeds its sentence, so the decode is unchanged (`beam.py:29-30`).
 * per node: interned ``word``/``morph0``/``tag0`` ids, the 21-bit
   mask/flag word (``lowering.py``), the node-local score terms and the
   coefficients of the node-local feature classes 4, 5 and 6.
@@ -28,7 +31,27 @@ from . import lowering as L
 from .tagset import BOS, CONTEXTUAL_TAGS, Unk
 from .word import Word, bos_word
 
-MAX_SPAN = 8            # span slots per end position in the packed layout
+MAX_SPAN = 8            # span slots per end position in the tuned kernels' layout
+MAX_LEN_ANY = 1 << 20   # LT_MAX_LEN_ANY (include/lattice_decode.h)
+
+
+def span_slots(max_len):
+    """Span slots per end position (csrc/lt_common.h span_slots)."""
+    return MAX_SPAN if max_len <= MAX_SPAN else int(max_len)
+
+
+def effective_max_len(max_len, lengths):
+    """``max_len`` clamped to ``max(8, longest sentence)`` -- the same decode
+    (a span never exceeds its sentence) with a smaller span table.  Raises
+    NotImplementedError below 1 (the caller handles those) or past
+    MAX_LEN_ANY."""
+    max_len = int(max_len)
+    if max_len < 1:
+        raise NotImplementedError('max_len < 1 is handled by the caller')
+    max_len = min(max_len, max([MAX_SPAN] + [int(n) for n in lengths]))
+    if max_len > MAX_LEN_ANY:
+        raise NotImplementedError('max_len > %d' % MAX_LEN_ANY)
+    return max_len
 
 
 class PackedBatch:
@@ -152,8 +175,9 @@ def pack(sentences, model, max_len=8):
     ``bindex`` is shorter than its character count, as the reference does
     (`beam.py:32`).
     """
-    if not 1 <= max_len <= MAX_SPAN:
-        raise NotImplementedError('max_len must be in 1..%d' % MAX_SPAN)
+    sentences = list(sentences)
+    max_len = effective_max_len(max_len, [len(chars) for _, chars in sentences])
+    S = span_slots(max_len)
     n_post = model.n_post
 
     sent_n, node_off, span_off = [], [0], [0]
@@ -186,7 +210,7 @@ def pack(sentences, model, max_len=8):
         add_node(objs[0])
         groups = [_span_candidates(bindex[b], b, n, max_len) for b in range(n)]
         for e in range(1, n + 1):
-            for d in range(MAX_SPAN, 0, -1):
+            for d in range(S, 0, -1):
                 span_start.append(len(objs))
                 b = e - d
                 if d > max_len or b < 0:

@@ -119,14 +119,15 @@ static int decode_sentence(const omodel* m, const lt_batch_desc* d, int s, int k
   ohyp bos = {0.0, 0, -1, 0, -1, -1, 0};
   H[0] = bos;
   cnt[0] = 1;
+  const int SS = d->max_len <= LT_MAX_SPAN ? LT_MAX_SPAN : d->max_len;   /* span slots per position */
   for (int e = 1; e <= n; ++e) {
     const int bmin = e - d->max_len > 0 ? e - d->max_len : 0;
     size_t ng = 0;
     int64_t gen = 0;
     for (int b = bmin; b < e; ++b) {
       const int dd = e - b;
-      const int j = LT_MAX_SPAN - dd;
-      const int32_t lo = ss[(e - 1) * LT_MAX_SPAN + j], hi = ss[(e - 1) * LT_MAX_SPAN + j + 1];
+      const int j = SS - dd;
+      const int32_t lo = ss[(int64_t)(e - 1) * SS + j], hi = ss[(int64_t)(e - 1) * SS + j + 1];
       for (int r = 0; r < cnt[b]; ++r) {
         const ohyp* h = &H[(size_t)b * k + r];
         for (int32_t x = lo; x < hi; ++x) {

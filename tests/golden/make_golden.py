@@ -89,9 +89,9 @@ def code_of(word, bindex):
     return ['U', word.b, word.e]
 
 
-def run_case(bindex, chars, funcs, max_len=8):
+def run_case(bindex, chars, funcs, max_len=8, beams=BEAMS):
     out = {}
-    for k in BEAMS:
+    for k in beams:
         try:
             matures = ref_beam_search(bindex, chars, funcs, beam_size=k, max_len=max_len)
         except Exception as exc:          # the reference's own behaviour is the vector
@@ -111,10 +111,10 @@ def run_case(bindex, chars, funcs, max_len=8):
     return out
 
 
-def case(bindex, chars, model, funcs, max_len=8, tag=''):
+def case(bindex, chars, model, funcs, max_len=8, tag='', beams=BEAMS):
     return {'chars': chars, 'bindex': [[enc_word(w) for w in ws] for ws in bindex],
             'max_len': max_len, 'model': model, 'tag': tag,
-            'expected': run_case(bindex, chars, funcs, max_len)}
+            'expected': run_case(bindex, chars, funcs, max_len, beams)}
 
 
 def dump(name, models, cases):
@@ -176,7 +176,7 @@ def make_sentences(dic, n_sent, n_eojeol, seed):
 
 
 def main():
-    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'lookup']
+    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'lookup', 'wide']
 
     if 'base' in sets:
         d = BaseMorphemeDictionary()
@@ -259,6 +259,9 @@ def main():
     if 'lookup' in sets:
         dump_lookup()
 
+    if 'wide' in sets:
+        dump_wide()
+
 
 def W(word, tag, b, e, length=None, is_l=False, morph0=None, morph1=None, tag1=None):
     return Word(word, morph0 if morph0 is not None else word, morph1, tag, tag1,
@@ -333,6 +336,58 @@ def dump_edge():
             for ml in ((8, 3) if tag in ('plain+duplicate', 'unknown_run', 'long_and_out_of_range') else (8,)):
                 cases.append(case(bindex, ch, name, funcs, max_len=ml, tag=tag))
     dump('edge', models, cases)
+
+
+def dump_wide():
+    """max_len beyond 8 (dictionary nodes of 9-16 characters, Unknown spans up
+    to max_len) and beams above 256 -- the general kernel's configurations --
+    plus max_len below 1 (no span at all, beam.py:29-31)."""
+    d = BaseMorphemeDictionary()
+    lk = MorphemeLookup(d, flatten=False)
+    sents = make_sentences(d, 10, 8, seed=23)
+    lats = []
+    for s in sents:
+        _, bindex = sentence_lookup_as_begin_index(s, lk)
+        lats.append((bindex, s.replace(' ', '')))
+    rng = random.Random(7)
+    long_lats = []
+    for bindex, ch in lats:
+        b2 = [list(ws) for ws in bindex]
+        n = len(ch)
+        for _ in range(8):                       # long dictionary nodes over the text
+            L = rng.randint(9, 16)
+            if n <= L:
+                break
+            b = rng.randrange(0, n - L + 1)
+            b2[b].append(W(ch[b:b + L], rng.choice(['Noun', 'Verb', 'Adjective']), b, b + L,
+                           is_l=rng.random() < 0.5))
+        long_lats.append((b2, ch))
+    enc, coef = trigram_from_paths(lats + long_lats, seed=3)
+    funcs = BeamScoreFunctions(RegularizationScore(), SimpleTrigramFeatureScore(enc, coef))
+    composites = {'wide_tri': funcs, 'wide_reg': BeamScoreFunctions(RegularizationScore())}
+    models = {k: [spec_of(f) for f in v.funcs] for k, v in composites.items()}
+    cases = []
+    for i, (bindex, ch) in enumerate(long_lats):
+        for ml in (9, 12, 20):
+            cases.append(case(bindex, ch, 'wide_tri', funcs, max_len=ml, tag='long_nodes',
+                              beams=(1, 5, 300) if i < 3 else (1, 5)))
+    cases.append(case(long_lats[0][0], long_lats[0][1], 'wide_tri', funcs, max_len=8, tag='long_nodes_max8',
+                      beams=(1, 300)))
+    cases.append(case(long_lats[1][0], long_lats[1][1], 'wide_tri', funcs, max_len=1000, tag='max_len_past_n',
+                      beams=(1, 5)))
+    for name in composites:
+        cases.append(case([[]] * 20, 'ㅋ' * 20, name, composites[name], max_len=12, tag='all_unknown_20',
+                          beams=(1, 5, 300)))
+    cases.append(case([[W('아이', 'Noun', 0, 2, is_l=True)]] + [[]] * 13, '아이ㅋㅋㅋㅋㅋㅋㅋㅋㅋㅋㅋㅋ', 'wide_reg',
+                      composites['wide_reg'], max_len=10, tag='unknown_run', beams=(1, 5, 300)))
+    cases.append(case([], '', 'wide_tri', funcs, max_len=12, tag='empty_sentence', beams=(1, 300)))
+    cases.append(case([], 'ㅋㅋㅋ', 'wide_tri', funcs, max_len=12, tag='no_dictionary_hit', beams=(1, 300)))
+    for ml in (0, -1):                           # no span: beam[e] = [] (bindex never read)
+        cases.append(case(long_lats[2][0], long_lats[2][1], 'wide_tri', funcs, max_len=ml, tag='max_len<1',
+                          beams=(1, 5)))
+        cases.append(case([], 'ㅋㅋㅋ', 'wide_tri', funcs, max_len=ml, tag='max_len<1', beams=(1,)))
+        cases.append(case([], '', 'wide_tri', funcs, max_len=ml, tag='max_len<1', beams=(1,)))
+    dump('wide', models, cases)
 
 
 def dump_dense():

@@ -12,7 +12,7 @@ from lattice_based_tagger_amd import (BeamScoreFunctions, RegularizationScore,
                                       SimpleTrigramFeatureScore, SimpleTrigramEncoder, Word)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
-SETS = ('base', 'demo', 'synth', 'scorers', 'edge', 'dense')
+SETS = ('base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'wide')
 
 
 def _tup(x):
@@ -55,11 +55,20 @@ class Case:
         return self.bindex[code[0]][code[1]]
 
 
-def load(name):
+def load(name, packable=False):
+    """The cases of set ``name``; ``packable``: only those a packed batch can
+    hold (max_len >= 1 -- below that beam_search decodes nothing and packs
+    nothing, beam.py:29-31)."""
     with gzip.open(os.path.join(GOLDEN, name + '.json.gz'), 'rt', encoding='utf-8') as f:
         data = json.load(f)
     models = {k: build_funcs(v) for k, v in data['models'].items()}
-    return [Case(c, models[c['model']]) for c in data['cases']]
+    cases = [Case(c, models[c['model']]) for c in data['cases']]
+    return [c for c in cases if c.max_len >= 1] if packable else cases
+
+
+def beams_of(cases):
+    """Beam sizes the reference was run with in any of ``cases``."""
+    return sorted({int(k) for c in cases for k in c.expected})
 
 
 def path_matches(case, codes, path_words):

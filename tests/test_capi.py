@@ -66,7 +66,7 @@ def test_kernel_name_without_gpu():
     assert lib.lt_kernel_name(32) == b'lt_beam_pk'
     assert lib.lt_kernel_name(33) == b'lt_beam_pk'
     assert lib.lt_kernel_name(256) == b'lt_beam_pk'
-    assert lib.lt_kernel_name(257) is None
+    assert lib.lt_kernel_name(257) == b'lt_beam_wide'      # the general kernel (also max_len > 8)
     assert lib.lt_kernel_name(0) is None or lib.lt_kernel_name(0) == b'lt_viterbi_pk'
 
 

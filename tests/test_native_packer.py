@@ -46,7 +46,7 @@ def _check(sentences, funcs, max_len):
 @pytest.mark.parametrize('name', SETS)
 def test_native_matches_python_on_golden(name):
     groups = {}
-    for c in load(name):
+    for c in load(name, packable=True):
         groups.setdefault((id(c.funcs), c.max_len), []).append(c)
     for group in groups.values():
         ok = [c for c in group if len(c.bindex) >= len(c.chars)]
