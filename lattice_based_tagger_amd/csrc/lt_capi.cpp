@@ -945,7 +945,9 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
     return fail(LT_EUNSUPPORTED, "decode: both +inf and -inf among the model's and the batch's score terms "
                                  "(their sum is a NaN, whose place in Python's sort is not reproduced)");
   p = DecodeParams{};
-  p.table = k == 1 ? m->d_table : m->d_plain;     // beam 1 probes primary first (flags)
+  // beam 1 and the general kernel probe primary first (flags); the tuned beam
+  // kernels load both slots of the flag-free copy
+  p.table = (k == 1 || decode_is_wide(b->max_len, k)) ? m->d_table : m->d_plain;
   p.slots = (uint32_t)m->slots;
   p.seed = m->seed;
   p.hk = narrow_hash(m->seed);
