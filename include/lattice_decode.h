@@ -254,6 +254,9 @@ typedef struct {
   double* exp_score;        /* [n_exp]: score of the grown sequence (0 if skipped) */
   uint32_t* exp_node;       /* [n_exp]: local node << 11 | (span - 1) << 8 | parent rank */
   uint8_t* exp_skip;        /* [n_exp]: 1 = skipped (unknown after unknown, beam.py:43-45) */
+  uint64_t* exp_link;       /* [n_exp] or NULL: local node | (span - 1) << 21 | parent rank << 42
+                               -- required past max_len 8 / beam 256, where exp_node holds the
+                               local node only */
 } lt_trace;
 lt_status lt_decode_trace(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k, lt_trace* trace);
 

@@ -334,7 +334,8 @@ class DeviceModel:
 class TraceDesc(C.Structure):
     _fields_ = [('pos_off', C.c_void_p), ('exp_off', C.c_void_p), ('n_exp', C.c_int64),
                 ('beam_count', C.c_void_p), ('beam_gen', C.c_void_p), ('exp_count', C.c_void_p),
-                ('exp_score', C.c_void_p), ('exp_node', C.c_void_p), ('exp_skip', C.c_void_p)]
+                ('exp_score', C.c_void_p), ('exp_node', C.c_void_p), ('exp_skip', C.c_void_p),
+                ('exp_link', C.c_void_p)]
 
 
 class DeviceBatch:
@@ -367,6 +368,7 @@ class DeviceBatch:
         self.handle = h
         self.ctx = ctx
         self.max_k = int(max_k)
+        self.max_len = int(packed.max_len)
 
     @property
     def pieces(self):
@@ -418,7 +420,8 @@ class DeviceBatch:
         """Every expansion of every end position (lt_decode_trace), as a dict
         of arrays: pos_off (positions of sentence s: pos_off[s] + e),
         exp_off, beam_count, beam_gen [positions, k], exp_count, exp_score,
-        exp_node (bp words), exp_skip."""
+        exp_node, exp_skip, exp_link (per expansion: node | span-1 << 21 |
+        parent rank << 42, csrc/lt_common.h bpw_pack)."""
         n = self.sent_n.astype(np.int64)
         pos_off = np.zeros(self.n_sent + 1, dtype=np.int64)
         np.cumsum(n + 1, out=pos_off[1:])
@@ -426,22 +429,24 @@ class DeviceBatch:
         # slots of position e of sentence s: k x (candidates ending at e)
         span = np.ascontiguousarray(self._span_start, dtype=np.int64)
         span_off = self._span_off
+        S = 8 if self.max_len <= 8 else int(self.max_len)          # span slots per position
         bound = np.zeros(P, dtype=np.int64)
         for s in range(self.n_sent):
             ns = int(n[s])
             if ns:
-                a = span[span_off[s]:span_off[s] + 8 * ns + 1]
-                bound[pos_off[s] + 1:pos_off[s] + 1 + ns] = (a[8::8] - a[0:-1:8]) * int(k)
+                a = span[span_off[s]:span_off[s] + S * ns + 1]
+                bound[pos_off[s] + 1:pos_off[s] + 1 + ns] = (a[S::S] - a[0:-1:S]) * int(k)
         exp_off = np.zeros(P + 1, dtype=np.int64)
         np.cumsum(bound, out=exp_off[1:])
         n_exp = int(exp_off[-1])
         out = {'pos_off': pos_off, 'exp_off': exp_off,
                'beam_count': np.zeros(P, dtype=np.int32), 'beam_gen': np.zeros((P, int(k)), dtype=np.uint32),
                'exp_count': np.zeros(P, dtype=np.int32), 'exp_score': np.zeros(max(n_exp, 1), dtype=np.float64),
-               'exp_node': np.zeros(max(n_exp, 1), dtype=np.uint32), 'exp_skip': np.zeros(max(n_exp, 1), dtype=np.uint8)}
+               'exp_node': np.zeros(max(n_exp, 1), dtype=np.uint32), 'exp_skip': np.zeros(max(n_exp, 1), dtype=np.uint8),
+               'exp_link': np.zeros(max(n_exp, 1), dtype=np.uint64)}
         desc = TraceDesc(*[_ptr(out[f]) for f in ('pos_off', 'exp_off')], n_exp,
                          *[_ptr(out[f]) for f in ('beam_count', 'beam_gen', 'exp_count', 'exp_score',
-                                                 'exp_node', 'exp_skip')])
+                                                 'exp_node', 'exp_skip', 'exp_link')])
         check(self.ctx._lib.lt_decode_trace(self.ctx.handle, model.handle, self.handle, int(k), C.byref(desc)))
         return out
 

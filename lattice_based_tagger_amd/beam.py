@@ -539,6 +539,10 @@ def debug_dump(bindex, chars, score_functions, beam_size=5, max_len=8, device=0,
     out = file or sys.stdout
     k = _check_beam(beam_size)
     model = lowered_model(score_functions)
+    if int(max_len) < 1:                 # no span at any end position (beam.py:29-31)
+        for e in range(1, len(chars) + 1):
+            print('\n{}\nEnd point = {}, len(growns) = {}\n'.format('-' * 40, e, 0), file=out)
+        return
     packed, objs = pack([(bindex, chars)], model, max_len)      # the Word objects, not views
     if len(chars) == 0:
         return
@@ -557,14 +561,14 @@ def debug_dump(bindex, chars, score_functions, beam_size=5, max_len=8, device=0,
     n = len(chars)
     paths = {(0, 0): (nodes[0],)}
     off = tr['exp_off']
-    node_of = lambda v: v >> 11                     # noqa: E731  (csrc/lt_common.h bp_pack)
-    span_of = lambda v: ((v >> 8) & 7) + 1           # noqa: E731
-    rank_of = lambda v: v & 255                      # noqa: E731
+    node_of = lambda v: v & 0x1FFFFF                # noqa: E731  (csrc/lt_common.h bpw_pack)
+    span_of = lambda v: ((v >> 21) & 0x1FFFFF) + 1   # noqa: E731
+    rank_of = lambda v: v >> 42                      # noqa: E731
 
     def path(pos, rank):
         got = paths.get((pos, rank))
         if got is None:
-            v = int(tr['exp_node'][off[pos] + tr['beam_gen'][pos, rank]])
+            v = int(tr['exp_link'][off[pos] + tr['beam_gen'][pos, rank]])
             got = path(pos - span_of(v), rank_of(v)) + (nodes[node_of(v)],)
             paths[(pos, rank)] = got
         return got
@@ -572,11 +576,11 @@ def debug_dump(bindex, chars, score_functions, beam_size=5, max_len=8, device=0,
     for e in range(1, n + 1):
         a, m = int(off[e]), int(tr['exp_count'][e])
         growns = [g for g in range(m) if not tr['exp_skip'][a + g]
-                  and (k > 0 or span_of(int(tr['exp_node'][a + g])) == e)]
+                  and (k > 0 or span_of(int(tr['exp_link'][a + g])) == e)]
         print('\n{}\nEnd point = {}, len(growns) = {}\n'.format('-' * 40, e, len(growns)), file=out)
         sc = tr['exp_score']
         for g in sorted(growns, key=lambda g: -sc[a + g]):      # stable: generation order on ties
-            v = int(tr['exp_node'][a + g])
+            v = int(tr['exp_link'][a + g])
             words = list(path(e - span_of(v), rank_of(v)) + (nodes[node_of(v)],))
             kind = path_score_type(model, words)
             num_unk = 0

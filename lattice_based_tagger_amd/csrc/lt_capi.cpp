@@ -1314,8 +1314,9 @@ lt_status lt_decode_trace(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_t
       (t->n_exp > 0 && (!t->exp_score || !t->exp_node || !t->exp_skip)) || t->n_exp < 0)
     return fail(LT_EINVAL, "lt_decode_trace: bad trace arrays");
   if (b->pieces.size() != 1) return fail(LT_EUNSUPPORTED, "lt_decode_trace: batch of several launch pieces");
-  if (decode_is_wide(b->max_len, k))
-    return fail(LT_EUNSUPPORTED, "lt_decode_trace: max_len > %d or beam > %d", MAX_SPAN, LT_MAX_BEAM_COMPILED);
+  if (decode_is_wide(b->max_len, k) && t->n_exp > 0 && !t->exp_link)
+    return fail(LT_EINVAL, "lt_decode_trace: exp_link is required past max_len %d / beam %d", MAX_SPAN,
+                LT_MAX_BEAM_COMPILED);
   const int64_t S = b->n_sent;
   if (t->pos_off[0] != 0) return fail(LT_EINVAL, "lt_decode_trace: pos_off[0] != 0");
   const int64_t P = t->pos_off[S];
@@ -1337,6 +1338,7 @@ lt_status lt_decode_trace(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_t
   uint32_t *d_bg = nullptr, *d_node = nullptr;
   double* d_score = nullptr;
   uint8_t* d_skip = nullptr;
+  uint64_t* d_link = nullptr;
   const size_t ne = (size_t)std::max<int64_t>(t->n_exp, 1);
   hipError_t e = dalloc_copy(&d_pos, t->pos_off, (size_t)S + 1, c->stream);
   if (e == hipSuccess) e = dalloc_copy(&d_exp, t->exp_off, (size_t)P + 1, c->stream);
@@ -1347,10 +1349,11 @@ lt_status lt_decode_trace(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_t
   if (e == hipSuccess) e = hipMalloc((void**)&d_node, ne * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&d_score, ne * 8);
   if (e == hipSuccess) e = hipMalloc((void**)&d_skip, ne);
+  if (e == hipSuccess && t->exp_link) e = hipMalloc((void**)&d_link, ne * 8);
   if (e == hipSuccess) {
     tp.pos_off = d_pos; tp.exp_off = d_exp; tp.ent = d_ent;
     tp.beam_count = d_bc; tp.beam_gen = d_bg; tp.exp_count = d_ec;
-    tp.exp_score = d_score; tp.exp_node = d_node; tp.exp_skip = d_skip;
+    tp.exp_score = d_score; tp.exp_node = d_node; tp.exp_skip = d_skip; tp.exp_link = d_link;
     e = launch_trace(p, tp, c->stream);
   }
   if (e == hipSuccess) e = hipMemcpyAsync(t->beam_count, d_bc, (size_t)P * 4, hipMemcpyDeviceToHost, c->stream);
@@ -1360,10 +1363,12 @@ lt_status lt_decode_trace(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_t
     e = hipMemcpyAsync(t->exp_score, d_score, (size_t)t->n_exp * 8, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(t->exp_node, d_node, (size_t)t->n_exp * 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(t->exp_skip, d_skip, (size_t)t->n_exp, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && d_link)
+      e = hipMemcpyAsync(t->exp_link, d_link, (size_t)t->n_exp * 8, hipMemcpyDeviceToHost, c->stream);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   dfree(d_pos); dfree(d_exp); dfree(d_ent); dfree(d_bc); dfree(d_ec); dfree(d_bg);
-  dfree(d_node); dfree(d_score); dfree(d_skip);
+  dfree(d_node); dfree(d_score); dfree(d_skip); dfree(d_link);
   if (e != hipSuccess) return fail(LT_EHIP, "lt_decode_trace: %s", hipGetErrorString(e));
   for (int64_t q = 0; q < P; ++q)
     if (t->exp_count[q] < 0) return fail(LT_EINVAL, "lt_decode_trace: position %lld has more expansions than slots",

@@ -1712,7 +1712,8 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
   if (s >= p.n_sent) return;
   const Bufs B = make_bufs(p);
   const Aux aux{nullptr, 0u, p.hk};             // class 3 from the table itself
-  const int k = p.k;
+  const int k = p.k, S = p.span_slots;
+  const bool wide = decode_is_wide(p.max_len, k);
   const int n = p.sent_n[s];
   const uint32_t nbase = (uint32_t)p.node_off[s];
   const int32_t* ssp = p.span_start + p.span_off[s];
@@ -1734,11 +1735,10 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
     const int dmax = min(e, p.max_len);
     const int64_t xo = t.exp_off[po + e], xe = t.exp_off[po + e + 1];
     uint32_t g = 0;
-    for (int j = 0; j < MAX_SPAN; ++j) {        // span j: length d = 8 - j, begin b = e - d
-      const int d = MAX_SPAN - j;
-      if (d > dmax) continue;
+    for (int j = S - dmax; j < S; ++j) {        // span j: length d = S - j, begin b = e - d
+      const int d = S - j;
       const int b = e - d;
-      const int lo = ssp[(e - 1) * MAX_SPAN + j], hi = ssp[(e - 1) * MAX_SPAN + j + 1];
+      const int lo = ssp[(int64_t)(e - 1) * S + j], hi = ssp[(int64_t)(e - 1) * S + j + 1];
       const int nb = t.beam_count[po + b];
       for (int r = 0; r < nb; ++r) {
         const Hyp h = read_entry(ent[(int64_t)b * k + r]);
@@ -1755,7 +1755,8 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
             sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);      // beam.py:115
           }
           t.exp_score[xo + g] = sc;
-          t.exp_node[xo + g] = bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+          t.exp_node[xo + g] = wide ? (uint32_t)node : bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+          if (t.exp_link) t.exp_link[xo + g] = bpw_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
           t.exp_skip[xo + g] = skip ? 1 : 0;
         }
       }
@@ -1779,8 +1780,11 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
       if (bg == INV) break;
       first = false;
       pk = bk; pg = bg;
-      const uint32_t v = t.exp_node[xo + bg];
-      const int d = (int)bp_d(v), r = (int)bp_rank(v), node = (int)bp_node(v);
+      const uint64_t v = t.exp_link ? t.exp_link[xo + bg] : 0ull;
+      const uint32_t v32 = t.exp_node[xo + bg];
+      const int d = t.exp_link ? (int)bpw_d(v) : (int)bp_d(v32);
+      const int r = t.exp_link ? (int)bpw_rank(v) : (int)bp_rank(v32);
+      const int node = t.exp_link ? (int)bpw_node(v) : (int)bp_node(v32);
       const Entry& h = ent[(int64_t)(e - d) * k + r];
       const Cand c = load_cand(B, nbase + (uint32_t)node);
       Entry ne;

@@ -138,6 +138,7 @@ struct TraceParams {
   double* exp_score;            // [expansion slots]
   uint32_t* exp_node;           // [expansion slots]: bp_pack(node, span, parent rank)
   uint8_t* exp_skip;            // [expansion slots]: 1 = skipped (beam.py:43-45)
+  uint64_t* exp_link;           // [expansion slots] or NULL: bpw_pack(node, span, parent rank)
 };
 hipError_t launch_trace(const DecodeParams& p, const TraceParams& t, hipStream_t st);
 
@@ -148,7 +149,7 @@ hipError_t launch_strip_flags(void* dst, const void* src, int64_t bytes, bool na
 constexpr int LT_MAX_BEAM_COMPILED = 256;
 // A decode goes to the general kernel when its max_len or beam is beyond the
 // tuned kernels' (backpointers of two words, bpw_pack).
-inline bool decode_is_wide(int max_len, int k) { return max_len > MAX_SPAN || k > LT_MAX_BEAM_COMPILED; }
+__host__ __device__ inline bool decode_is_wide(int max_len, int k) { return max_len > MAX_SPAN || k > LT_MAX_BEAM_COMPILED; }
 // Scratch of one lt_beam_wide thread: the beams of the last S + 1 end
 // positions (48 B entries), their sizes, and the selection heap of k items.
 constexpr int WIDE_ENTRY_BYTES = 48, WIDE_ITEM_BYTES = 24;

@@ -36,7 +36,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 # (set, max chars, how many cases, beams): short sentences keep the dump small
 PICK = [('demo', 14, 4, (1, 3)), ('edge', 12, 14, (1, 2)), ('scorers', 30, 3, (1, 4)),
-        ('synth', 40, 2, (1, 5)), ('dense', 30, 2, (2,))]
+        ('synth', 40, 2, (1, 5)), ('dense', 30, 2, (2,)),
+        # the general kernel's configurations: beams above 256, max_len > 8 and < 1
+        ('wide', 20, 11, (1, 300)), ('wide', 33, 3, (2,))]
 
 
 def ref_funcs(specs):
