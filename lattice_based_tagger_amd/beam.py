@@ -25,6 +25,11 @@ from .packer import pack
 from .tagset import Unk
 from .word import Word, bos_word, eos_word
 
+from functools import partial
+from itertools import repeat
+
+_new_word = partial(tuple.__new__, Word)      # Word from a 9-tuple, one C call
+
 __all__ = ['beam_search', 'beam_search_batch', 'Beam', 'Sequence', 'Decoder']
 
 
@@ -452,21 +457,24 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
     glob = packed.sent_node_off[seg // T] + local
     src = objs[0].src[glob]
     lat = objs[0].words
-    flat = [None] * total
+    flat = np.empty(total, dtype=object)              # filled by two bulk assignments
     dic = np.flatnonzero(src >= 0)
     sel = src[dic]
     # native lattices build their Words in bulk; Word lists hand back the
     # caller's own objects (as the reference's paths hold them)
     words = lat.words_bulk(sel) if hasattr(lat, 'words_bulk') else [lat[i] for i in sel.tolist()]
-    for j, w in zip(dic.tolist(), words):
-        flat[j] = w
+    if dic.size:                                       # (fromiter: Words are tuples, kept whole)
+        flat[dic] = np.fromiter(words, dtype=object, count=dic.size)
     unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
     if unk.size:
         code = -2 - src[unk]
-        for j, b, d, s in zip(unk.tolist(), (code >> 32).tolist(), ((code & 0xFFFFFFFF) + 1).tolist(),
-                              (seg[unk] // T).tolist()):
-            sub = chars_list[s][b:b + d]
-            flat[j] = Word(sub, sub, None, Unk, None, d, b, b + d, False)
+        bl = (code >> 32).tolist()
+        dl = ((code & 0xFFFFFFFF) + 1).tolist()
+        subs = [chars_list[s][b:b + d] for b, d, s in zip(bl, dl, (seg[unk] // T).tolist())]
+        flat[unk] = np.fromiter(map(_new_word, zip(subs, subs, repeat(None), repeat(Unk), repeat(None), dl, bl,
+                                                   [b + d for b, d in zip(bl, dl)], repeat(False))),
+                                dtype=object, count=unk.size)
+    flat = flat.tolist()
     # the sentinels are immutable tuples: one BOS, one EOS per sentence length
     bos, eos = bos_word(), {}
     vals = _typed_scores(model, packed, glob, seg, Lf, first, score[:, :T], n, T, bos, flat)

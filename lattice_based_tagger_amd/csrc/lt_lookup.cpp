@@ -883,13 +883,14 @@ lt_status lt_lattices_strings_coded(const lt_lattices* L, int field, const int64
   const uint8_t* null = field == 2 ? L->m1null.data() : field == 4 ? L->t1null.data() : nullptr;
   const char* blob = blobs[field]->data();
   const int64_t* off = offs[field]->data();
-  // open addressing over (hash, code); the distinct strings in `uniq`
+  // open addressing over (hash, code); the distinct strings in `uniq`.  The
+  // table grows with the distinct strings (load <= 1/2), not with n: paths
+  // repeat few strings, and a small table stays in cache.
   struct Slot {
     uint64_t h;                                    // 0: empty
     int32_t code;
   };
-  size_t tn = 64;
-  while (tn < (size_t)n * 2) tn <<= 1;
+  size_t tn = 1024;
   std::vector<Slot> tab;
   std::vector<std::string_view> uniq;
   try {
@@ -897,7 +898,20 @@ lt_status lt_lattices_strings_coded(const lt_lattices* L, int field, const int64
   } catch (...) {
     return lt::set_error(LT_ENOMEM, "lt_lattices_strings_coded: out of memory");
   }
-  const uint64_t mask = tn - 1;
+  uint64_t mask = tn - 1;
+  auto grow = [&]() {
+    std::vector<Slot> t2(tn * 2, Slot{0, 0});
+    const uint64_t m2 = tn * 2 - 1;
+    for (const Slot& x : tab)
+      if (x.h) {
+        uint64_t j = x.h & m2;
+        while (t2[j].h) j = (j + 1) & m2;
+        t2[j] = x;
+      }
+    tab.swap(t2);
+    tn *= 2;
+    mask = m2;
+  };
   int64_t need = 0;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t v = idx[i];
@@ -920,11 +934,21 @@ lt_status lt_lattices_strings_coded(const lt_lattices* L, int field, const int64
         tab[j] = Slot{h, (int32_t)uniq.size()};
         uniq.push_back(sv);
         need += (int64_t)sv.size() + 1;
+        if (uniq.size() * 2 > tn) {
+          try {
+            grow();
+          } catch (...) {
+            return lt::set_error(LT_ENOMEM, "lt_lattices_strings_coded: out of memory");
+          }
+          codes[i] = (int32_t)uniq.size() - 1;
+          goto next;
+        }
         break;
       }
       if (tab[j].h == h && uniq[(size_t)tab[j].code] == sv) break;
     }
     codes[i] = tab[j].code;
+  next:;
   }
   if (used) *used = need;
   if (n_unique) *n_unique = (int64_t)uniq.size();

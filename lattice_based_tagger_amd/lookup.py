@@ -385,12 +385,20 @@ class NativeLattices:
         fields = []
         codes = np.empty(idx.size, dtype=np.int32)
         lib = self.lib.held
-        cap = max(int(lib.lt_lattices_field_bytes(self.handle, f)) for f in range(5)) + idx.size
-        buf = C.create_string_buffer(cap)                       # one for the five fields
+        # one buffer for the five fields' distinct strings (paths repeat few
+        # of them); a field that needs more is coded again into a larger one
+        full = max(int(lib.lt_lattices_field_bytes(self.handle, f)) for f in range(5)) + idx.size
+        cap = min(full, 1 << 20)
+        buf = C.create_string_buffer(cap)
         used, n_u = C.c_int64(), C.c_int64()
         for f, name in enumerate(('word', 'morph0', 'morph1', 'tag0', 'tag1')):
             st = lib.lt_lattices_strings_coded(self.handle, f, idx.ctypes.data, idx.size,
                                                codes.ctypes.data, buf, cap, C.byref(used), C.byref(n_u))
+            if st == -1 and used.value > cap:                   # LT_EINVAL: too small
+                cap = int(used.value)
+                buf = C.create_string_buffer(cap)
+                st = lib.lt_lattices_strings_coded(self.handle, f, idx.ctypes.data, idx.size,
+                                                   codes.ctypes.data, buf, cap, C.byref(used), C.byref(n_u))
             if st == _capi.LT_EUNSUPPORTED:                     # a NUL inside a string: slice each
                 (blob, off), null = self._columns()[name]
                 vals = [blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()]
