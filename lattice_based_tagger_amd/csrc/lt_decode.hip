@@ -497,7 +497,10 @@ __device__ __forceinline__ Hyp read_hyp(const VEntry& e) {
 #ifndef PK_BPL
 #define PK_BPL 64
 #endif
-constexpr int P_WPB = 4;                // waves per block
+#ifndef PK_WPB
+#define PK_WPB 4
+#endif
+constexpr int P_WPB = PK_WPB;           // waves per block
 
 // Stage the records of the wave's packed candidates (lane l's node gn, INV =
 // none) into wave_planes: the 3 x 64 chunks of 16 B form one stream in lane
@@ -537,7 +540,7 @@ struct alignas(16) SentRec {
 };
 
 template <int W, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(256, (NARROW && W <= 6) ? PK_WAVES : 3)
+__global__ void __launch_bounds__(64 * P_WPB, (NARROW && W <= 6) ? PK_WAVES : 3)
 lt_viterbi_pk(DecodeParams p) {
   constexpr int BPL = PK_BPL;                   // end positions whose backpointer stays in LDS
   __shared__ VEntry ring[P_WPB][W][RING];
@@ -787,7 +790,7 @@ hipError_t launch_pk(const DecodeParams& p, const Launch& L) {
   constexpr int SPB = W * P_WPB;
   const int blocks = (p.n_sent + SPB - 1) / SPB;
   if (blocks == 0) return hipSuccess;
-  hipExtLaunchKernelGGL((lt_viterbi_pk<W, NARROW, COUNT>), dim3(blocks), dim3(256), 0, L.st, L.e0, L.e1, 0, p);
+  hipExtLaunchKernelGGL((lt_viterbi_pk<W, NARROW, COUNT>), dim3(blocks), dim3(64 * P_WPB), 0, L.st, L.e0, L.e1, 0, p);
   return hipGetLastError();
 }
 
