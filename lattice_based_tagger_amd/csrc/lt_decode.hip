@@ -1018,18 +1018,23 @@ lt_beam_pk(DecodeParams p) {
 #pragma unroll
         for (int t = 0; t < RPC; ++t)
           if (t < R0) mx = myk[t] > mx ? myk[t] : mx;
-        unsigned long long* const MX = LK + KTP;                 // chunk entries are in registers now
-        MX[lane] = mx;
+        // tau from the maxima's high 32 bits (a nonzero key's are nonzero):
+        // the k-th largest h_k of them, tau = h_k << 32, still has at least k
+        // entries >= it, at half the compare work of 64-bit keys
+        uint32_t* const MX = reinterpret_cast<uint32_t*>(LK + KTP);   // chunk entries are in registers now
+        const uint32_t mh = (uint32_t)(mx >> 32);
+        MX[lane] = mh;
         if (lane == 0) tkey[wv][0] = ~0ull;
         int gtc = 0;
 #pragma unroll 4
-        for (int q = 0; q < 64; q += 2) {
-          const ulonglong2 m2 = *reinterpret_cast<const ulonglong2*>(&MX[q]);
-          gtc += (m2.x > mx ? 1 : 0) + (m2.y > mx ? 1 : 0);
+        for (int q = 0; q < 64; q += 4) {
+          const uint4 m4 = *reinterpret_cast<const uint4*>(&MX[q]);
+          gtc += (m4.x > mh ? 1 : 0) + (m4.y > mh ? 1 : 0) + (m4.z > mh ? 1 : 0) + (m4.w > mh ? 1 : 0);
         }
         const int nz = __builtin_popcountll(__ballot(mx != 0ull));
         if (mx != 0ull && gtc < k)
-          __hip_atomic_fetch_min(&tkey[wv][0], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_min(&tkey[wv][0], (unsigned long long)mh << 32, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned long long tau = nz >= k ? tkey[wv][0] : 1ull;
         // compact the entries >= tau to the list head (in lane order per slot)
         int nc = 0;
@@ -1407,18 +1412,21 @@ lt_beam_hw(DecodeParams p) {
         unsigned long long mx = rk;
 #pragma unroll
         for (int t = 0; t < RPC; ++t) mx = myk[t] > mx ? myk[t] : mx;
-        unsigned long long* const MX = LK + KTP;                 // chunk entries are in registers now
-        MX[hl] = mx;
+        // (tau from the maxima's high 32 bits, as lt_beam_pk)
+        uint32_t* const MX = reinterpret_cast<uint32_t*>(LK + KTP);   // chunk entries are in registers now
+        const uint32_t mh = (uint32_t)(mx >> 32);
+        MX[hl] = mh;
         if (hl == 0) TK[0] = ~0ull;
         int gtc = 0;
 #pragma unroll 4
-        for (int q = 0; q < G; q += 2) {
-          const ulonglong2 m2 = *reinterpret_cast<const ulonglong2*>(&MX[q]);
-          gtc += (m2.x > mx ? 1 : 0) + (m2.y > mx ? 1 : 0);
+        for (int q = 0; q < G; q += 4) {
+          const uint4 m4 = *reinterpret_cast<const uint4*>(&MX[q]);
+          gtc += (m4.x > mh ? 1 : 0) + (m4.y > mh ? 1 : 0) + (m4.z > mh ? 1 : 0) + (m4.w > mh ? 1 : 0);
         }
         const int nz = hcount(__ballot(mx != 0ull));
         if (mx != 0ull && gtc < k)
-          __hip_atomic_fetch_min(&TK[0], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_min(&TK[0], (unsigned long long)mh << 32, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned long long tau = nz >= k ? TK[0] : 1ull;
         int nc = 0;
         auto push = [&](unsigned long long key, uint32_t g) {
