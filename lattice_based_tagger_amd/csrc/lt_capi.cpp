@@ -817,6 +817,13 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   const size_t h_slab = cv.host(b->slab_cap);
   const size_t h_count = cv.host((size_t)S * 4), h_len = cv.host(nres * 4), h_score = cv.host(nres * 8),
                h_codes = cv.host(ncodes * 4);
+  // node records staged in the arena's pinned memory when the arena is kept
+  // for reuse (a pipeline's chunks): the upload is then a DMA from pinned
+  // memory, no runtime staging copy on the host, and no fresh pages to fault
+  // in per batch.  A larger batch stages them in pageable memory (pinning
+  // gigabytes once costs more than the copy).
+  const bool pin_recs = cv.d <= SPARE_MAX && d->n_nodes > 0;
+  const size_t h_recs = pin_recs ? cv.host((size_t)d->n_nodes * sizeof(NodeRec)) : SIZE_MAX;
   hipError_t e = arena_take(c, cv.d, cv.h, b->arena);
   if (e != hipSuccess) {
     delete b;
@@ -859,7 +866,9 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   up(b->d_sent_n, d->sent_n, (size_t)S);
   up(b->d_cum_n, cum_n.data(), (size_t)S + 1);
   // device node records: AoS, mask + each node's span length d-1 (bits 24-26)
-  std::unique_ptr<NodeRec[]> recs(new (std::nothrow) NodeRec[(size_t)std::max<int64_t>(d->n_nodes, 1)]);
+  std::unique_ptr<NodeRec[]> heap_recs(pin_recs ? nullptr
+                                               : new (std::nothrow) NodeRec[(size_t)std::max<int64_t>(d->n_nodes, 1)]);
+  NodeRec* const recs = pin_recs ? at<NodeRec>(H, h_recs) : heap_recs.get();
   if (!recs) {
     batch_free(b);
     return fail(LT_ENOMEM, "lt_batch_create: out of host memory");
@@ -899,7 +908,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     up(pc.d_bp_off, bp_off[q].data(), n + 1);
     up(pc.d_cum_n, pcum[q].data(), n + 1);
     up(pc.d_span_start, d->span_start + pc.span0, (size_t)pc.n_span);
-    up(pc.d_nodes, recs.get() + pc.node0, (size_t)pc.n_nodes);
+    up(pc.d_nodes, recs + pc.node0, (size_t)pc.n_nodes);
     for (int32_t t = 0; t < d->n_post; ++t)
       up(pc.d_post + (size_t)t * pc.n_nodes, d->node_post + (size_t)t * d->n_nodes + pc.node0, (size_t)pc.n_nodes);
   }
