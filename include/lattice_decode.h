@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 2   /* 2: compact results (slabs), gathers of slabs */
+#define LT_ABI_VERSION 3   /* 2: compact results (slabs), gathers of slabs;
+                              3: any max_len / beam (general kernel), lt_trace.exp_link */
 #define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
 #define LT_MAX_BEAM 256    /* largest beam_size of the tuned kernels */
 /* Any other configuration -- max_len > 8 (span slots = max_len) or a beam

@@ -13,7 +13,7 @@ import numpy as np
 from ._build import LIB
 
 LT_OK = 0
-ABI_VERSION = 2           # include/lattice_decode.h LT_ABI_VERSION
+ABI_VERSION = 3           # include/lattice_decode.h LT_ABI_VERSION
 LT_MAX_BEAM = 256          # tuned kernels (lattice_decode.h)
 LT_MAX_BEAM_ANY = 1 << 20  # the general kernel lt_beam_wide
 LT_EUNSUPPORTED = -4

@@ -1644,10 +1644,15 @@ hipError_t launch_k(const DecodeParams& p, int kt, const Launch& L) {
       default: return hipErrorInvalidValue;
     }
   }
+  if constexpr (COUNT) {                 // (decodes of k <= 8 returned above)
+    switch (kt) {
+      case 2: return launch_bp<2, 4, NARROW, COUNT>(p, L);
+      case 4: return launch_bp<4, 4, NARROW, COUNT>(p, L);
+      case 8: return launch_bp<8, 4, NARROW, COUNT>(p, L);
+      default: break;
+    }
+  }
   switch (kt) {
-    case 2: return launch_bp<2, 4, NARROW, COUNT>(p, L);
-    case 4: return launch_bp<4, 4, NARROW, COUNT>(p, L);
-    case 8: return launch_bp<8, 4, NARROW, COUNT>(p, L);
     case 16: return launch_bp<16, BP16_WPB, NARROW, COUNT>(p, L);
     case 32: return launch_bp<32, BP32_WPB, NARROW, COUNT>(p, L);
     // beams above 32: one wave per block (the LDS ring of 9 x KT entries)
