@@ -186,6 +186,22 @@ inline uint64_t seq_hash(const uint32_t* s, uint32_t n) {
   return h ^ (h >> 32);
 }
 
+// seq_hash of the concatenation a[0 .. na) + b[0 .. nb), without building it
+inline uint64_t seq_hash2(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)(na + nb) * 0xC2B2AE3D27D4EB4Full);
+  for (uint32_t i = 0; i < na; ++i) {
+    h ^= a[i];
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 29;
+  }
+  for (uint32_t i = 0; i < nb; ++i) {
+    h ^= b[i];
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 29;
+  }
+  return h ^ (h >> 32);
+}
+
 class Table {
  public:
   std::vector<uint32_t> pool;                 // key code points (+ rule strings)
@@ -195,54 +211,75 @@ class Table {
   void reserve(size_t n) {
     size_t cap = 16;
     while (cap < 2 * n + 16) cap <<= 1;
-    slots_.assign(cap, -1);
+    slots_.assign(cap, 0);
     mask_ = cap - 1;
   }
 
   Info& get_or_add(const uint32_t* s, uint32_t n) {
     const uint64_t h = seq_hash(s, n);
     size_t i = (size_t)h & mask_;
-    while (slots_[i] >= 0) {
-      const Span& k = keys[(size_t)slots_[i]];
-      if (k.len == n && std::equal(s, s + n, pool.data() + k.off)) return infos[(size_t)slots_[i]];
-      i = (i + 1) & mask_;
-    }
+    for (uint64_t v; (v = slots_[i]) != 0; i = (i + 1) & mask_)
+      if (tag_of(v) == tag(h) && same(idx_of(v), s, n)) return infos[idx_of(v)];
     if (2 * (keys.size() + 1) > slots_.size()) {      // grow and re-place
       grow();
       return get_or_add(s, n);
     }
-    slots_[i] = (int32_t)keys.size();
+    slots_[i] = entry(h, keys.size());
     keys.push_back(Span{(uint32_t)pool.size(), n});
     pool.insert(pool.end(), s, s + n);
     infos.emplace_back();
     return infos.back();
   }
 
+  // Most lookups miss (substrings that are no morpheme): a slot carries the
+  // key's hash tag beside its index, so a probe compares the tag in the slot
+  // array and touches the key's span and code points only on a tag match.
   const Info* find(const uint32_t* s, uint32_t n) const {
     const uint64_t h = seq_hash(s, n);
     size_t i = (size_t)h & mask_;
-    while (slots_[i] >= 0) {
-      const Span& k = keys[(size_t)slots_[i]];
-      if (k.len == n && std::equal(s, s + n, pool.data() + k.off)) return &infos[(size_t)slots_[i]];
-      i = (i + 1) & mask_;
+    for (uint64_t v; (v = slots_[i]) != 0; i = (i + 1) & mask_)
+      if (tag_of(v) == tag(h) && same(idx_of(v), s, n)) return &infos[idx_of(v)];
+    return nullptr;
+  }
+  // find() of the concatenation a + b
+  const Info* find2(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb) const {
+    const uint64_t h = seq_hash2(a, na, b, nb);
+    size_t i = (size_t)h & mask_;
+    for (uint64_t v; (v = slots_[i]) != 0; i = (i + 1) & mask_) {
+      if (tag_of(v) != tag(h)) continue;
+      const Span& k = keys[idx_of(v)];
+      const uint32_t* q = pool.data() + k.off;
+      if (k.len == na + nb && std::equal(a, a + na, q) && std::equal(b, b + nb, q + na))
+        return &infos[idx_of(v)];
     }
     return nullptr;
   }
 
  private:
-  std::vector<int32_t> slots_;
+  // slot: hash tag (high 32 bits of the key's hash) << 32 | index + 1; 0 = empty
+  std::vector<uint64_t> slots_;
   size_t mask_ = 0;
 
+  static uint32_t tag(uint64_t h) { return (uint32_t)(h >> 32); }
+  static uint32_t tag_of(uint64_t v) { return (uint32_t)(v >> 32); }
+  static size_t idx_of(uint64_t v) { return (size_t)(uint32_t)v - 1; }
+  static uint64_t entry(uint64_t h, size_t idx) { return ((uint64_t)tag(h) << 32) | (uint64_t)(idx + 1); }
+  bool same(size_t x, const uint32_t* s, uint32_t n) const {
+    const Span& k = keys[x];
+    return k.len == n && std::equal(s, s + n, pool.data() + k.off);
+  }
+
   void grow() {
-    std::vector<int32_t> old;
+    std::vector<uint64_t> old;
     old.swap(slots_);
-    slots_.assign(old.size() * 2, -1);
+    slots_.assign(old.size() * 2, 0);
     mask_ = slots_.size() - 1;
     for (size_t x = 0; x < keys.size(); ++x) {
       const Span& k = keys[x];
-      size_t i = (size_t)seq_hash(pool.data() + k.off, k.len) & mask_;
-      while (slots_[i] >= 0) i = (i + 1) & mask_;
-      slots_[i] = (int32_t)x;
+      const uint64_t h = seq_hash(pool.data() + k.off, k.len);
+      size_t i = (size_t)h & mask_;
+      while (slots_[i] != 0) i = (i + 1) & mask_;
+      slots_[i] = entry(h, x);
     }
   }
 };
@@ -357,6 +394,20 @@ struct Worker {
       out.push_back(WordRec{w_off, m, so, sl, eo, el, lx.name_verb, lx.name_eomi, len, b, e, is_l});
   }
 
+  // consider() of stem s1 + s2, eomi e1 + e2: the two lookups run on the
+  // pieces; the candidate is copied only when both succeed
+  void consider_parts(const uint32_t* s1, uint32_t n1, const uint32_t* s2, uint32_t n2,
+                      const uint32_t* e1, uint32_t m1, const uint32_t* e2, uint32_t m2,
+                      uint32_t w_off, uint32_t m, int32_t len, int32_t b, int32_t e, bool is_l,
+                      std::vector<WordRec>& out) {
+    const Info* ei = lx.table.find2(e1, m1, e2, m2);
+    if (!ei || !(ei->flags & F_EOMI)) return;
+    const Info* si = lx.table.find2(s1, n1, s2, n2);
+    if (!si || !(si->flags & (F_ADJ | F_VERB))) return;
+    set_cand(s1, n1, s2, n2, e1, m1, e2, m2);
+    consider(w_off, m, len, b, e, is_l, out);
+  }
+
   // consider() of the split text[s .. s + sl) + text[s + sl .. s + sl + el)
   void consider_text(uint32_t s, uint32_t sl, uint32_t el, uint32_t w_off, uint32_t m, int32_t len,
                      int32_t b, int32_t e, bool is_l, std::vector<WordRec>& out) {
@@ -394,8 +445,8 @@ struct Worker {
         const size_t first = out.size();
         for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
           const RulePair& rp = R[(size_t)q];
-          set_cand(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, w + i + 1, m - i - 1);
-          consider(w_off, m, len, b, e, is_l, out);
+          consider_parts(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, w + i + 1,
+                         m - i - 1, w_off, m, len, b, e, is_l, out);
         }
         const size_t pass = out.size() - first;
         if (pass) out.reserve(out.size() + pass * (size_t)(ci->rule_n - 1));
@@ -418,8 +469,8 @@ struct Worker {
         if (!ci) continue;
         for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
           const RulePair& rp = R[(size_t)q];
-          set_cand(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, rest, nrest);
-          consider(w_off, m, len, b, e, is_l, out);
+          consider_parts(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, rest, nrest,
+                         w_off, m, len, b, e, is_l, out);
         }
       }
     }
