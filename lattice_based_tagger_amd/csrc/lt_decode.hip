@@ -1620,7 +1620,7 @@ __global__ void __launch_bounds__(256) lt_eval_paths_k(EvalParams p) {
 #define HW_WPB 4                        // waves per block of lt_beam_hw
 #endif
 #ifndef BP16_WPB
-#define BP16_WPB 2                      // waves per block of lt_beam_pk, k = 9..16
+#define BP16_WPB 1                      // waves per block of lt_beam_pk, k = 9..16 (1: 15.9 ms at k=16, 2: 16.7, 4: 16.7)
 #endif
 #ifndef BP32_WPB
 #define BP32_WPB 2                      // waves per block of lt_beam_pk, k = 17..32
