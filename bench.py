@@ -68,7 +68,11 @@ def parse():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--gather', type=int, default=None,
                     help='1: gather every rank\'s results to rank 0 with RCCL inside each step '
-                         '(default: on when WORLD_SIZE > 1)')
+                         '(default: on when WORLD_SIZE > 1; a failed RCCL setup then fails the run); '
+                         '0: no result exchange (labelled in the JSON line)')
+    ap.add_argument('--extra-k', default='5,16',
+                    help='beams timed after the headline on the same batch (single GPU), reported under '
+                         '"extra": BASELINE config 3 secondary (k=5) and config 5 (k=16); "" for none')
     return ap.parse_args()
 
 
@@ -349,15 +353,21 @@ def main():
             uid = d.broadcast_bytes(_capi.comm_unique_id() if d.rank == 0 else None)
             comm = _capi.Comm(ctx, d.world, d.rank, uid)
             comm.prepare(db, k, root=0)
-        except (_capi.LTError, OSError) as exc:      # reported in the JSON line, never silent
+        except (_capi.LTError, OSError) as exc:
             gather_error = '%s: %s' % (type(exc).__name__, exc)
-            print('bench.py: result gather disabled on rank %d: %s' % (d.rank, gather_error),
+            print('bench.py: RCCL result gather failed on rank %d: %s' % (d.rank, gather_error),
                   file=sys.stderr)
-        if d.min(0.0 if gather_error else 1.0) < 1.0:  # every rank gathers, or none does
+        if d.min(0.0 if gather_error else 1.0) < 1.0:
+            # the step includes the gather: without it there is
+            # no valid multi-GPU number -- fail the run on every rank (--gather 0
+            # is the explicit, labelled opt-out)
             if comm:
                 comm.close()
-            comm = None
-            gather_error = gather_error or 'failed on another rank'
+            print('bench.py: rank %d exits: the RCCL gather could not be set up (%s); '
+                  'run with --gather 0 to time the shards without the exchange'
+                  % (d.rank, gather_error or 'failed on another rank'), file=sys.stderr)
+            d.close()
+            sys.exit(3)
     root = d.rank == 0
 
     def step():
@@ -438,6 +448,14 @@ def main():
     else:
         d2h = 4 * piece.n_sent * (1 + 3 * k) + 4 * int(np.sum(piece.sent_n)) * k
 
+    extra = None
+    extra_ks = [int(x) for x in a.extra_k.split(',') if x.strip()]
+    if d.world == 1 and extra_ks:
+        extra = {}
+        for kx in extra_ks:
+            if kx != k:
+                extra['k%d' % kx] = time_beam(ctx, dm, piece, raw, order, lo, hi, kx, a)
+
     if root:
         wl = ('config3' if a.sentences == 65536 else 'config4' if a.sentences == 1048576 else 'custom')
         line = {
@@ -494,15 +512,19 @@ def main():
                             'pinned host memory on a copy stream' if comm else
                             'padded results by DMA to pinned host memory on a copy stream') +
                            ', under the next decode'},
-            'gather': ({'error': gather_error} if gather_error else
-                       {'collective': 'one ncclGather of packed result slabs (RCCL), root 0, on its '
+            'gather': ({'collective': 'one ncclGather of packed result slabs (RCCL), root 0, on its '
                                       'own stream: gather of step i overlaps decode of step i+1',
                         'rccl': (lib.lt_comm_library() or b'?').decode(),
-                        'last_gather_ms': gather_ms, 'in_timed_region': True} if comm else None),
+                        'last_gather_ms': gather_ms, 'in_timed_region': True} if comm else
+                       {'disabled': '--gather 0: every rank decodes its shard, no result exchange; '
+                                    'not a multi-GPU result of the north star'}
+                       if d.world > 1 else None),
             'check': check,
             'host': {'gen_s': t_gen, 'h2d_s': t_up, 'nproc': os.cpu_count(), 'cpu': cpu_model(),
                      'visible_gpus': ndev},
         }
+        if extra is not None:
+            line['extra'] = extra
         if not a.no_cpu_baseline and d.world == 1:
             line['cpu_baseline'] = cpu_baseline(raw, sm, a.cpu_seconds)
             line['cpu_baseline_c'] = cpu_baseline_c(packed, keys, coefs, k, a.cpu_seconds / 2)
@@ -516,6 +538,54 @@ def main():
     dm.close()
     ctx.close()
     d.close()
+
+
+def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a):
+    """The headline's step (decode + result D2H on the copy stream, batch
+    resident in HBM) at beam k on the same batch, same warmup / steps, one
+    GPU: BASELINE config 3's k=5 secondary and config 5 (k=16).  Results
+    are bit-checked against lt_oracle.c in tests/test_gpu_parity.py."""
+    lib = _capi.load()
+    db = _capi.DeviceBatch(ctx, piece, max_k=k)                 # H2D, outside the timed region
+    try:
+        expansions, tuples, probes, table_loads = db.count_ops(dm, k)
+        for _ in range(max(1, a.warmup)):
+            db.launch(dm, k)
+            db.fetch()
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            db.launch(dm, k)
+            db.fetch()
+        ctx.sync()
+        elapsed = time.perf_counter() - t0
+        kern = ctx.kernel_ms_recent(a.steps)
+        count, length = db.results(k)[:2]
+    finally:
+        db.close()
+    kernel = (lib.lt_kernel_name(k) or b'?').decode()
+    avg_kernel_s = float(np.mean(kern)) / 1e3
+    B = algorithmic_bytes(piece, dict_nodes(raw, order, lo, hi), tuples, length, count, k)
+    KB = kernel_bytes(piece, table_loads, k)
+    traffic = traffic_from_profiles(kernel, k, piece.n_sent, a.features, a.seed)
+    return {
+        'beam': k,
+        'value': piece.n_sent * a.steps / elapsed,
+        'unit': 'sentences/s',
+        'ms_per_step': elapsed / a.steps * 1e3,
+        'step': 'decode + result D2H (pinned, copy stream), batch resident in HBM',
+        'kernel': kernel,
+        'avg_kernel_ms': avg_kernel_s * 1e3,
+        'kernel_only_sentences_per_s': piece.n_sent / avg_kernel_s,
+        'roofline': {'bound': 'hbm', 'achieved': B / avg_kernel_s / 1e9, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+                     'algorithmic_bytes_per_launch': B, 'kernel_bytes_per_launch': KB,
+                     'kernel_bytes_frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+                     'traffic': traffic[0] if traffic else None,
+                     'traffic_source': traffic[1] if traffic else None},
+        'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
+                           'table_probes': probes, 'table_slot_loads': table_loads},
+    }
 
 
 def padded_as_packed(res, sent_n, k):

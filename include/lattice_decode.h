@@ -216,9 +216,10 @@ typedef struct {
   const double* score;     /* [n_sent * k] */
   const int32_t* codes;    /* [n_codes] */
 } lt_packed_view;
-/* As lt_result_fetch, for the slab: packing on the decode stream, the copy
- * of the used bytes into the batch's pinned slab on the copy stream (under
- * the next decode).  Complete after lt_sync; overwritten by the next fetch. */
+/* As lt_result_fetch, for the slab: the packing kernels and the copy of the
+ * used bytes into the batch's pinned slab both run on the ctx's copy stream
+ * (after the decode, under the next one).  Complete after lt_sync;
+ * overwritten by the next fetch. */
 lt_status lt_result_fetch_packed(lt_ctx* ctx, lt_batch* batch);
 /* View of the batch's pinned slab (after lt_result_fetch_packed + lt_sync). */
 lt_status lt_result_view_packed(lt_batch* batch, lt_packed_view* view);
@@ -286,10 +287,11 @@ lt_status lt_comm_destroy(lt_comm* comm);
  * slabs and one pinned mirror).  Blocking. */
 lt_status lt_gather_prepare(lt_comm* comm, lt_batch* batch, int k, int root);
 /* Gather the last decode's results (beam k of the prepare) to the root: the
- * results are packed into the next send slot on the ctx stream (a slab, see
- * "compact results"), then one ncclGather of the slabs runs on the
- * communicator's own stream -- so the next decode on the ctx stream overlaps
- * this gather.  Complete after lt_gather_sync. */
+ * results are packed into the next send slot (a slab, see "compact
+ * results") and one ncclGather of the slabs runs, both on the communicator's
+ * own stream -- so the next decode on the ctx stream overlaps this gather.
+ * Complete after lt_gather_sync (lt_sync does not cover it);
+ * lt_batch_destroy waits for the pack's reads of the batch. */
 lt_status lt_gather_launch(lt_comm* comm, lt_batch* batch);
 /* Wait for this rank's outstanding gathers (local, not collective). */
 lt_status lt_gather_sync(lt_comm* comm);

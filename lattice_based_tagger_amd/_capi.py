@@ -205,6 +205,16 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
+def parse_slab(buf):
+    """PackedResults of a slab held in host memory (``buf``: a contiguous
+    uint8 array whose size is the slab's capacity), checked by
+    lt_slab_parse -- how the root reads every rank's slab of a gather."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    v = PackedView()
+    check(load().lt_slab_parse(buf.ctypes.data, buf.size, C.byref(v)))
+    return PackedResults(v)
+
+
 class Context:
     """One device + one HIP stream (lt_ctx)."""
 

@@ -75,8 +75,24 @@ class Beam:
 _model_cache = weakref.WeakKeyDictionary()
 
 
+def _immutable(a):
+    """True when no one can write into the array's memory: the array and
+    every array it views are read-only and the memory is owned by numpy or
+    by an immutable ``bytes`` object."""
+    while isinstance(a, np.ndarray):
+        if a.flags.writeable:
+            return False
+        a = a.base
+    return a is None or isinstance(a, bytes)
+
+
 def _digest_array(a):
-    """Content digest of a numpy array (in-place edits change it)."""
+    """Content digest of a numpy array (in-place edits change it).  A
+    read-only array (``coef.flags.writeable = False``) cannot change, so its
+    identity stands in for the content and the per-call hash of the whole
+    array (about 1 ms for 1M coefficients) is skipped."""
+    if isinstance(a, np.ndarray) and _immutable(a):
+        return ('ro', a.dtype.str, a.shape, a.__array_interface__['data'][0], a.strides)
     a = np.ascontiguousarray(a)
     try:
         import xxhash

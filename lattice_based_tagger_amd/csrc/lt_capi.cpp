@@ -259,7 +259,7 @@ lt_status lt_ctx_create(int device, lt_ctx** out) {
     e = hipEventCreate(&c->kev0[i]);
     if (e == hipSuccess) e = hipEventCreate(&c->kev1[i]);
   }
-  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_counters, 16 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     lt_ctx_destroy(c);
     return fail(LT_EHIP, "lt_ctx_create: %s", hipGetErrorString(e));
@@ -934,6 +934,15 @@ lt_status lt_batch_destroy(lt_batch* b) {
   (void)hipSetDevice(b->ctx->device);
   (void)hipStreamSynchronize(b->ctx->stream);
   (void)hipStreamSynchronize(b->ctx->cstream);
+  // readers of the result slots on other streams (a gather's pack on its
+  // communicator stream, lt_gather_launch): the arena may be recycled by the
+  // next lt_batch_create, so they must be done with it first
+  for (int i = 0; i < 2; ++i)
+    for (int r = 0; r < 2; ++r)
+      if (b->rd_pending[i][r] && b->ev_rd[i][r]) {
+        (void)hipEventSynchronize(b->ev_rd[i][r]);
+        b->rd_pending[i][r] = false;
+      }
   batch_free(b);
   return LT_OK;
 }
@@ -1395,7 +1404,23 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
                 MAX_SPAN, LT_MAX_BEAM_COMPILED);
   HIP_TRY(hipSetDevice(c->device));
   if ((st = next_slot(c, b)) != LT_OK) return st;
-  HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
+#ifdef PK_PHASES
+  // diagnostic build: the shipping (non-counting) kernel, its phase stamps
+  for (size_t q = 0; q < b->pieces.size(); ++q) {
+    piece_params(b, q, k, p);
+    HIP_TRY(launch_decode(p, c->stream, false));
+  }
+  {
+    unsigned long long ph[16];
+    HIP_TRY(hipMemcpyAsync(ph, c->d_counters, sizeof ph, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    fprintf(stderr, "PK_PHASES k=%d waves=%llu steps=%llu lifetime=%llu phases=", k, ph[14], ph[12], ph[13]);
+    for (int i = 0; i < 8; ++i) fprintf(stderr, "%s%llu", i ? "," : "", ph[4 + i]);
+    fprintf(stderr, "\n");
+  }
+  HIP_TRY(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
+#endif
   for (size_t q = 0; q < b->pieces.size(); ++q) {
     piece_params(b, q, k, p);
     HIP_TRY(launch_decode(p, c->stream, true));

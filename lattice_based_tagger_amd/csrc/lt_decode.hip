@@ -531,6 +531,22 @@ __device__ __forceinline__ unsigned long long ord_key(double sc) {
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
+// Phase stamps of the k=1 macro-step (diagnostic builds with -DPK_PHASES only;
+// tools/gpu_phases.sh): s_memtime with its own lgkmcnt(0), fenced by
+// scheduling barriers, summed per wave into counters[4..].
+#ifdef PK_PHASES
+__device__ __forceinline__ unsigned long long pk_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PK_STAMP(i) do { const unsigned long long t_ = pk_stamp(); ph[i] += t_ - tprev; tprev = t_; } while (0)
+#else
+#define PK_STAMP(i) do { } while (0)
+#endif
+
 // per-sentence record of one end position (LDS): first candidate (global
 // node index), candidates, first candidate (local index)
 struct alignas(16) SegRec {
@@ -566,6 +582,12 @@ lt_viterbi_pk(DecodeParams p) {
   uint4* const wst = stg[wv];
   VEntry (*const R)[RING] = ring[wv];
   Counts cnt;
+#ifdef PK_PHASES
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long tstart = pk_stamp();
+  unsigned long long tprev = tstart;
+  unsigned long long nsteps = 0;
+#endif
 
   // lane w < W owns sentence w of the wave
   const bool own = lane < W && slot0 + lane < p.n_sent;
@@ -635,7 +657,9 @@ lt_viterbi_pk(DecodeParams p) {
   // macro-steps (e, r): round r of end position e
   int e = 1, r = 0, em9 = 1;
   while (e <= nmax) {
+    PK_STAMP(0);                                 // [0] loop bookkeeping of the previous step
     __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): staged records, span starts
+    PK_STAMP(1);                                 // [1] wait for the staged records
     const int dmax = min(e, p.max_len);
     const int cb = e & 1;
     const bool act = ms < W;
@@ -672,6 +696,11 @@ lt_viterbi_pk(DecodeParams p) {
     Probe<NARROW> P;
     probe_issue<NARROW>(P, B, slots, seed, h0, cur,
                         (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, aux);
+#ifdef PK_PHASES
+    PK_STAMP(2);                                 // [2] records/ring reads, mapping, primary issue
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    PK_STAMP(3);                                 // [3] wait for the primary slots
+#endif
     // primary slots back: hits, and the secondary loads of misses at flagged
     // slots -- issued before the next macro-step's records are DMA'd, so the
     // DMA's latency hides under theirs.  The DMA comes after every LDS read of
@@ -684,6 +713,11 @@ lt_viterbi_pk(DecodeParams p) {
     dma_packed(B, gn1, wst, lane);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
+#ifdef PK_PHASES
+    PK_STAMP(4);                                 // [4] hit checks, secondary issue, record DMA issue
+    __builtin_amdgcn_s_waitcnt(0x0F73);         // vmcnt(3): all but the 3 DMA instructions
+    PK_STAMP(5);                                 // [5] wait for the secondary slots
+#endif
     double best_s = -INFINITY;
     if (!skip0) {
       const double tri = has_tri ? probe_finish<NARROW, COUNT, false>(P, h1, cur, cnt) : 0.0;
@@ -697,6 +731,7 @@ lt_viterbi_pk(DecodeParams p) {
     // before it.  A round that raises a sentence's maximum discards the
     // earlier rounds' minimum (it belonged to a smaller key); ties with an
     // earlier round keep it (earlier rounds hold smaller indices).
+    PK_STAMP(6);                                 // [6] numpy-order sum, increment
     const unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
     const unsigned long long mprev = (key && r > 0) ? amax[wv][cb][msr] : 0ull;
     if (key) __hip_atomic_fetch_max(&amax[wv][cb][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -725,6 +760,10 @@ lt_viterbi_pk(DecodeParams p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
+    PK_STAMP(7);                                 // [7] argmax (LDS atomics), ring + backpointer write
+#ifdef PK_PHASES
+    ++nsteps;
+#endif
     if (last) {
       A0 = A1; A1 = A2; A2 = A3;
       ++e;
@@ -764,6 +803,15 @@ lt_viterbi_pk(DecodeParams p) {
       atomicAdd(p.counters + 3, ld);
     }
   }
+#ifdef PK_PHASES
+  const unsigned long long tend = pk_stamp();
+  if (lane == 0) {
+    for (int i = 0; i < 8; ++i) atomicAdd(p.counters + 4 + i, ph[i]);
+    atomicAdd(p.counters + 12, nsteps);
+    atomicAdd(p.counters + 13, tend - tstart);
+    atomicAdd(p.counters + 14, 1ull);
+  }
+#endif
 }
 
 // ===========================================================================

@@ -90,7 +90,7 @@ def _default_lookup(dictionary):
             import lattice_tagger.dictionary as ref       # the user's reference install
         except ImportError as exc:
             raise NotImplementedError(
-                'no eojeol lookup: pass lookup=<callable(eojeol, offset) -> [Word]> or a '
+                'no eojeol lookup: pass custom_lookup=<callable(eojeol, offset) -> [Word]> or a '
                 'lattice_tagger MorphemeDictionary') from exc
     return ref.MorphemeLookup(dictionary, flatten=False)
 
@@ -100,11 +100,13 @@ class Tagger:
 
     ``dictionary``  a reference ``MorphemeDictionary`` (or the string
                     'base', which builds the reference BaseMorphemeDictionary)
-    ``lookup``      optional callable ``(eojeol, offset) -> [Word]``; when not
-                    callable the tagger uses MorphemeLookup over
-                    ``dictionary`` with its defaults, as the reference does
-                    (`tagger.py:60`)
+    ``lookup``, ``encoder``  accepted and ignored, as in the reference
+                    (`tagger.py:57-62`: the lattices always come from
+                    ``MorphemeLookup(dictionary, flatten=False)``)
     ``score_funcs`` a ``BeamScoreFunctions`` composite (reference or mirror)
+    ``custom_lookup`` (extension, not in the reference) a callable
+                    ``(eojeol, offset) -> [Word]`` that builds the lattices
+                    instead of MorphemeLookup
     ``device``      HIP device ordinal of the decoder, or a sequence of
                     ordinals: ``tag_batch`` then deals its chunks to the
                     devices in turn (one context per entry; results in
@@ -119,14 +121,17 @@ class Tagger:
     """
 
     def __init__(self, dictionary='base', lookup='subword_lookup', encoder=None,
-                 score_funcs=None, device=0, lexicon=None, native_lookup=True, lookup_threads=0):
+                 score_funcs=None, device=0, lexicon=None, native_lookup=True, lookup_threads=0,
+                 custom_lookup=None):
         self._lexicon = lexicon
         self._lexicon_given = lexicon is not None     # used as given, never rebuilt
         self._eojeol_lookup = None
         self.lookup_threads = lookup_threads
-        if callable(lookup):
+        if custom_lookup is not None:
+            if not callable(custom_lookup):
+                raise TypeError('custom_lookup must be a callable (eojeol, offset) -> [Word]')
             self.dictionary = dictionary
-            self._eojeol_lookup = lookup
+            self._eojeol_lookup = custom_lookup
             self.native = lexicon is not None
         else:
             if isinstance(dictionary, str):

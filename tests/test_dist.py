@@ -105,6 +105,37 @@ def test_bench_dist_shares_the_communicator_id():
     assert res == [(0, True, 1.0, 2.0), (1, True, 1.0, 2.0)]
 
 
+def _al16(x):
+    return (x + 15) // 16 * 16
+
+
+def _slab_layout(n_sent, k, chars):
+    """Section offsets of a slab (lattice_decode.h "compact results",
+    lt_internal.h slab_layout): 32 B header, then 16 B aligned count,
+    length, score and codes; capacity for `chars` characters."""
+    count = 32
+    length = count + _al16(4 * n_sent)
+    score = length + _al16(4 * n_sent * k)
+    codes = score + _al16(8 * n_sent * k)
+    return count, length, score, codes, codes + _al16(4 * chars * k)
+
+
+def _write_slab(res, chars):
+    """A rank's PackedResults as the bytes of its slab, padded to the
+    capacity of its shard (what lt_gather_launch sends)."""
+    S, k = res.n_sent, res.k
+    c0, l0, s0, d0, cap = _slab_layout(S, k, chars)
+    buf = np.zeros(cap, dtype=np.uint8)
+    used = d0 + _al16(4 * res.codes.size)
+    buf[:32] = np.frombuffer(np.array([S, k], np.int32).tobytes() +
+                             np.array([res.codes.size, used, 0], np.int64).tobytes(), np.uint8)
+    buf[c0:c0 + 4 * S] = res.count.astype(np.int32).view(np.uint8)
+    buf[l0:l0 + 4 * S * k] = res.length.astype(np.int32).ravel().view(np.uint8)
+    buf[s0:s0 + 8 * S * k] = res.score.astype(np.float64).ravel().view(np.uint8)
+    buf[d0:d0 + 4 * res.codes.size] = res.codes.astype(np.int32).view(np.uint8)
+    return buf
+
+
 def _strong_worker(rank, world, port, total, out_q):
     """bench.py's strong-scaling path on the CPU: the seeded batch (in
     seeded permutations past the generated lattices, as config 4 builds
@@ -126,7 +157,13 @@ def _strong_worker(rank, world, port, total, out_q):
     g = dist.HostGroup.__new__(dist.HostGroup)
     g.ranks, g.pg = dist.Ranks(), d.pg
     parts = g.gather(mine)
+    # the RCCL path's bytes: every rank's slab (padded to its capacity), laid
+    # out by the root at stride cap = the largest capacity, as the receive
+    # slot of lt_gather_launch holds them, and read back with lt_slab_parse
+    # (lt_gather_view) -- the reassembly that runs only at N > 1 on a node
+    slabs = g.gather(_write_slab(mine, int(np.sum(piece.sent_n))))
     if rank == 0:
+        from lattice_based_tagger_amd import _capi
         ref = bench.padded_as_packed(lt_oracle.decode(packed, keys, coefs, k)[:4], packed.sent_n, k)
         idx = np.arange(packed.n_sent) if order is None else order
         ok = bench.check_results(parts, ref, idx)
@@ -135,6 +172,19 @@ def _strong_worker(rank, world, port, total, out_q):
             caught = False
         except AssertionError:
             caught = True
+        cap = max(x.size for x in slabs)
+        recv = np.zeros(cap * world, dtype=np.uint8)
+        for q, x in enumerate(slabs):
+            recv[q * cap:q * cap + x.size] = x
+        views = [_capi.parse_slab(recv[q * cap:(q + 1) * cap]) for q in range(world)]
+        ok = ok and bench.check_results(views, ref, idx)
+        bad = recv[:cap].copy()
+        bad[16:24] = np.frombuffer(np.int64(cap + 16).tobytes(), np.uint8)   # used bytes past the slot
+        try:
+            _capi.parse_slab(bad)
+            caught = False
+        except _capi.LTError:
+            pass
         out_q.put((ok, caught, all(p.n_sent > 0 for p in parts), [p.n_sent for p in parts]))
     d.close()
 

@@ -74,7 +74,7 @@ def _gpu_decode(ctx, packed, keys, coefs, k):
         dm.close()
 
 
-@pytest.mark.parametrize('k,n_sent', [(1, 65536), (5, 8192), (16, 4096), (2, 2048), (3, 2048), (8, 2048), (32, 512),
+@pytest.mark.parametrize('k,n_sent', [(5, 8192), (16, 4096), (2, 2048), (3, 2048), (8, 2048), (32, 512),
                                        (33, 300), (64, 300), (100, 200), (256, 120)])
 def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
     packed, keys, coefs = _synthetic(n_sent, seed=100 + k, n_features=1_000_000)
@@ -105,6 +105,44 @@ def test_dense_lattices_with_ties_match_c_oracle(gpu_decoder, k):
     assert np.array_equal(score.view(np.uint64), o_score.view(np.uint64))
     assert np.array_equal(codes, o_codes)
     assert (ex, tu) == (o_ex, o_tu)
+
+
+@pytest.fixture(scope='module')
+def config3_batch():
+    """BASELINE config 3 exactly as bench.py builds it: 65,536 synthetic
+    sentences (seed 0), 1M-key trigram model."""
+    import bench
+    raw, lay, sm, packed, keys, coefs = bench.make_workload(65536, 0, 1_000_000)
+    return packed, keys, coefs
+
+
+@pytest.mark.parametrize('k', [1, 5, 16])
+def test_config3_full_batch_matches_c_oracle(gpu_decoder, config3_batch, k):
+    """The whole 64K-sentence bench batch, byte for byte against the C
+    restatement: k=1 (the headline), k=5 (config 3 secondary, Tagger.tag's
+    default) and k=16 (config 5) -- counts, lengths, score bits, codes and
+    the reference-algorithm operation counts."""
+    packed, keys, coefs = config3_batch
+    (count, length, score, codes), (ex, tu, _, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
+    o_count, o_len, o_score, o_codes, o_ex, o_tu = lt_oracle.decode(packed, keys, coefs, k, nthreads=16)
+    assert np.array_equal(count, o_count)
+    assert np.array_equal(length, o_len)
+    assert np.array_equal(score.view(np.uint64), o_score.view(np.uint64))   # 0 ULP
+    assert np.array_equal(codes, o_codes)
+    assert (ex, tu) == (o_ex, o_tu)
+
+
+def test_long_sentences_cross_the_lds_backpointer_window(gpu_decoder):
+    """k=1 keeps the backpointers of end positions < PK_BPL (87) in LDS and
+    the rest in HBM: 40-eojeol sentences (about 140 characters) put most
+    positions past the window; byte-equal to the C restatement."""
+    packed, keys, coefs = _synthetic(8192, seed=4040, n_features=200_000, eojeols=40)
+    assert float(np.mean(packed.sent_n)) > 120
+    (count, length, score, codes), _ = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, 1)
+    o = lt_oracle.decode(packed, keys, coefs, 1, nthreads=16)
+    assert np.array_equal(count, o[0]) and np.array_equal(length, o[1])
+    assert np.array_equal(score.view(np.uint64), o[2].view(np.uint64))
+    assert np.array_equal(codes, o[3])
 
 
 def test_full_size_properties(gpu_decoder):

@@ -166,3 +166,29 @@ def test_words_bulk_strings_with_nul():
     bulk = lat.words_bulk(idx)
     assert [tuple(w) for w in bulk] == [tuple(lat.word(int(i))) for i in idx]
     assert any('\x00' in w.word for w in bulk)
+
+
+def test_tagger_ignores_lookup_argument_like_the_reference(fix):
+    """The reference Tagger ignores its ``lookup`` argument and always builds
+    MorphemeLookup(dictionary) (tagger.py:57-62): a callable passed as
+    ``lookup`` is never called and the lattices are the reference's.  The
+    build's own extension keyword ``custom_lookup`` does use the callable."""
+    from lattice_based_tagger_amd import Tagger
+    entry = fix['demo']
+    calls = []
+
+    def f(eojeol, offset):
+        calls.append(eojeol)
+        return []
+
+    t = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lookup=f, lexicon=fixture_lexicon(entry))
+    for sent, exp in list(zip(entry['sentences'], entry['lattices']))[:10]:
+        bindex, _ = t.lattice(sent)
+        assert [[list(w) for w in ws] for ws in bindex] == exp
+    assert calls == []
+    t2 = Tagger(dictionary=fixture_dictionary(entry['lexicon']), custom_lookup=f)
+    sent = entry['sentences'][0]
+    assert t2.lattice(sent)[0] == []
+    assert calls == sent.split()
+    with pytest.raises(TypeError):
+        Tagger(dictionary=fixture_dictionary(entry['lexicon']), custom_lookup='not callable')

@@ -58,3 +58,19 @@ def test_scalar_table_and_coefficient_edits_relower():
             assert beam.lowered_model(funcs) is not m4
         finally:
             del inner['__probe__']
+
+
+def test_read_only_coefficients_skip_the_content_hash():
+    """A read-only coefficient array cannot change, so its identity is its
+    fingerprint (no per-call hash of the array); a read-only view of a
+    writeable array is still hashed (the owner can write through)."""
+    owned = np.arange(1000, dtype=np.float64)
+    owned.flags.writeable = False
+    assert beam._digest_array(owned)[0] == 'ro'
+    base = np.arange(1000, dtype=np.float64)
+    view = base[:]
+    view.flags.writeable = False
+    d0 = beam._digest_array(view)
+    assert d0[0] != 'ro'
+    base[3] = -1.0
+    assert beam._digest_array(view) != d0
