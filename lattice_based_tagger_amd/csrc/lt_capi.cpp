@@ -883,11 +883,15 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
         r.word = (uint32_t)d->node_word[i];
         r.morph = (uint32_t)d->node_morph0[i];
         r.tag = (uint32_t)d->node_tag[i];
-        r.mask = d->node_mask[i] & ~(D_MASK | F_WI);
+        // device mask layout (lt_common.h device_mask); an absent class 4/5/6
+        // coefficient is stored as -0.0, the identity of a float64 sum, so a
+        // decoder may add it unconditionally
+        const uint32_t am = (uint32_t)d->node_mask[i];
+        r.mask = device_mask(am);
         r.pre = d->node_pre[i];
-        r.f4 = d->node_f4[i];
-        r.f5 = d->node_f5[i];
-        r.f6 = d->node_f6[i];
+        r.f4 = (am & F_HAS4) ? d->node_f4[i] : -0.0;
+        r.f5 = (am & F_HAS5) ? d->node_f5[i] : -0.0;
+        r.f6 = (am & F_HAS6) ? d->node_f6[i] : -0.0;
       }
       // (the general kernel of max_len > 8 takes the span from the table)
       const int32_t* ss = d->span_start + d->sent_span_off[s];
@@ -1116,7 +1120,7 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
     r.word = (uint32_t)d->word[w];
     r.morph = (uint32_t)d->morph0[w];
     r.tag = (uint32_t)d->tag[w];
-    r.mask = d->mask[w] & ~(D_MASK | F_WI);
+    r.mask = device_mask((uint32_t)d->mask[w]);          // lt_common.h device layout
     r.pre = 0.0;
     r.f4 = d->f4[w];
     r.f5 = d->f5[w];

@@ -35,6 +35,40 @@ constexpr int D_SHIFT = 24;
 constexpr uint32_t D_MASK = 7u << D_SHIFT;
 constexpr uint32_t F_WI = 1u << 31;
 
+// -- device node mask (NodeRec.mask) ----------------------------------------
+// The library re-encodes the API mask above per role, so that the probes an
+// expansion needs are one AND of the candidate's and the hypothesis' bits.
+// Probe q = 0..5 is feature class 0, 1, 2, 3, 7, 8 (feature.py:95-119).
+//   bits 0-5   DK: probe q can be present with this node as wk
+//              (q0 K0B&K0C, q1 K1B, q2 K2B&K2C, q3 K3B, q4 K7C, q5 K8B&ctx)
+//   bits 6-11  DJ: ... as wj (q0 J0A, q1 J1A, q2 J2A, q3 J3A, q4 J7B,
+//              q5 J8A&ctx -- class 8 from (wj, wk))
+//   bit 12     DJ_NCTX: tag0 not in C (class 8 then comes from (wi, wk))
+//   bit 13     DI_7: as wi of class 7 (I7A); bit 14 DI_8: as wi of class 8 (I8A&ctx)
+//   bits 16-20 the API flags (F_UNK, F_CTX, F_HAS4, F_HAS5, F_HAS6)
+//   bits 24-26 span length d-1 (D_SHIFT); bit 31 F_WI (hypothesis entries)
+constexpr int DJ_SHIFT = 6;
+constexpr uint32_t DQ_ALL = 0x3Fu;
+constexpr uint32_t DJ_NCTX = 1u << 12, DI_7 = 1u << 13, DI_8 = 1u << 14;
+LT_HD uint32_t device_mask(uint32_t m) {
+  const uint32_t ctx = (m & F_CTX) ? 1u : 0u;
+  const auto b = [m](uint32_t bit) -> uint32_t { return (m & bit) ? 1u : 0u; };
+  uint32_t d = 0;
+  d |= (b(K0B) & b(K0C)) << 0 | b(K1B) << 1 | (b(K2B) & b(K2C)) << 2 | b(K3B) << 3 | b(K7C) << 4 |
+       (b(K8B) & ctx) << 5;
+  d |= (b(J0A) << 0 | b(J1A) << 1 | b(J2A) << 2 | b(J3A) << 3 | b(J7B) << 4 | (b(J8A) & ctx) << 5) << DJ_SHIFT;
+  d |= (ctx ^ 1u) << 12 | b(I7A) << 13 | (b(I8A) & ctx) << 14;
+  return d | (m & FLAG_BITS);
+}
+// The hypothesis' half of the probe bits: wj's DJ bits, class 7 only with a
+// wi that can take part, class 8 from (wj, wk) or else (wi, wk).  `wi` = the
+// device mask of wi (its DI bits used), `has_i` = wi exists.
+LT_HD uint32_t hyp_probe_bits(uint32_t wj, uint32_t wi, bool has_i) {
+  const uint32_t i7 = has_i ? (wi >> 13) & 1u : 0u, i8 = has_i ? (wi >> 14) & 1u : 0u;
+  return ((wj >> DJ_SHIFT) & 0xFu) | ((((wj >> 10) & 1u) & i7) << 4) |
+         ((((wj >> 11) & 1u) | (((wj >> 12) & 1u) & i8)) << 5);
+}
+
 constexpr int MAX_SPAN = 8;
 constexpr int RING = MAX_SPAN + 1;     // frontier positions e-8 .. e
 // span slots per end position of a batch with this max_len: 8 (the tuned

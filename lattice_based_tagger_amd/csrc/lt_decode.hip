@@ -203,6 +203,12 @@ struct Tab<true> {
                                    uint32_t, uint32_t slots) {
     return narrow_slot2(x.hk, a, b, c, cls, slots);
   }
+  // a frozen arbitrary value (no instruction): lanes that load nothing keep a
+  // defined slot, so a check can select on it instead of branching
+  __device__ static void arbitrary(S& s) {
+    s.key = __builtin_nondeterministic_value(s.key);
+    s.coef = __builtin_nondeterministic_value(s.coef);
+  }
   __device__ static S load(rsrc_t t, uint32_t off) {
     const u32x4 v = ld128(t, off);
     S s;
@@ -234,6 +240,13 @@ struct Tab<false> {
   __device__ static uint32_t slot2(const Aux&, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
                                    uint32_t seed, uint32_t slots) {
     return wide_slot2(a, b, c, cls, seed, slots);
+  }
+  __device__ static void arbitrary(S& s) {
+    s.a = __builtin_nondeterministic_value(s.a);
+    s.b = __builtin_nondeterministic_value(s.b);
+    s.c = __builtin_nondeterministic_value(s.c);
+    s.cls1 = __builtin_nondeterministic_value(s.cls1);
+    s.coef = __builtin_nondeterministic_value(s.coef);
   }
   __device__ static S load(rsrc_t t, uint32_t off) {
     const u32x4 k = ld128(t, off);
@@ -296,22 +309,11 @@ __device__ __forceinline__ bool use_j8_of(const Hyp& h, const Cand& c) {
   return (c.mask & F_CTX) && (h.jmask & F_CTX);
 }
 
-// Which of the six probed classes can be present (exact pre-filter on the
-// component-slot bits; an absent class issues no load).
+// Which of the six probed classes can be present: the candidate's DK bits
+// and the hypothesis' bits (exact pre-filter on the component-slot bits, the
+// device mask layout of lt_common.h); an absent class issues no load.
 __device__ __forceinline__ uint32_t probe_need(const Hyp& h, const Cand& c) {
-  const uint32_t jm = h.jmask, km = c.mask, im = h.imask;
-  const bool has_i = (im & F_WI) != 0;
-  const bool k_ctx = (km & F_CTX) != 0, j_ctx = (jm & F_CTX) != 0;
-  const bool use_j8 = k_ctx && j_ctx;
-  const bool use_i8 = k_ctx && !j_ctx && has_i && (im & F_CTX);
-  uint32_t need = 0;
-  need |= ((jm & J0A) && (km & K0B) && (km & K0C)) ? 1u : 0u;
-  need |= ((jm & J1A) && (km & K1B)) ? 2u : 0u;
-  need |= ((jm & J2A) && (km & K2B) && (km & K2C)) ? 4u : 0u;
-  need |= ((jm & J3A) && (km & K3B)) ? 8u : 0u;
-  need |= (has_i && (im & I7A) && (jm & J7B) && (km & K7C)) ? 16u : 0u;
-  need |= (use_j8 ? ((jm & J8A) && (km & K8B)) : (use_i8 && (im & I8A) && (km & K8B))) ? 32u : 0u;
-  return need;
+  return c.mask & hyp_probe_bits(h.jmask, h.imask, (h.imask & F_WI) != 0) & DQ_ALL;
 }
 
 // Stage the LDS parts of the model (all threads of the block, before any
@@ -466,18 +468,153 @@ __device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c
 // beam_size = 1
 // ===========================================================================
 
+// Ring entry of the k=1 kernel: the hypothesis (best path ending at one end
+// position) reduced to what scoring an expansion of it needs.
 struct alignas(16) VEntry {
-  double score, f6;
-  uint32_t jword, jmorph, jtag, jmask;
-  uint32_t iword, imorph, imask, depth;
+  double score, f6;             // f6: wj's class-6 coefficient (-0.0 when absent)
+  uint32_t jword, jtag, a8, meta;
+  uint32_t iword, jmorph, depth, pad;
+};
+// meta: bits 0-5 the hypothesis' probe bits (hyp_probe_bits), wj's DI_7 /
+// DI_8 (bits 13-14, for the next hypothesis), wj's F_UNK / F_CTX / F_HAS6;
+// bit 15 (counting builds) wi's F_CTX.  a8: the first component of class 8
+// (feature.py:113-119): wj.morph0 when wj's tag is in C, else wi.morph0.
+constexpr uint32_t V_META_J = DI_7 | DI_8 | F_UNK | F_CTX | F_HAS6;
+constexpr uint32_t V_ICTX = 1u << 15;
+
+// k=1 probe q = 0..5 (classes 0, 1, 2, 3, 7, 8) of appending candidate c to
+// the ring entry h: its key components (feature.py:95-119)
+struct V1Keys {
+  uint32_t a[6], b[6], c[6];
+};
+__device__ __forceinline__ V1Keys v1_keys(const VEntry& h, const Cand& c) {
+  V1Keys K;
+  K.a[0] = h.jword; K.b[0] = c.word;  K.c[0] = c.tag;
+  K.a[1] = h.jword; K.b[1] = c.tag;   K.c[1] = 0;
+  K.a[2] = h.jtag;  K.b[2] = c.word;  K.c[2] = c.tag;
+  K.a[3] = h.jtag;  K.b[3] = c.tag;   K.c[3] = 0;
+  K.a[4] = h.iword; K.b[4] = h.jword; K.c[4] = c.word;
+  K.a[5] = h.a8;    K.b[5] = c.morph; K.c[5] = 0;
+  return K;
+}
+
+// Exact key match of a slot (the overflow flag ignored), narrow tables as
+// two 32-bit halves of c3<<60 | a<<40 | b<<20 | c (v_lshl_or_b32 builds).
+template <bool NARROW>
+__device__ __forceinline__ bool v1_hit(const typename Tab<NARROW>::S& s, uint32_t a, uint32_t b, uint32_t c,
+                                       uint32_t cls) {
+  if constexpr (NARROW) {
+    const uint32_t lo = (b << 20) | c;
+    const uint32_t hi = (cls_code(cls) << 28) | (a << 8) | (b >> 12);
+    const uint32_t slo = (uint32_t)s.key, shi = (uint32_t)(s.key >> 32) & 0x7FFFFFFFu;
+    return (slo == lo) & (shi == hi);
+  } else {
+    return Tab<false>::hit(s, Tab<false>::key(a, b, c, cls));
+  }
+}
+
+// One expansion's trigram probes in three phases around the two memory round
+// trips: issue the primary slot of every needed probe; check them (hit ->
+// coefficient, miss at a flagged slot -> secondary load into the same
+// registers); check the secondaries.  cf[q] ends as the coefficient of a
+// present feature or -0.0 (the identity of the float64 sum) when absent.
+template <bool NARROW>
+struct V1Probe {
+  typename Tab<NARROW>::S s[6];           // primary slots
+  typename Tab<NARROW>::S s2[6];          // secondary slots (where loaded)
+  double cf[6];
+  uint32_t gneed, need2, pres;
 };
 
-__device__ __forceinline__ Hyp read_hyp(const VEntry& e) {
-  Hyp h;
-  h.score = e.score; h.f6 = e.f6;
-  h.jword = e.jword; h.jmorph = e.jmorph; h.jtag = e.jtag; h.jmask = e.jmask;
-  h.iword = e.iword; h.imorph = e.imorph; h.imask = e.imask; h.depth = e.depth;
-  return h;
+template <bool NARROW>
+__device__ __forceinline__ void v1_issue(V1Probe<NARROW>& P, const Bufs& B, uint32_t slots, uint32_t seed,
+                                         const VEntry& h, const Cand& c, uint32_t need, const Aux& aux) {
+  using T = Tab<NARROW>;
+  const V1Keys K = v1_keys(h, c);
+  uint32_t gneed = need, pres = 0;
+  P.cf[3] = -0.0;
+  if (aux.d3 && ((need >> 3) & 1u)) {        // class 3 from the dense LDS table
+    const double v = aux.d3[d3_index(h.jtag, aux.d3mul) * D3_DIM + d3_index(c.tag, aux.d3mul)];
+    const bool present = __builtin_bit_cast(uint64_t, v) != D3_ABSENT;
+    P.cf[3] = present ? v : -0.0;
+    pres = present ? 8u : 0u;
+    gneed &= ~8u;
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    T::arbitrary(P.s[q]);
+    if ((gneed >> q) & 1u)                    // exec-masked: an idle lane costs the TA nothing
+      P.s[q] = T::load(B.tab, T::slot1(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+  }
+  P.gneed = gneed;
+  P.pres = pres;
+}
+
+template <bool NARROW>
+__device__ __forceinline__ void v1_check(V1Probe<NARROW>& P, const Bufs& B, uint32_t slots, uint32_t seed,
+                                         const VEntry& h, const Cand& c, const Aux& aux) {
+  using T = Tab<NARROW>;
+  const V1Keys K = v1_keys(h, c);
+  uint32_t need2 = 0, pres = P.pres;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    if (q == 3 && aux.d3) continue;
+    // branch-free: every lane's slot is defined (T::arbitrary)
+    const bool n = (P.gneed >> q) & 1u;
+    const bool hit = n & v1_hit<NARROW>(P.s[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
+    const bool sec = n & !hit & T::flagged(P.s[q]);
+    P.cf[q] = hit ? P.s[q].coef : -0.0;
+    pres |= hit ? 1u << q : 0u;
+    need2 |= sec ? 1u << q : 0u;
+  }
+  P.need2 = need2;
+  P.pres = pres;
+}
+
+// The secondary slots of the misses at flagged primaries (fresh registers:
+// reusing the primary's would need a copy that waits for the load).
+template <bool NARROW>
+__device__ __forceinline__ void v1_issue2(V1Probe<NARROW>& P, const Bufs& B, uint32_t slots, uint32_t seed,
+                                          const VEntry& h, const Cand& c, const Aux& aux) {
+  using T = Tab<NARROW>;
+  const V1Keys K = v1_keys(h, c);
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    if ((P.need2 >> q) & 1u)
+      P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+}
+
+template <bool NARROW>
+__device__ __forceinline__ void v1_second(V1Probe<NARROW>& P, const VEntry& h, const Cand& c) {
+  const V1Keys K = v1_keys(h, c);
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    if ((P.need2 >> q) & 1u) {                   // (skipped by the wave when no lane loaded one)
+      const bool hit = v1_hit<NARROW>(P.s2[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
+      P.cf[q] = hit ? P.s2[q].coef : P.cf[q];
+      P.pres |= hit ? 1u << q : 0u;
+    }
+}
+
+// Trigram score (score_funcs.py:141-144): numpy's pairwise order over the
+// present features v = [c0, c1, c2, c3, f4, f5, f6, c7, c8] (H7).  With
+// fewer than 8 present it is the left-to-right sum, in which an absent
+// feature's -0.0 changes nothing; 8 or 9 present (rare) take numpy_sum9.
+__device__ __forceinline__ double v1_sum(const double (&cf)[6], uint32_t pres6, const Cand& c,
+                                         const VEntry& h) {
+  const uint32_t pres = (pres6 & 0xFu) | ((c.mask >> 14) & 0x30u) | ((h.meta >> 14) & 0x40u) |
+                        ((pres6 & 0x30u) << 3);
+  const double v[9] = {cf[0], cf[1], cf[2], cf[3], c.f4, c.f5, h.f6, cf[4], cf[5]};
+  if (__builtin_popcount(pres) >= 8) {
+    bool pr[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) pr[q] = (pres >> q) & 1u;
+    return numpy_sum9(v, pr);
+  }
+  double t = 0.0;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) t = t + v[q];
+  return t;
 }
 
 // ---------------------------------------------------------------------------
@@ -604,8 +741,10 @@ lt_viterbi_pk(DecodeParams p) {
     const Cand b0 = load_cand(B, nbase);       // beam[0] = [BOS] (beam.py:21-23)
     VEntry e0;
     e0.score = 0.0; e0.f6 = b0.f6;
-    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
-    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+    e0.jword = b0.word; e0.jtag = b0.tag; e0.jmorph = b0.morph;
+    e0.a8 = b0.morph;                          // (used only when BOS's tag is in C)
+    e0.meta = hyp_probe_bits(b0.mask, 0u, false) | (b0.mask & V_META_J);
+    e0.iword = 0; e0.depth = 0; e0.pad = 0;
     R[lane][0] = e0;
   }
   if (lane < W) {
@@ -676,8 +815,8 @@ lt_viterbi_pk(DecodeParams p) {
     const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
     int bm0 = em9 - d0;
     bm0 += bm0 < 0 ? RING : 0;
-    const Hyp h0 = read_hyp(R[msr][act ? bm0 : 0]);
-    const bool skip0 = !act || ((h0.jmask & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));   // beam.py:43-45
+    const VEntry h0 = R[msr][act ? bm0 : 0];
+    const bool skip0 = !act || ((h0.meta & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));   // beam.py:43-45
 
     // next macro-step: another round of e, or round 0 of e + 1 (then also the
     // span start two positions ahead for the owner lanes)
@@ -693,9 +832,9 @@ lt_viterbi_pk(DecodeParams p) {
       map_round(e, r + 1, A0, A1, cb, false, ms1, mg1, gn1);
     }
 
-    Probe<NARROW> P;
-    probe_issue<NARROW>(P, B, slots, seed, h0, cur,
-                        (!skip0 && has_tri) ? probe_need(h0, cur) : 0u, aux);
+    V1Probe<NARROW> P;
+    const uint32_t need = (!skip0 && has_tri) ? (cur.mask & h0.meta & DQ_ALL) : 0u;
+    v1_issue<NARROW>(P, B, slots, seed, h0, cur, need, aux);
 #ifdef PK_PHASES
     PK_STAMP(2);                                 // [2] records/ring reads, mapping, primary issue
     __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -706,22 +845,32 @@ lt_viterbi_pk(DecodeParams p) {
     // DMA's latency hides under theirs.  The DMA comes after every LDS read of
     // this step's scoring: an LDS read issued after a buffer->LDS DMA waits
     // for it (vmcnt).
-    const Hyp h1 = read_hyp(R[msr][act ? bm0 : 0]);
-    if (!skip0 && has_tri) probe_second<NARROW>(P, B, slots, seed, aux, h1, cur);
+    const VEntry h1 = R[msr][act ? bm0 : 0];
+    v1_check<NARROW>(P, B, slots, seed, h1, cur, aux);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
     dma_packed(B, gn1, wst, lane);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
+    v1_issue2<NARROW>(P, B, slots, seed, h1, cur, aux);   // secondaries: their wait covers the DMA too
 #ifdef PK_PHASES
-    PK_STAMP(4);                                 // [4] hit checks, secondary issue, record DMA issue
-    __builtin_amdgcn_s_waitcnt(0x0F73);         // vmcnt(3): all but the 3 DMA instructions
-    PK_STAMP(5);                                 // [5] wait for the secondary slots
+    PK_STAMP(4);                                 // [4] hit checks, record DMA issue, secondary issue
+    __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0)
+    PK_STAMP(5);                                 // [5] wait for the secondary slots and the DMA
 #endif
     double best_s = -INFINITY;
     if (!skip0) {
-      const double tri = has_tri ? probe_finish<NARROW, COUNT, false>(P, h1, cur, cnt) : 0.0;
-      if (COUNT) ++cnt.exp;
+      v1_second<NARROW>(P, h1, cur);
+      const double tri = has_tri ? v1_sum(P.cf, P.pres, cur, h1) : 0.0;
+      if (COUNT) {
+        const bool has_i = h1.depth > 0;
+        const bool k_ctx = (cur.mask & F_CTX) != 0, j_ctx = (h1.meta & F_CTX) != 0;
+        const bool i_ctx = (h1.meta & V_ICTX) != 0;
+        ++cnt.exp;
+        cnt.tup += 6 + ((h1.meta & F_UNK) ? 1 : 0) + (has_i ? 1 : 0) + ((k_ctx && (j_ctx || (has_i && i_ctx))) ? 1 : 0);
+        cnt.probe += __builtin_popcount(need);
+        cnt.load += __builtin_popcount(P.gneed) + __builtin_popcount(P.need2);
+      }
       best_s = h1.score + increment(p, cur, tri, gn0);              // beam.py:115
     }
 
@@ -745,11 +894,13 @@ lt_viterbi_pk(DecodeParams p) {
       amin[wv][cb ^ 1][lane] = INV;
     }
     if (top && mgw == (uint32_t)mg) {            // the (round's) winner writes beam[e]
-      VEntry ne;
+      VEntry ne;                                 // Sequence.add (beam.py:112-116): wi = wj, wj = wk
       ne.score = best_s; ne.f6 = cur.f6;
-      ne.jword = cur.word; ne.jmorph = cur.morph; ne.jtag = cur.tag; ne.jmask = cur.mask;
-      ne.iword = h1.jword; ne.imorph = h1.jmorph; ne.imask = h1.jmask | F_WI;
-      ne.depth = h1.depth + 1;
+      ne.jword = cur.word; ne.jtag = cur.tag; ne.jmorph = cur.morph;
+      ne.a8 = (cur.mask & F_CTX) ? cur.morph : h1.jmorph;
+      ne.meta = hyp_probe_bits(cur.mask, h1.meta, true) | (cur.mask & V_META_J);
+      if (COUNT) ne.meta |= (h1.meta & F_CTX) ? V_ICTX : 0u;
+      ne.iword = h1.jword; ne.depth = h1.depth + 1; ne.pad = 0;
       R[msr][em9] = ne;
       const uint32_t bpv = bp_pack(sr.a + (uint32_t)mg, (uint32_t)d0, 0u);
       if (e < BPL) {
