@@ -617,6 +617,105 @@ __device__ __forceinline__ double v1_sum(const double (&cf)[6], uint32_t pres6, 
   return t;
 }
 
+// The beam kernels' probes: both candidate slots of every needed probe in
+// one round trip (the flag-free copy of the table, lt_model.d_plain), checked
+// branch-free into cf[q] / pres as v1_check.
+template <bool NARROW>
+struct BMProbe {
+  typename Tab<NARROW>::S s1[6], s2[6];
+  double cf3;                              // class 3 from the dense LDS table
+  uint32_t gneed, pres3;
+};
+
+template <bool NARROW>
+__device__ __forceinline__ void bm_issue(BMProbe<NARROW>& P, const Bufs& B, uint32_t slots, uint32_t seed,
+                                         const VEntry& h, const Cand& c, uint32_t need, const Aux& aux) {
+  using T = Tab<NARROW>;
+  const V1Keys K = v1_keys(h, c);
+  uint32_t gneed = need;
+  P.cf3 = -0.0;
+  P.pres3 = 0;
+  if (aux.d3 && ((need >> 3) & 1u)) {
+    const double v = aux.d3[d3_index(h.jtag, aux.d3mul) * D3_DIM + d3_index(c.tag, aux.d3mul)];
+    const bool present = __builtin_bit_cast(uint64_t, v) != D3_ABSENT;
+    P.cf3 = present ? v : -0.0;
+    P.pres3 = present ? 8u : 0u;
+    gneed &= ~8u;
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    T::arbitrary(P.s1[q]);
+    T::arbitrary(P.s2[q]);
+    if ((gneed >> q) & 1u) {
+      P.s1[q] = T::load(B.tab, T::slot1(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+      P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+    }
+  }
+  P.gneed = gneed;
+}
+
+// key match in the flag-free table
+template <bool NARROW>
+__device__ __forceinline__ bool bm_hit(const typename Tab<NARROW>::S& s, uint32_t a, uint32_t b, uint32_t c,
+                                       uint32_t cls) {
+  if constexpr (NARROW) {
+    const uint32_t lo = (b << 20) | c;
+    const uint32_t hi = (cls_code(cls) << 28) | (a << 8) | (b >> 12);
+    return ((uint32_t)s.key == lo) & ((uint32_t)(s.key >> 32) == hi);
+  } else {
+    return Tab<false>::hit_plain(s, Tab<false>::key(a, b, c, cls));
+  }
+}
+
+template <bool NARROW>
+__device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntry& h, const Cand& c) {
+  const V1Keys K = v1_keys(h, c);
+  double cf[6];
+  uint32_t pres = P.pres3;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const bool n = (P.gneed >> q) & 1u;
+    const bool m1 = n & bm_hit<NARROW>(P.s1[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
+    const bool m2 = n & bm_hit<NARROW>(P.s2[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
+    cf[q] = m1 ? P.s1[q].coef : (m2 ? P.s2[q].coef : (q == 3 ? P.cf3 : -0.0));
+    pres |= (m1 | m2) ? 1u << q : 0u;
+  }
+  return v1_sum(cf, pres, c, h);
+}
+
+// Sequence.add into a ring entry (beam.py:112-116): wi = wj, wj = wk
+template <bool COUNT>
+__device__ __forceinline__ VEntry v_grow(const VEntry& h, const Cand& c, double score) {
+  VEntry ne;
+  ne.score = score; ne.f6 = c.f6;
+  ne.jword = c.word; ne.jtag = c.tag; ne.jmorph = c.morph;
+  ne.a8 = (c.mask & F_CTX) ? c.morph : h.jmorph;
+  ne.meta = hyp_probe_bits(c.mask, h.meta, true) | (c.mask & V_META_J);
+  if (COUNT) ne.meta |= (h.meta & F_CTX) ? V_ICTX : 0u;
+  ne.iword = h.jword; ne.depth = h.depth + 1; ne.pad = 0;
+  return ne;
+}
+// beam[0] = [BOS] (beam.py:21-23)
+__device__ __forceinline__ VEntry v_bos(const Cand& b0) {
+  VEntry e0;
+  e0.score = 0.0; e0.f6 = b0.f6;
+  e0.jword = b0.word; e0.jtag = b0.tag; e0.jmorph = b0.morph;
+  e0.a8 = b0.morph;                          // (used only when BOS's tag is in C)
+  e0.meta = hyp_probe_bits(b0.mask, 0u, false) | (b0.mask & V_META_J);
+  e0.iword = 0; e0.depth = 0; e0.pad = 0;
+  return e0;
+}
+// operation counts of one expansion (lt_count_ops)
+__device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand& c, uint32_t need, uint32_t loads) {
+  const bool has_i = h.depth > 0;
+  const bool k_ctx = (c.mask & F_CTX) != 0, j_ctx = (h.meta & F_CTX) != 0;
+  const bool i_ctx = (h.meta & V_ICTX) != 0;
+  ++cnt.exp;
+  cnt.tup += 6 + ((h.meta & F_UNK) ? 1 : 0) + (has_i ? 1 : 0) + ((k_ctx && (j_ctx || (has_i && i_ctx))) ? 1 : 0);
+  cnt.probe += __builtin_popcount(need);
+  cnt.load += loads;
+}
+
 // ---------------------------------------------------------------------------
 // beam_size = 1, packed lanes.  A wave owns W sentences and walks their end
 // positions in lockstep; at each position the candidates of all W sentences
@@ -738,14 +837,7 @@ lt_viterbi_pk(DecodeParams p) {
     r.n = (uint32_t)nw; r.bp_lo = (uint32_t)bo; r.bp_hi = (uint32_t)(bo >> 32);
     r.in_lds = 0u;
     srec[wv][lane] = r;
-    const Cand b0 = load_cand(B, nbase);       // beam[0] = [BOS] (beam.py:21-23)
-    VEntry e0;
-    e0.score = 0.0; e0.f6 = b0.f6;
-    e0.jword = b0.word; e0.jtag = b0.tag; e0.jmorph = b0.morph;
-    e0.a8 = b0.morph;                          // (used only when BOS's tag is in C)
-    e0.meta = hyp_probe_bits(b0.mask, 0u, false) | (b0.mask & V_META_J);
-    e0.iword = 0; e0.depth = 0; e0.pad = 0;
-    R[lane][0] = e0;
+    R[lane][0] = v_bos(load_cand(B, nbase));  // beam[0] = [BOS] (beam.py:21-23)
   }
   if (lane < W) {
     amax[wv][0][lane] = 0ull; amax[wv][1][lane] = 0ull;
@@ -862,15 +954,7 @@ lt_viterbi_pk(DecodeParams p) {
     if (!skip0) {
       v1_second<NARROW>(P, h1, cur);
       const double tri = has_tri ? v1_sum(P.cf, P.pres, cur, h1) : 0.0;
-      if (COUNT) {
-        const bool has_i = h1.depth > 0;
-        const bool k_ctx = (cur.mask & F_CTX) != 0, j_ctx = (h1.meta & F_CTX) != 0;
-        const bool i_ctx = (h1.meta & V_ICTX) != 0;
-        ++cnt.exp;
-        cnt.tup += 6 + ((h1.meta & F_UNK) ? 1 : 0) + (has_i ? 1 : 0) + ((k_ctx && (j_ctx || (has_i && i_ctx))) ? 1 : 0);
-        cnt.probe += __builtin_popcount(need);
-        cnt.load += __builtin_popcount(P.gneed) + __builtin_popcount(P.need2);
-      }
+      if (COUNT) v_count(cnt, h1, cur, need, __builtin_popcount(P.gneed) + __builtin_popcount(P.need2));
       best_s = h1.score + increment(p, cur, tri, gn0);              // beam.py:115
     }
 
@@ -894,14 +978,7 @@ lt_viterbi_pk(DecodeParams p) {
       amin[wv][cb ^ 1][lane] = INV;
     }
     if (top && mgw == (uint32_t)mg) {            // the (round's) winner writes beam[e]
-      VEntry ne;                                 // Sequence.add (beam.py:112-116): wi = wj, wj = wk
-      ne.score = best_s; ne.f6 = cur.f6;
-      ne.jword = cur.word; ne.jtag = cur.tag; ne.jmorph = cur.morph;
-      ne.a8 = (cur.mask & F_CTX) ? cur.morph : h1.jmorph;
-      ne.meta = hyp_probe_bits(cur.mask, h1.meta, true) | (cur.mask & V_META_J);
-      if (COUNT) ne.meta |= (h1.meta & F_CTX) ? V_ICTX : 0u;
-      ne.iword = h1.jword; ne.depth = h1.depth + 1; ne.pad = 0;
-      R[msr][em9] = ne;
+      R[msr][em9] = v_grow<COUNT>(h1, cur, best_s);   // Sequence.add (beam.py:112-116)
       const uint32_t bpv = bp_pack(sr.a + (uint32_t)mg, (uint32_t)d0, 0u);
       if (e < BPL) {
         bpl[wv][msr][e] = bpv;
@@ -1023,7 +1100,7 @@ lt_beam_pk(DecodeParams p) {
   constexpr int LN = KTP + CH;                  // ranked list: running top-k + chunk
   static_assert(KTP % 4 == 0, "list alignment");
   constexpr int STAGE = 64;                     // candidate records staged per position
-  __shared__ Entry ring[WPB][RING][KT];
+  __shared__ VEntry ring[WPB][RING][KT];
   __shared__ int32_t cntl[WPB][RING];
   __shared__ uint4 stg[WPB][3 * 64];            // records of the current position
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][LN];
@@ -1053,19 +1130,14 @@ lt_beam_pk(DecodeParams p) {
   const int bstride = p.bp_stride;
   const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
-  Entry (&R)[RING][KT] = ring[wv];
+  VEntry (&R)[RING][KT] = ring[wv];
   int32_t* const cnt9 = cntl[wv];
   unsigned long long* const LK = lkey[wv];
   uint32_t* const LG = lgen[wv];
   Counts cnt;
 
   if (lane == 0) {                              // beam[0] = [BOS] (beam.py:21-23)
-    const Cand b0 = load_cand(B, nbase);
-    Entry e0;
-    e0.score = 0.0; e0.f6 = b0.f6;
-    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
-    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
-    R[0][0] = e0;
+    R[0][0] = v_bos(load_cand(B, nbase));
     cnt9[0] = 1;
   }
   // The next position's first 64 records (lane t holds 16 B chunks t,
@@ -1156,17 +1228,17 @@ lt_beam_pk(DecodeParams p) {
         }
         const int hb = act ? (e - d) % RING : 0;
         const int hr = act ? r : 0;
-        const Hyp h0 = read_entry(R[hb][hr]);
+        const VEntry h0 = R[hb][hr];
         // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
-        const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));
-        Probe<NARROW, true> P;
-        probe_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
+        const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));
+        BMProbe<NARROW> P;
+        const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
+        bm_issue<NARROW>(P, B, slots, seed, h0, c, need, aux);
         asm volatile("" ::: "memory");
-        const Hyp h1 = read_entry(R[hb][hr]);
+        const VEntry h1 = R[hb][hr];
         if (!skip) {
-          const double tri = has_tri ? (probe_second<NARROW>(P, B, slots, seed, aux, h1, c),
-                                         probe_finish<NARROW, COUNT, true>(P, h1, c, cnt)) : 0.0;
-          if (COUNT) ++cnt.exp;
+          const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
+          if (COUNT) v_count(cnt, h1, c, need, 2 * __builtin_popcount(P.gneed));
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
@@ -1300,7 +1372,7 @@ lt_beam_pk(DecodeParams p) {
     // for (and does not wait for the prefetch above).
     for (int w0 = 0; w0 < (BIG ? nrun : 1); w0 += 64) {   // one pass unless the beam exceeds 64
     const int wl = w0 + lane;                   // winner (rank) of this lane
-    Entry ne;
+    VEntry ne;
     uint32_t bpv = 0;
     const bool writer = wl < nrun;
     int wj = 0, wr = 0, wi = 0;
@@ -1309,11 +1381,7 @@ lt_beam_pk(DecodeParams p) {
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
-      const Entry& h = R[(e - d) % RING][wr];
-      ne.score = ord_score(LK[KTP - nrun + wl]); ne.f6 = c.f6;
-      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
-      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
-      ne.depth = h.depth + 1;
+      ne = v_grow<COUNT>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + wl]));
       bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
@@ -1342,7 +1410,7 @@ lt_beam_pk(DecodeParams p) {
       for (int j = 0; j < n; ++j) codes[j] = -1;
       continue;
     }
-    const Entry& f = R[n % RING][t];
+    const VEntry& f = R[n % RING][t];
     const int64_t o = (int64_t)s * k + t;
     p.out_score[o] = f.score + 0.0;
     p.out_len[o] = (int32_t)f.depth;
@@ -1398,7 +1466,7 @@ lt_beam_hw(DecodeParams p) {
   constexpr int STAGE = 64 / S;                 // records staged per group and position
   constexpr int CPG = 3 * STAGE;                // staged 16 B chunks per group
   static_assert(KT <= G && G >= MAX_SPAN + 1, "one writer lane per rank in a group; span starts fit a group");
-  __shared__ Entry ring[WPB][S][RING][KT];
+  __shared__ VEntry ring[WPB][S][RING][KT];
   __shared__ int32_t cntl[WPB][S][RING];
   __shared__ uint4 stg[WPB][3 * 64];            // group h's record r: chunks CPG h + 3r .. +2
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][S][LN];
@@ -1444,7 +1512,7 @@ lt_beam_hw(DecodeParams p) {
     nS[h] = __builtin_amdgcn_readlane(n, h * G);
   }
   const rsrc_t bpr = make_rsrc(p.bp, (uint64_t)p.bp_bytes);
-  Entry (*const R)[KT] = ring[wv][hf];
+  VEntry (*const R)[KT] = ring[wv][hf];
   int32_t* const cnt9 = cntl[wv][hf];
   unsigned long long* const LK = lkey[wv][hf];
   uint32_t* const LG = lgen[wv][hf];
@@ -1454,12 +1522,7 @@ lt_beam_hw(DecodeParams p) {
   auto hcount = [&](unsigned long long bal) { return __builtin_popcountll(bal & hmask); };
 
   if (hv && hl == 0) {                          // beam[0] = [BOS] (beam.py:21-23)
-    const Cand b0 = load_cand(B, nbase);
-    Entry e0;
-    e0.score = 0.0; e0.f6 = b0.f6;
-    e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
-    e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
-    R[0][0] = e0;
+    R[0][0] = v_bos(load_cand(B, nbase));
     cnt9[0] = 1;
   }
   // next position's first STAGE records of every group (chunk c = 64 pl +
@@ -1566,15 +1629,14 @@ lt_beam_hw(DecodeParams p) {
         }
         const int hb = act ? (e - d) % RING : 0;
         const int hr = act ? r : 0;
-        const Hyp h0 = read_entry(R[hb][hr]);
-        const bool skip = !act || ((h0.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
-        Probe<NARROW, true> P;
-        probe_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? probe_need(h0, c) : 0u, aux);
+        const VEntry h0 = R[hb][hr];
+        const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
+        BMProbe<NARROW> P;
+        bm_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u, aux);
         asm volatile("" ::: "memory");
-        const Hyp h1 = read_entry(R[hb][hr]);
+        const VEntry h1 = R[hb][hr];
         if (!skip) {
-          const double tri = has_tri ? (probe_second<NARROW>(P, B, slots, seed, aux, h1, c),
-                                         probe_finish<NARROW, false, true>(P, h1, c, cnt)) : 0.0;
+          const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
@@ -1672,7 +1734,7 @@ lt_beam_hw(DecodeParams p) {
     prefetch(e + 1, ss[MAX_SPAN]);              // after the position's last load wait
 
     // beam[e] of each half (Sequence.add, beam.py:112-116)
-    Entry ne;
+    VEntry ne;
     uint32_t bpv = 0;
     const bool writer = live && hl < nrun;
     int wj = 0, wr = 0, wi = 0;
@@ -1681,11 +1743,7 @@ lt_beam_hw(DecodeParams p) {
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
-      const Entry& h = R[(e - d) % RING][wr];
-      ne.score = ord_score(LK[KTP - nrun + hl]); ne.f6 = c.f6;
-      ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
-      ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
-      ne.depth = h.depth + 1;
+      ne = v_grow<false>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + hl]));
       bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
     };
     auto staged = [&](int r) {
@@ -1723,7 +1781,7 @@ lt_beam_hw(DecodeParams p) {
       int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
       for (int j = 0; j < n; ++j) codes[j] = -1;
     } else {
-      const Entry& f = R[n % RING][hl];
+      const VEntry& f = R[n % RING][hl];
       p.out_score[o] = f.score + 0.0;
       p.out_len[o] = (int32_t)f.depth;
       int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;

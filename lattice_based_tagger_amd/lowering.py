@@ -77,6 +77,20 @@ def node_mask_from_vocab(vm_word, vm_morph, vm_tag):
     return m
 
 
+# kinds of the scorers after the leading node-local ones (lt_batch_desc.term_kinds)
+KIND_TRI, KIND_NODE, KIND_EDGE = 0, 1, 2
+MAX_TERMS = 32
+
+
+class EdgeSequence:
+    """The hypothesis an ``edge_local`` plugin sees: its last word only
+    (the plugin declares that it reads nothing else of the Sequence)."""
+    __slots__ = ('sequences',)
+
+    def __init__(self, wj):
+        self.sequences = (wj,)
+
+
 NODE_LOCAL_SCORERS = ('RegularizationScore', 'MorphemePreferenceScore',
                       'WordPreferenceScore')
 TRIGRAM_SCORER = 'SimpleTrigramFeatureScore'
@@ -94,7 +108,12 @@ class LoweredModel:
 
     Attributes
     ----------
-    pre_funcs, post_funcs : node-local plugins before / after the trigram
+    pre_funcs : the leading node-local plugins (summed per node on the host)
+    plan : [(kind, func)] every later scorer in constructor order, kind
+           KIND_TRI (the trigram), KIND_NODE (a node-local plugin: a
+           node_post row) or KIND_EDGE (an ``edge_local`` plugin: an edge_val
+           row, one value per lattice edge)
+    post_funcs, edge_funcs : the KIND_NODE / KIND_EDGE plugins of ``plan``
     trigram : the SimpleTrigramFeatureScore or None
     vocab : dict value -> id (1-based) over every key component
     vmask : uint32[len(vocab)+1] key-slot bits per id
@@ -108,7 +127,8 @@ class LoweredModel:
         if not hasattr(score_functions, 'funcs'):
             raise NotImplementedError(
                 'beam_search expects a BeamScoreFunctions composite')
-        self.pre_funcs, self.post_funcs = [], []
+        self.pre_funcs, self.post_funcs, self.edge_funcs = [], [], []
+        self.plan = []
         self.trigram = None
         for f in funcs:
             name = type(f).__name__
@@ -116,13 +136,25 @@ class LoweredModel:
                 if self.trigram is not None:
                     raise NotImplementedError('at most one SimpleTrigramFeatureScore is supported')
                 self.trigram = f
+                self.plan.append((KIND_TRI, f))
             elif name in NODE_LOCAL_SCORERS or getattr(f, 'node_local', False) is True:
-                (self.post_funcs if self.trigram is not None else self.pre_funcs).append(f)
+                if self.plan:
+                    self.plan.append((KIND_NODE, f))
+                    self.post_funcs.append(f)
+                else:
+                    self.pre_funcs.append(f)
+            elif getattr(f, 'edge_local', False) is True:
+                # reads only seq.sequences[-1] and word_k: one value per lattice
+                # edge (wj, wk), evaluated on the host
+                self.plan.append((KIND_EDGE, f))
+                self.edge_funcs.append(f)
             else:
                 raise NotImplementedError(
                     'scorer %s has no device lowering (supported: %s, %s, and any '
-                    'BeamScoreFunction that declares node_local = True)'
+                    'BeamScoreFunction that declares node_local = True or edge_local = True)'
                     % (name, ', '.join(NODE_LOCAL_SCORERS), TRIGRAM_SCORER))
+        if len(self.plan) > MAX_TERMS:
+            raise NotImplementedError('more than %d scorers after the leading node-local ones' % MAX_TERMS)
         self.vocab = {}
         self.vmask = np.zeros(1, dtype=np.uint32)
         self.keys = np.zeros((0, 4), dtype=np.uint32)
@@ -141,6 +173,15 @@ class LoweredModel:
     @property
     def n_post(self):
         return len(self.post_funcs)
+
+    @property
+    def n_edge(self):
+        return len(self.edge_funcs)
+
+    @property
+    def term_kinds(self):
+        """The plan's kinds, 2 bits per term (lt_batch_desc.term_kinds)."""
+        return sum(kind << (2 * t) for t, (kind, _) in enumerate(self.plan))
 
     @property
     def has_trigram(self):
@@ -215,6 +256,13 @@ class LoweredModel:
         for f in self.pre_funcs:
             pre = pre + f.score(None, w)
         return pre, [f.score(None, w) for f in self.post_funcs]
+
+    def edge_terms(self, wj, wk):
+        """[value...] of the edge_local plugins for appending ``wk`` to a
+        hypothesis whose last word is ``wj`` (score_funcs.py:50-54 calls
+        ``f(seq, wk)``; such a plugin reads only ``seq.sequences[-1]``)."""
+        seq = EdgeSequence(wj)
+        return [f.score(seq, wk) for f in self.edge_funcs]
 
     def node_local_features(self, w, is_unk):
         """Coefficients (or None) of feature classes 4, 5 and 6 for node w."""
