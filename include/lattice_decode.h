@@ -30,8 +30,9 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 3   /* 2: compact results (slabs), gathers of slabs;
-                              3: any max_len / beam (general kernel), lt_trace.exp_link */
+#define LT_ABI_VERSION 4   /* 2: compact results (slabs), gathers of slabs;
+                              3: any max_len / beam (general kernel), lt_trace.exp_link;
+                              4: edge terms (lt_batch_desc.n_edge ...) */
 #define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
 #define LT_MAX_BEAM 256    /* largest beam_size of the tuned kernels */
 /* Any other configuration -- max_len > 8 (span slots = max_len) or a beam
@@ -137,6 +138,25 @@ typedef struct {
   const double* node_f5;          /* coef of (5, word, tag0, is_l)    if flag */
   const double* node_f6;          /* coef of (6, min(8, len))         if flag */
   const double* node_post;        /* [n_post][n_nodes] or NULL */
+  /* Edge terms: scorers of (wj, wk) -- BeamScoreFunction plugins that read
+   * only seq.sequences[-1] and word_k (score_funcs.py:7-15, 50-54), one value
+   * per lattice edge.  n_edge = 0: none (the fields below are ignored and the
+   * increment is node_pre + trigram + node_post..., as before).  Otherwise
+   * the increment (score_funcs.py:50-54) is ((node_pre + t_0) + t_1) + ...
+   * over the n_terms terms that follow the leading node-local ones, in
+   * constructor order; term_kinds holds 2 bits per term: 0 the trigram,
+   * 1 the next node_post row, 2 the next edge_val row.  The predecessors
+   * of a node of span (b, e) are the local nodes of end position b (BOS for
+   * b = 0): the value of predecessor local node j is
+   * edge_val[t * n_edges + node_edge_base[node] + j], inside its sentence's
+   * block [sent_edge_off[s], sent_edge_off[s+1]). */
+  int32_t n_edge;
+  int32_t n_terms;                /* <= 32 */
+  uint64_t term_kinds;
+  int64_t n_edges;
+  const int64_t* sent_edge_off;   /* [n_sent+1] */
+  const int64_t* node_edge_base;  /* [n_nodes] */
+  const double* edge_val;         /* [n_edge][n_edges] */
 } lt_batch_desc;
 
 /* Copies the batch to the device (H2D) and allocates result buffers for

@@ -13,7 +13,7 @@ import numpy as np
 from ._build import LIB
 
 LT_OK = 0
-ABI_VERSION = 3           # include/lattice_decode.h LT_ABI_VERSION
+ABI_VERSION = 4           # include/lattice_decode.h LT_ABI_VERSION
 LT_MAX_BEAM = 256          # tuned kernels (lattice_decode.h)
 LT_MAX_BEAM_ANY = 1 << 20  # the general kernel lt_beam_wide
 LT_EUNSUPPORTED = -4
@@ -51,7 +51,10 @@ class BatchDesc(C.Structure):
                 ('sent_span_off', C.c_void_p), ('span_start', C.c_void_p),
                 ('node_word', C.c_void_p), ('node_morph0', C.c_void_p), ('node_tag', C.c_void_p),
                 ('node_mask', C.c_void_p), ('node_pre', C.c_void_p), ('node_f4', C.c_void_p),
-                ('node_f5', C.c_void_p), ('node_f6', C.c_void_p), ('node_post', C.c_void_p)]
+                ('node_f5', C.c_void_p), ('node_f6', C.c_void_p), ('node_post', C.c_void_p),
+                ('n_edge', C.c_int32), ('n_terms', C.c_int32), ('term_kinds', C.c_uint64),
+                ('n_edges', C.c_int64), ('sent_edge_off', C.c_void_p), ('node_edge_base', C.c_void_p),
+                ('edge_val', C.c_void_p)]
 
 
 class Result(C.Structure):
@@ -369,10 +372,20 @@ class DeviceBatch:
         self._span_start, self._span_off = arr['span_start'], arr['sent_span_off']
         self.cum_n = np.zeros(self.n_sent + 1, dtype=np.int64)
         np.cumsum(self.sent_n, out=self.cum_n[1:])
+        n_edge = int(getattr(packed, 'edge_terms', 0))
+        edges = (None, None, None)
+        if n_edge:                   # edge_local plugins (lowering.KIND_EDGE)
+            edges = (np.ascontiguousarray(packed.sent_edge_off, dtype=np.int64),
+                     np.ascontiguousarray(packed.node_edge_base, dtype=np.int64),
+                     np.ascontiguousarray(packed.edge_val, dtype=np.float64))
+        self._keep = (post,) + edges
         desc = BatchDesc(
             self.n_sent, int(packed.max_len), n_post, int(packed.has_trigram),
             int(arr['node_word'].shape[0]), int(arr['span_start'].shape[0]),
-            *[_ptr(arr[f]) for f in self.FIELDS], _ptr(post))
+            *[_ptr(arr[f]) for f in self.FIELDS], _ptr(post),
+            n_edge, int(getattr(packed, 'n_terms', 0)) if n_edge else 0,
+            int(getattr(packed, 'term_kinds', 0)) if n_edge else 0,
+            int(edges[2].shape[1]) if n_edge else 0, *[_ptr(x) for x in edges])
         h = C.c_void_p()
         check(ctx._lib.lt_batch_create(ctx.handle, C.byref(desc), int(max_k), C.byref(h)))
         self.handle = h

@@ -358,17 +358,22 @@ _TRI_LOCAL = F_HAS4 | F_HAS5          # a class-4/5 feature of wk: the trigram s
 def path_score_type(model, path):
     """Type of the reference score of ``path`` (BOS, words...; no EOS) under
     the lowered composite: the increments' values replayed on the host
-    (node-local scorers evaluated, trigram presence from the encoder)."""
-    funcs = model.pre_funcs + ([model.trigram] if model.trigram is not None else []) + model.post_funcs
+    (node-local and edge plugins evaluated, trigram presence from the
+    encoder), in constructor order (score_funcs.py:50-54)."""
+    from .lowering import KIND_EDGE, EdgeSequence
     enc = model.trigram.encoder if model.trigram is not None else None
     acc = 0
     for q in range(1, len(path)):
         wk, wj = path[q], path[q - 1]
         wi = None if q == 1 else path[q - 2]
         inc = 0
-        for f in funcs:
+        for f in model.pre_funcs:
+            inc = inc + f.score(None, wk)
+        for kind, f in model.plan:
             if f is model.trigram:
                 inc = inc + (np.float64(0.0) if enc.encode_word(wi, wj, wk) else 0)
+            elif kind == KIND_EDGE:
+                inc = inc + f.score(EdgeSequence(wj), wk)
             else:
                 inc = inc + f.score(None, wk)
         acc = acc + inc

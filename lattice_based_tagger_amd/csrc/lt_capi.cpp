@@ -525,6 +525,25 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
                          !d->node_pre || !d->node_f4 || !d->node_f5 || !d->node_f6))
     return fail(LT_EINVAL, "batch: NULL node arrays");
   if (d->n_post > 0 && !d->node_post) return fail(LT_EINVAL, "batch: NULL node_post");
+  if (d->n_edge < 0) return fail(LT_EINVAL, "batch: negative n_edge");
+  if (d->n_edge > 0) {
+    // the term plan: every node_post row, every edge row and the trigram (when
+    // the batch has one) exactly once
+    if (d->n_terms < 1 || d->n_terms > 32) return fail(LT_EINVAL, "batch: n_terms %d not in 1..32", d->n_terms);
+    if (d->n_terms < 32 && (d->term_kinds >> (2 * d->n_terms)) != 0)
+      return fail(LT_EINVAL, "batch: term_kinds has bits past n_terms");
+    int kinds[4] = {0, 0, 0, 0};
+    for (int t = 0; t < d->n_terms; ++t) ++kinds[(d->term_kinds >> (2 * t)) & 3u];
+    if (kinds[3] || kinds[1] != d->n_post || kinds[2] != d->n_edge || kinds[0] != (d->has_trigram ? 1 : 0))
+      return fail(LT_EINVAL, "batch: term_kinds does not list the trigram, the %d node_post rows and the %d "
+                             "edge rows once each", d->n_post, d->n_edge);
+    if (!d->sent_edge_off || (d->n_nodes > 0 && !d->node_edge_base) || (d->n_edges > 0 && !d->edge_val))
+      return fail(LT_EINVAL, "batch: NULL edge arrays");
+    if (d->sent_edge_off[0] != 0 || d->sent_edge_off[d->n_sent] != d->n_edges || d->n_edges < 0)
+      return fail(LT_EINVAL, "batch: sent_edge_off must run from 0 to n_edges");
+    for (int32_t s = 0; s < d->n_sent; ++s)
+      if (d->sent_edge_off[s + 1] < d->sent_edge_off[s]) return fail(LT_EINVAL, "batch: sent_edge_off not monotone");
+  }
   if (d->n_span > 0 && !d->span_start) return fail(LT_EINVAL, "batch: NULL span_start");
   if (d->sent_node_off[0] != 0 || d->sent_span_off[0] != 0)
     return fail(LT_EINVAL, "batch: offsets must start at 0");
@@ -576,6 +595,18 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
             return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span (e=%lld,d=%lld) has no candidate", s, e, dd);
           if (dd > dmax && cnt != 0)
             return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span (e=%lld,d=%lld) is out of range", s, e, dd);
+          if (d->n_edge > 0 && cnt > 0) {
+            // the candidates' predecessors: the nodes of end position b (BOS
+            // for b = 0); their values must lie in the sentence's edge block
+            const int64_t b = e - dd;
+            const int64_t plo = b == 0 ? 0 : ss[(b - 1) * SS], phi = b == 0 ? 1 : ss[b * SS];
+            for (int32_t v = ss[idx]; v < ss[idx + 1]; ++v) {
+              const int64_t base = d->node_edge_base[d->sent_node_off[s] + v];
+              if (base + plo < d->sent_edge_off[s] || base + phi > d->sent_edge_off[s + 1])
+                return note(bad[t], s, LT_EINVAL, "batch: sentence %lld node %lld edge values outside the "
+                                                  "sentence's block%.0lld", s, v, 0);
+            }
+          }
         }
       }
     }
@@ -598,6 +629,10 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
   for (int64_t i = 0; i < (int64_t)d->n_post * d->n_nodes; ++i) {
     if (std::isnan(d->node_post[i])) return fail(LT_EUNSUPPORTED, "batch: NaN post term %lld", (long long)i);
     signs |= inf_sign_bits(d->node_post[i]);
+  }
+  for (int64_t i = 0; d->n_edge > 0 && i < (int64_t)d->n_edge * d->n_edges; ++i) {
+    if (std::isnan(d->edge_val[i])) return fail(LT_EUNSUPPORTED, "batch: NaN edge term %lld", (long long)i);
+    signs |= inf_sign_bits(d->edge_val[i]);
   }
   if (signs == 3)
     return fail(LT_EUNSUPPORTED, "batch: both +inf and -inf among the node score terms (their sum is a NaN, "
@@ -741,6 +776,9 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   b->max_len = d->max_len;
   b->n_post = d->n_post;
   b->has_tri = d->has_trigram ? 1 : 0;
+  b->n_edge = d->n_edge;
+  b->n_terms = d->n_edge ? d->n_terms : 0;
+  b->term_kinds = d->n_edge ? d->term_kinds : 0;
   b->max_k = max_k;
   b->n_nodes = d->n_nodes;
   b->n_span = d->n_span;
@@ -767,6 +805,10 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     pc.n_nodes = d->sent_node_off[s1] - pc.node0;
     pc.n_span = d->sent_span_off[s1] - pc.span0;
     pc.chars0 = cum_n[s0];
+    if (d->n_edge > 0) {
+      pc.edge0 = d->sent_edge_off[s0];
+      pc.n_edges = d->sent_edge_off[s1] - pc.edge0;
+    }
     order[q].resize(n);
     node_off[q].resize(n + 1);
     span_off[q].resize(n + 1);
@@ -792,16 +834,19 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   // the batch's buffers as offsets into one arena
   Carve cv;
   struct PieceOff {
-    size_t order, sent_n, node_off, span_off, bp_off, cum_n, span_start, nodes, post, bp;
+    size_t order, sent_n, node_off, span_off, bp_off, cum_n, span_start, nodes, post, bp, edge_base, edge_val;
   };
   std::vector<PieceOff> po(P);
   for (size_t q = 0; q < P; ++q) {
     const lt_piece& pc = b->pieces[q];
     const size_t n = (size_t)pc.n_sent;
+    const bool ed = d->n_edge > 0;
     po[q] = PieceOff{cv.dev(n * 4), cv.dev(n * 4), cv.dev((n + 1) * 8), cv.dev((n + 1) * 8),
                      cv.dev((n + 1) * 8), cv.dev((n + 1) * 8), cv.dev((size_t)pc.n_span * 4),
                      cv.dev((size_t)pc.n_nodes * sizeof(NodeRec)),
-                     cv.dev((size_t)d->n_post * (size_t)pc.n_nodes * 8), cv.dev((size_t)pc.bp_entries * 4)};
+                     cv.dev((size_t)d->n_post * (size_t)pc.n_nodes * 8), cv.dev((size_t)pc.bp_entries * 4),
+                     cv.dev(ed ? (size_t)pc.n_nodes * 8 : 0),
+                     cv.dev(ed ? (size_t)d->n_edge * (size_t)pc.n_edges * 8 : 0)};
   }
   const size_t o_sent_n = cv.dev((size_t)S * 4), o_cum_n = cv.dev(((size_t)S + 1) * 8);
   b->slab_cap = slab_layout(S, max_k, b->total_chars).capacity;
@@ -843,6 +888,8 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     pc.d_nodes = at<NodeRec>(D, po[q].nodes);
     pc.d_post = at<double>(D, po[q].post);
     pc.d_bp = at<uint32_t>(D, po[q].bp);
+    pc.d_edge_base = d->n_edge > 0 ? at<int64_t>(D, po[q].edge_base) : nullptr;
+    pc.d_edge_val = d->n_edge > 0 ? at<double>(D, po[q].edge_val) : nullptr;
   }
   b->d_sent_n = at<int32_t>(D, o_sent_n);
   b->d_cum_n = at<int64_t>(D, o_cum_n);
@@ -902,6 +949,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       }
     }
   }, 256);
+  std::vector<std::vector<int64_t>> edge_base_tmp(P);
   for (size_t q = 0; q < P; ++q) {
     const lt_piece& pc = b->pieces[q];
     const size_t n = (size_t)pc.n_sent;
@@ -915,6 +963,15 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     up(pc.d_nodes, recs + pc.node0, (size_t)pc.n_nodes);
     for (int32_t t = 0; t < d->n_post; ++t)
       up(pc.d_post + (size_t)t * pc.n_nodes, d->node_post + (size_t)t * d->n_nodes + pc.node0, (size_t)pc.n_nodes);
+    if (d->n_edge > 0) {
+      // bases rebased to the piece's edge block (host copy kept alive past the
+      // upload: the stream is synchronised below)
+      edge_base_tmp[q].resize((size_t)pc.n_nodes);
+      for (int64_t i = 0; i < pc.n_nodes; ++i) edge_base_tmp[q][(size_t)i] = d->node_edge_base[pc.node0 + i] - pc.edge0;
+      up(pc.d_edge_base, edge_base_tmp[q].data(), (size_t)pc.n_nodes);
+      for (int32_t t = 0; t < d->n_edge; ++t)
+        up(pc.d_edge_val + (size_t)t * pc.n_edges, d->edge_val + (size_t)t * d->n_edges + pc.edge0, (size_t)pc.n_edges);
+    }
   }
   if (e == hipSuccess) e = hipStreamSynchronize(stm);
   if (e != hipSuccess) {
@@ -979,6 +1036,9 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.has_tri = b->has_tri;
   p.max_len = b->max_len;
   p.n_post = b->n_post;
+  p.n_edge = b->n_edge;
+  p.n_terms = b->n_terms;
+  p.term_kinds = b->term_kinds;
   p.k = k;
   p.bp_stride = b->max_k;
   p.counters = c->d_counters;
@@ -999,6 +1059,9 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
   p.span_start = pc.d_span_start;
   p.nodes = pc.d_nodes;
   p.npost = pc.d_post;
+  p.n_edges = pc.n_edges;
+  p.edge_base = pc.d_edge_base;
+  p.edge_val = pc.d_edge_val;
   p.bp = pc.d_bp;
   p.bp_bytes = pc.bp_entries * 4;
   p.bp_off = pc.d_bp_off;

@@ -138,6 +138,7 @@ __device__ __forceinline__ Cand read_block(const uint4* wave_planes, int gbase, 
 struct Hyp {
   double score, f6;
   uint32_t jword, jmorph, jtag, jmask, iword, imorph, imask, depth;
+  uint32_t jnode;                 // local index of wj (edge terms)
 };
 
 template <int G>
@@ -456,11 +457,27 @@ __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_
   return probe_finish<NARROW, COUNT, false>(P, h, c, cnt);
 }
 
-// inc = ((0 + pre...) + tri) + post...   (score_funcs.py:50-54)
+// inc = ((0 + pre...) + tri) + post...   (score_funcs.py:50-54).  With edge
+// terms (p.n_edge > 0) the terms after `pre` follow the composite's order
+// (term_kinds): the trigram, node-local rows, and edge rows -- the value of the
+// edge from wj (local node jl) to the candidate gn.
 __device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c, double tri,
-                                            uint32_t gn) {
-  double inc = c.pre + tri;
-  for (int t = 0; t < p.n_post; ++t) inc += p.npost[(int64_t)t * p.n_nodes + gn];
+                                            uint32_t gn, uint32_t jl) {
+  if (p.n_edge == 0) {
+    double inc = c.pre + tri;
+    for (int t = 0; t < p.n_post; ++t) inc += p.npost[(int64_t)t * p.n_nodes + gn];
+    return inc;
+  }
+  double inc = c.pre;
+  int nd = 0, ne = 0;
+  for (int t = 0; t < p.n_terms; ++t) {
+    const uint32_t kind = (uint32_t)(p.term_kinds >> (2 * t)) & 3u;
+    double v;
+    if (kind == 0) v = tri;
+    else if (kind == 1) v = p.npost[(int64_t)(nd++) * p.n_nodes + gn];
+    else v = p.edge_val[(int64_t)(ne++) * p.n_edges + p.edge_base[gn] + jl];
+    inc += v;
+  }
   return inc;
 }
 
@@ -473,7 +490,7 @@ __device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c
 struct alignas(16) VEntry {
   double score, f6;             // f6: wj's class-6 coefficient (-0.0 when absent)
   uint32_t jword, jtag, a8, meta;
-  uint32_t iword, jmorph, depth, pad;
+  uint32_t iword, jmorph, depth, jnode;    // jnode: local index of wj (edge terms)
 };
 // meta: bits 0-5 the hypothesis' probe bits (hyp_probe_bits), wj's DI_7 /
 // DI_8 (bits 13-14, for the next hypothesis), wj's F_UNK / F_CTX / F_HAS6;
@@ -667,6 +684,9 @@ __device__ __forceinline__ bool bm_hit(const typename Tab<NARROW>::S& s, uint32_
   }
 }
 
+#ifndef BM_BRANCHY
+#define BM_BRANCHY 1
+#endif
 template <bool NARROW>
 __device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntry& h, const Cand& c) {
   const V1Keys K = v1_keys(h, c);
@@ -675,24 +695,27 @@ __device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntr
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     const bool n = (P.gneed >> q) & 1u;
-    const bool m1 = n & bm_hit<NARROW>(P.s1[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
-    const bool m2 = n & bm_hit<NARROW>(P.s2[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
-    cf[q] = m1 ? P.s1[q].coef : (m2 ? P.s2[q].coef : (q == 3 ? P.cf3 : -0.0));
-    pres |= (m1 | m2) ? 1u << q : 0u;
+    cf[q] = q == 3 ? P.cf3 : -0.0;
+    if (BM_BRANCHY ? n : true) {               // BM_BRANCHY: a class no lane needs is skipped
+      const bool m1 = n & bm_hit<NARROW>(P.s1[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
+      const bool m2 = n & bm_hit<NARROW>(P.s2[q], K.a[q], K.b[q], K.c[q], PCLS[q]);
+      cf[q] = m1 ? P.s1[q].coef : (m2 ? P.s2[q].coef : cf[q]);
+      pres |= (m1 | m2) ? 1u << q : 0u;
+    }
   }
   return v1_sum(cf, pres, c, h);
 }
 
 // Sequence.add into a ring entry (beam.py:112-116): wi = wj, wj = wk
 template <bool COUNT>
-__device__ __forceinline__ VEntry v_grow(const VEntry& h, const Cand& c, double score) {
+__device__ __forceinline__ VEntry v_grow(const VEntry& h, const Cand& c, double score, uint32_t cl) {
   VEntry ne;
   ne.score = score; ne.f6 = c.f6;
   ne.jword = c.word; ne.jtag = c.tag; ne.jmorph = c.morph;
   ne.a8 = (c.mask & F_CTX) ? c.morph : h.jmorph;
   ne.meta = hyp_probe_bits(c.mask, h.meta, true) | (c.mask & V_META_J);
   if (COUNT) ne.meta |= (h.meta & F_CTX) ? V_ICTX : 0u;
-  ne.iword = h.jword; ne.depth = h.depth + 1; ne.pad = 0;
+  ne.iword = h.jword; ne.depth = h.depth + 1; ne.jnode = cl;
   return ne;
 }
 // beam[0] = [BOS] (beam.py:21-23)
@@ -702,7 +725,7 @@ __device__ __forceinline__ VEntry v_bos(const Cand& b0) {
   e0.jword = b0.word; e0.jtag = b0.tag; e0.jmorph = b0.morph;
   e0.a8 = b0.morph;                          // (used only when BOS's tag is in C)
   e0.meta = hyp_probe_bits(b0.mask, 0u, false) | (b0.mask & V_META_J);
-  e0.iword = 0; e0.depth = 0; e0.pad = 0;
+  e0.iword = 0; e0.depth = 0; e0.jnode = 0;
   return e0;
 }
 // operation counts of one expansion (lt_count_ops)
@@ -955,7 +978,7 @@ lt_viterbi_pk(DecodeParams p) {
       v1_second<NARROW>(P, h1, cur);
       const double tri = has_tri ? v1_sum(P.cf, P.pres, cur, h1) : 0.0;
       if (COUNT) v_count(cnt, h1, cur, need, __builtin_popcount(P.gneed) + __builtin_popcount(P.need2));
-      best_s = h1.score + increment(p, cur, tri, gn0);              // beam.py:115
+      best_s = h1.score + increment(p, cur, tri, gn0, h1.jnode);              // beam.py:115
     }
 
     // per-sentence argmax over the rounds of e (beam.py:112-116): max score
@@ -978,7 +1001,7 @@ lt_viterbi_pk(DecodeParams p) {
       amin[wv][cb ^ 1][lane] = INV;
     }
     if (top && mgw == (uint32_t)mg) {            // the (round's) winner writes beam[e]
-      R[msr][em9] = v_grow<COUNT>(h1, cur, best_s);   // Sequence.add (beam.py:112-116)
+      R[msr][em9] = v_grow<COUNT>(h1, cur, best_s, sr.a + (uint32_t)mg);   // Sequence.add (beam.py:112-116)
       const uint32_t bpv = bp_pack(sr.a + (uint32_t)mg, (uint32_t)d0, 0u);
       if (e < BPL) {
         bpl[wv][msr][e] = bpv;
@@ -1045,10 +1068,12 @@ lt_viterbi_pk(DecodeParams p) {
 // ===========================================================================
 // beam_size 2..32
 // ===========================================================================
+// Hypothesis entry of the untuned kernels (general beam, trace)
 struct alignas(16) Entry {
   double score, f6;
   uint32_t jword, jmorph, jtag, jmask;
   uint32_t iword, imorph, imask, depth;
+  uint32_t jnode, pad0, pad1, pad2;
 };
 
 __device__ __forceinline__ Hyp read_entry(const Entry& e) {
@@ -1056,6 +1081,7 @@ __device__ __forceinline__ Hyp read_entry(const Entry& e) {
   h.score = e.score; h.f6 = e.f6;
   h.jword = e.jword; h.jmorph = e.jmorph; h.jtag = e.jtag; h.jmask = e.jmask;
   h.iword = e.iword; h.imorph = e.imorph; h.imask = e.imask; h.depth = e.depth;
+  h.jnode = e.jnode;
   return h;
 }
 
@@ -1239,7 +1265,7 @@ lt_beam_pk(DecodeParams p) {
         if (!skip) {
           const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
           if (COUNT) v_count(cnt, h1, c, need, 2 * __builtin_popcount(P.gneed));
-          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
+          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
         }
@@ -1381,7 +1407,7 @@ lt_beam_pk(DecodeParams p) {
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
-      ne = v_grow<COUNT>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + wl]));
+      ne = v_grow<COUNT>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + wl]), (uint32_t)wnode);
       bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
@@ -1637,7 +1663,7 @@ lt_beam_hw(DecodeParams p) {
         const VEntry h1 = R[hb][hr];
         if (!skip) {
           const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
-          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
+          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
         }
@@ -1743,7 +1769,7 @@ lt_beam_hw(DecodeParams p) {
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
-      ne = v_grow<false>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + hl]));
+      ne = v_grow<false>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + hl]), (uint32_t)wnode);
       bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
     };
     auto staged = [&](int r) {
@@ -1845,6 +1871,7 @@ __global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
   h.jword = cj.word; h.jmorph = cj.morph; h.jtag = cj.tag; h.jmask = cj.mask;
   h.iword = ci.word; h.imorph = ci.morph; h.imask = i >= 0 ? (ci.mask | F_WI) : 0u;
   h.depth = 0;
+  h.jnode = 0;
   Counts cnt;
   p.inc[w] = trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux);
 }
@@ -2001,6 +2028,7 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
     e0.score = 0.0; e0.f6 = b0.f6;
     e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
     e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+    e0.jnode = 0; e0.pad0 = e0.pad1 = e0.pad2 = 0;
     ent[0] = e0;
     t.beam_count[po] = 1;
     t.beam_gen[po * k] = 0u;
@@ -2027,7 +2055,7 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
           double sc = 0.0;
           if (!skip) {
             const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux) : 0.0;
-            sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);      // beam.py:115
+            sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode);      // beam.py:115
           }
           t.exp_score[xo + g] = sc;
           t.exp_node[xo + g] = wide ? (uint32_t)node : bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
@@ -2067,6 +2095,7 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
       ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
       ne.depth = h.depth + 1;
+      ne.jnode = (uint32_t)node; ne.pad0 = ne.pad1 = ne.pad2 = 0;
       ent[(int64_t)e * k + kept] = ne;
       t.beam_gen[(po + e) * k + kept] = bg;
     }
@@ -2158,6 +2187,7 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
       e0.score = 0.0; e0.f6 = b0.f6;
       e0.jword = b0.word; e0.jmorph = b0.morph; e0.jtag = b0.tag; e0.jmask = b0.mask;
       e0.iword = 0; e0.imorph = 0; e0.imask = 0; e0.depth = 0;
+      e0.jnode = 0; e0.pad0 = e0.pad1 = e0.pad2 = 0;
       R[0] = e0;
       cnt[0] = 1;
     }
@@ -2176,7 +2206,7 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
             const Cand c = load_cand(B, nbase + (uint32_t)node);
             if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;    // beam.py:43-45
             const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cn, aux) : 0.0;
-            const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node);   // beam.py:115
+            const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode);   // beam.py:115
             const WItem it{ord_key(sc), g, (uint32_t)node, (uint32_t)d, (uint32_t)r};
             if (hn < k) {
               H[hn] = it;
@@ -2205,6 +2235,7 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
         ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
         ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
         ne.depth = h.depth + 1;
+        ne.jnode = it.node; ne.pad0 = ne.pad1 = ne.pad2 = 0;
         R[(int64_t)es * k + t] = ne;
         bp[(int64_t)e * bstride + t] = bpw_pack(it.node, it.d, it.r);
       }

@@ -52,11 +52,16 @@ struct lt_piece {
   lt::NodeRec* d_nodes = nullptr;
   double* d_post = nullptr;
   uint32_t* d_bp = nullptr;
+  int64_t edge0 = 0, n_edges = 0;                // the piece's edge values (edge terms)
+  int64_t* d_edge_base = nullptr;                // [n_nodes], rebased to the piece
+  double* d_edge_val = nullptr;                  // [n_edge][n_edges]
 };
 
 struct lt_batch {
   lt_ctx* ctx = nullptr;
   int32_t n_sent = 0, max_len = 8, n_post = 0, has_tri = 0, max_k = 1;
+  int32_t n_edge = 0, n_terms = 0;    // edge terms (lt_batch_desc.n_edge)
+  uint64_t term_kinds = 0;
   int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
   int inf_signs = 0;                  // +inf (1) / -inf (2) among the node score terms
   int last_k = 0;

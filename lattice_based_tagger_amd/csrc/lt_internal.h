@@ -30,6 +30,13 @@ struct DecodeParams {
   const int32_t* span_start;
   const NodeRec* nodes;         // AoS node records; mask + span length bits (D_SHIFT)
   const double* npost;
+  // edge terms (lt_batch_desc.n_edge; 0 = none): increment = ((pre + t_0) + t_1)...
+  int32_t n_edge;
+  int32_t n_terms;
+  uint64_t term_kinds;          // 2 bits per term: 0 trigram, 1 npost row, 2 edge row
+  int64_t n_edges;
+  const int64_t* edge_base;     // [n_nodes]: value of predecessor local node j at edge_base[gn] + j
+  const double* edge_val;       // [n_edge][n_edges]
   // scratch + results
   uint32_t* bp;
   int64_t bp_bytes;             // bytes of bp (< 2^31: 32-bit buffer offsets)
@@ -127,7 +134,7 @@ hipError_t launch_slab_to_host(const void* slab, void* host, size_t capacity, hi
 // of every end position in generation order, and each position's beam.  One
 // thread per sentence over global memory; the same scoring code as the
 // decoders.  Positions of sentence s: pos_off[s] + e (e = 0..n_s).
-constexpr int TRACE_ENTRY_BYTES = 48;
+constexpr int TRACE_ENTRY_BYTES = 64;
 struct TraceParams {
   const int64_t* pos_off;       // [n_sent + 1]
   const int64_t* exp_off;       // [positions + 1]: expansion slots of position q: [exp_off[q], exp_off[q+1])
@@ -151,8 +158,8 @@ constexpr int LT_MAX_BEAM_COMPILED = 256;
 // tuned kernels' (backpointers of two words, bpw_pack).
 __host__ __device__ inline bool decode_is_wide(int max_len, int k) { return max_len > MAX_SPAN || k > LT_MAX_BEAM_COMPILED; }
 // Scratch of one lt_beam_wide thread: the beams of the last S + 1 end
-// positions (48 B entries), their sizes, and the selection heap of k items.
-constexpr int WIDE_ENTRY_BYTES = 48, WIDE_ITEM_BYTES = 24;
+// positions (64 B entries), their sizes, and the selection heap of k items.
+constexpr int WIDE_ENTRY_BYTES = 64, WIDE_ITEM_BYTES = 24;
 inline int64_t wide_scratch_bytes(int span_slots, int k) {
   const int64_t ring = (int64_t)(span_slots + 1) * k * WIDE_ENTRY_BYTES;
   const int64_t cnt = ((int64_t)(span_slots + 1) * 4 + 15) & ~(int64_t)15;

@@ -7,6 +7,8 @@ The reference scores a given path (e.g. a gold sequence for training) with
 
 * node-local scorers (`:62-63, 81-82, 96-97`): ``sum(score(None, w) for w in
   seq.sequences)`` -- every word, BOS and EOS included, left to right;
+* ``edge_local`` plugins: their own ``evaluate(seq)`` (user code, on the host),
+  entered as that scorer's value of the path;
 * ``SimpleTrigramFeatureScore`` (`:127-135`): replays the path with
   ``Sequence.add`` from ``Sequence([seq.sequences[0]], 0)``, skipping words
   tagged BOS/EOS; each increment is the trigram score of the word after its
@@ -26,7 +28,7 @@ import numpy as np
 
 from . import _capi
 from .beam import Decoder, lowered_model
-from .lowering import TRIGRAM_SCORER, PACKED_TRIGRAM_SCORER
+from .lowering import EdgeSequence, NODE_LOCAL_SCORERS, TRIGRAM_SCORER, PACKED_TRIGRAM_SCORER
 from .packer import node_record
 from .tagset import BOS, EOS
 
@@ -76,7 +78,13 @@ def evaluate_batch(sequences, score_functions, device=0):
             cols['f5'].append(0.0 if c5 is None else c5)
             cols['f6'].append(0.0 if c6 is None else c6)
             for t, f in enumerate(local):
-                terms[t].append(float(f.score(None, w)))
+                if getattr(f, 'edge_local', False) is True and type(f).__name__ not in NODE_LOCAL_SCORERS:
+                    # an edge plugin's own evaluate(seq) (user code, host), as one
+                    # value of the path: ((0 + E) + -0.0) + ... == E
+                    sq = seq if hasattr(seq, 'sequences') else EdgeSequence(None, words)
+                    terms[t].append(float(f.evaluate(sq)) if idx == 0 else -0.0)
+                else:
+                    terms[t].append(float(f.score(None, w)))
             if w.tag0 == BOS or w.tag0 == EOS:
                 cols['p1'].append(-2)
                 cols['p2'].append(-1)

@@ -87,8 +87,8 @@ class EdgeSequence:
     (the plugin declares that it reads nothing else of the Sequence)."""
     __slots__ = ('sequences',)
 
-    def __init__(self, wj):
-        self.sequences = (wj,)
+    def __init__(self, wj, path=None):
+        self.sequences = (wj,) if path is None else path
 
 
 NODE_LOCAL_SCORERS = ('RegularizationScore', 'MorphemePreferenceScore',

@@ -193,6 +193,8 @@ class NativePacker:
         c5w, c5t = _StrTable([k[0] for k in c5k]), _StrTable([k[1] for k in c5k])
         c5i = np.asarray([k[2] for k in c5k], dtype=np.int64)
         c5c = np.asarray(list(c5.values()), dtype=np.float64)
+        if getattr(model, 'edge_funcs', None):      # edge_local plugins: Python, per lattice edge
+            raise Unsupported('edge_local scorers are evaluated per edge in Python')
         # node-local scorers in constructor order
         funcs = list(model.pre_funcs) + list(model.post_funcs)
         kinds, reg, ptag, pkey, pscorer, pval = [], [], [], [], [], []

@@ -19,6 +19,13 @@ layout described in DESIGN.md §Data layout:
 * per node: interned ``word``/``morph0``/``tag0`` ids, the 21-bit
   mask/flag word (``lowering.py``), the node-local score terms and the
   coefficients of the node-local feature classes 4, 5 and 6.
+* with ``edge_local`` plugins (``lowering.KIND_EDGE``): one value per lattice
+  edge and plugin.  The hypotheses a candidate of span (b, e) extends end in
+  the candidates of end position b (beam.py:41: ``beam[b]``), or in BOS for
+  b = 0, so its predecessors are the contiguous local nodes
+  ``[first(b), first(b+1))``; its values sit at ``edge_val[t][base + j]`` for
+  predecessor local node j, ``node_edge_base = base`` (``sent_edge_off``
+  delimits each sentence's block).
 
 The packer never reorders candidates: duplicates, ``len != e-b`` nodes and
 nodes filed under a begin slot other than their ``b`` field are kept exactly
@@ -71,6 +78,30 @@ class PackedBatch:
     NODE_FIELDS = ('node_word', 'node_morph0', 'node_tag', 'node_mask', 'node_pre', 'node_f4',
                    'node_f5', 'node_f6')
 
+    @property
+    def n_edge(self):
+        return int(getattr(self, 'edge_terms', 0))
+
+    def _edges_of(self, out, node_sel, sent_sel):
+        """Edge arrays of a sub-batch: sentences ``sent_sel`` (their nodes
+        ``node_sel``), blocks rebuilt in the new order."""
+        out['edge_terms'] = self.n_edge
+        out['term_kinds'] = getattr(self, 'term_kinds', 0)
+        out['n_terms'] = getattr(self, 'n_terms', 0)
+        if not self.n_edge:
+            return
+        eoff = self.sent_edge_off
+        cnt = (eoff[1:] - eoff[:-1])[sent_sel]
+        new_off = np.zeros(len(cnt) + 1, dtype=np.int64)
+        np.cumsum(cnt, out=new_off[1:])
+        seg = np.repeat(np.arange(len(cnt), dtype=np.int64), cnt)
+        ei = eoff[:-1][sent_sel][seg] + (np.arange(int(new_off[-1]), dtype=np.int64) - new_off[seg])
+        out['edge_val'] = self.edge_val[:, ei]
+        out['sent_edge_off'] = new_off
+        nodes_per = np.diff(self.sent_node_off)[sent_sel]
+        nseg = np.repeat(np.arange(len(cnt), dtype=np.int64), nodes_per)
+        out['node_edge_base'] = self.node_edge_base[node_sel] - eoff[:-1][sent_sel][nseg] + new_off[nseg]
+
     def slice(self, s0, s1):
         """Sentences [s0, s1) as a batch of their own (views; offsets rebased)."""
         n0, n1 = int(self.sent_node_off[s0]), int(self.sent_node_off[s1])
@@ -83,6 +114,7 @@ class PackedBatch:
                    node_post=self.node_post[:, n0:n1] if self.n_post else np.zeros((0, n1 - n0)))
         for f in self.NODE_FIELDS:
             out[f] = getattr(self, f)[n0:n1]
+        self._edges_of(out, np.arange(n0, n1), np.arange(s0, s1))
         return PackedBatch(**out)
 
     # backpointer bytes of one launch: lt_batch_create takes sum_s (n_s + 1) * k
@@ -131,6 +163,7 @@ class PackedBatch:
                    node_post=self.node_post[:, ni] if self.n_post else np.zeros((0, len(ni))))
         for f in self.NODE_FIELDS:
             out[f] = getattr(self, f)[ni]
+        self._edges_of(out, ni, order)
         return PackedBatch(**out)
 
 
@@ -179,6 +212,9 @@ def pack(sentences, model, max_len=8):
     max_len = effective_max_len(max_len, [len(chars) for _, chars in sentences])
     S = span_slots(max_len)
     n_post = model.n_post
+    n_edge = model.n_edge
+    edge_vals = [[] for _ in range(n_edge)]
+    edge_base, edge_off = [], [0]
 
     sent_n, node_off, span_off = [], [0], [0]
     span_start = []
@@ -222,6 +258,9 @@ def pack(sentences, model, max_len=8):
                     objs.append(w)
                     add_node(w)
         span_start.append(len(objs))
+        if n_edge:
+            _pack_edges(model, objs, span_start[len(span_start) - S * n - 1:], S, n,
+                        edge_vals, edge_base, edge_off)
         sent_n.append(n)
         node_off.append(base + len(objs))
         span_off.append(len(span_start))
@@ -239,5 +278,36 @@ def pack(sentences, model, max_len=8):
         node_mask=u32(masks), node_pre=f64(pre), node_f4=f64(f4),
         node_f5=f64(f5), node_f6=f64(f6),
         node_post=f64(post).reshape(n_post, -1) if n_post else np.zeros((0, len(words))),
+        edge_terms=n_edge, term_kinds=int(model.term_kinds), n_terms=len(model.plan),
     )
+    if n_edge:
+        batch.edge_val = f64(edge_vals).reshape(n_edge, -1)
+        batch.node_edge_base = np.asarray(edge_base, dtype=np.int64)
+        batch.sent_edge_off = np.asarray(edge_off, dtype=np.int64)
     return batch, node_objects
+
+
+def _pack_edges(model, objs, ss, S, n, edge_vals, edge_base, edge_off):
+    """Edge values of one sentence (``objs``: its local nodes; ``ss``: its
+    span_start entries, S per end position + the closing one): per local
+    node, in node order, one value per predecessor and edge plugin
+    (``model.edge_terms``).  Appends to the batch-wide lists."""
+    first = [0] + [ss[(e - 1) * S] for e in range(1, n + 1)] + [ss[S * n]]
+    pos = edge_off[-1]
+    edge_base.append(pos)                       # BOS: no predecessor
+    for e in range(1, n + 1):
+        for slot in range(S):
+            d = S - slot
+            b = e - d
+            lo_n, hi_n = ss[(e - 1) * S + slot], ss[(e - 1) * S + slot + 1]
+            if lo_n == hi_n:
+                continue
+            lo, hi = (0, 1) if b == 0 else (first[b], first[b + 1])
+            for k in range(lo_n, hi_n):
+                edge_base.append(pos - lo)
+                wk = objs[k]
+                for j in range(lo, hi):
+                    for t, v in enumerate(model.edge_terms(objs[j], wk)):
+                        edge_vals[t].append(float(v))
+                pos += hi - lo
+    edge_off.append(pos)

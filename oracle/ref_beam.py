@@ -112,7 +112,17 @@ def _scorer_value(func, path, wk):
         return numpy_pairwise_sum([float(coef[i]) for i in idx])
     if getattr(func, 'node_local', False) is True:           # a user plugin: the reference calls it
         return func.score(path, wk)                          # (score_funcs.py:50-54); it reads wk only
+    if getattr(func, 'edge_local', False) is True:           # a user plugin of (seq.sequences[-1], wk)
+        return func.score(_PathSeq(path), wk)
     raise TypeError('oracle has no restatement of scorer %r' % name)
+
+
+class _PathSeq:
+    """The hypothesis as a plugin sees it (``Sequence.sequences``)."""
+    __slots__ = ('sequences',)
+
+    def __init__(self, path):
+        self.sequences = path
 
 
 def composite_increment(funcs, path, wk):

@@ -31,14 +31,22 @@ from lattice_tagger.beam import (BeamScoreFunctions, RegularizationScore,  # noq
                                  SimpleTrigramFeatureScore)
 from lattice_tagger.features import SimpleTrigramEncoder        # noqa: E402
 from lattice_tagger.dictionary import Word                      # noqa: E402
+from lattice_tagger.beam.score_funcs import BeamScoreFunction   # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+import sys                                                      # noqa: E402
+sys.path.insert(0, os.path.join(HERE, '..'))
+from plugin_defs import edge_from_spec, make_edge_table_class   # noqa: E402
+
+EdgeTableScore = make_edge_table_class(BeamScoreFunction)       # the user plugin, inside the reference
 
 # (set, max chars, how many cases, beams): short sentences keep the dump small
 PICK = [('demo', 14, 4, (1, 3)), ('edge', 12, 14, (1, 2)), ('scorers', 30, 3, (1, 4)),
         ('synth', 40, 2, (1, 5)), ('dense', 30, 2, (2,)),
         # the general kernel's configurations: beams above 256, max_len > 8 and < 1
-        ('wide', 20, 11, (1, 300)), ('wide', 33, 3, (2,))]
+        ('wide', 20, 11, (1, 300)), ('wide', 33, 3, (2,)),
+        # user plugins of (wj, wk) (tests/plugin_defs.py)
+        ('plugins', 24, 4, (1, 3))]
 
 
 def ref_funcs(specs):
@@ -56,6 +64,8 @@ def ref_funcs(specs):
             dic = {tuple(f): i for i, f in enumerate(sp['features'])}
             coef = np.array([float.fromhex(c) for c in sp['coef']], dtype=np.float64)
             funcs.append(SimpleTrigramFeatureScore(SimpleTrigramEncoder(dic), coef))
+        elif t == 'EdgeTableScore':
+            funcs.append(edge_from_spec(EdgeTableScore, sp))
         else:
             raise ValueError(t)
     return BeamScoreFunctions(*funcs)

@@ -45,7 +45,12 @@ from lattice_tagger.dictionary import (Word, BaseMorphemeDictionary,  # noqa: E4
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, '..', '..'))
+sys.path.insert(0, os.path.join(HERE, '..'))
 from lattice_based_tagger_amd import synth                      # noqa: E402
+from lattice_tagger.beam.score_funcs import BeamScoreFunction as RefBeamScoreFunction  # noqa: E402
+from plugin_defs import make_edge_table_class, spec_of_edge     # noqa: E402
+
+EdgeTableScore = make_edge_table_class(RefBeamScoreFunction)   # a user plugin inside the reference
 
 BEAMS = (1, 5, 16)
 
@@ -71,6 +76,8 @@ def spec_of(func):
         return {'type': name, 'table': func.tag_to_morph}
     if name == 'WordPreferenceScore':
         return {'type': name, 'table': func.tag_to_word}
+    if name == 'EdgeTableScore':
+        return spec_of_edge(func)
     if name == 'SimpleTrigramFeatureScore':
         dic = func.encoder.feature_dic
         feats = [None] * len(dic)
@@ -176,7 +183,7 @@ def make_sentences(dic, n_sent, n_eojeol, seed):
 
 
 def main():
-    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'lookup', 'wide']
+    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'lookup', 'wide', 'plugins']
 
     if 'base' in sets:
         d = BaseMorphemeDictionary()
@@ -261,6 +268,65 @@ def main():
 
     if 'wide' in sets:
         dump_wide()
+
+    if 'plugins' in sets:
+        dump_plugins()
+
+
+def dump_plugins():
+    """User scoring plugins of the last two words (EdgeTableScore, an
+    ``edge_local`` BeamScoreFunction subclass defined in tests/plugin_defs.py)
+    inside the reference's own composite: before, between and after the
+    built-in scorers, int and float values (score types), alone (ties), and
+    at max_len 12 with a beam of 300 (the general kernel)."""
+    d = BaseMorphemeDictionary()
+    lk = MorphemeLookup(d, flatten=False)
+    lats = []
+    for s in make_sentences(d, 24, 12, seed=21):
+        _, bindex = sentence_lookup_as_begin_index(s, lk)
+        lats.append((bindex, s.replace(' ', '')))
+    raw = synth.make_lattices(16, seed=23, eojeols=6)
+    sm = synth.make_model(raw, seed=23, n_features=4000)
+    slats, sdic, scoef = synth.to_words(raw, sm, word_cls=Word)
+    enc, coef = trigram_from_paths(lats, seed=2)
+    rng = random.Random(7)
+    tags = sorted({w.tag0 for b, _ in lats + slats for ws in b for w in ws} | {'BOS', 'Unknown'})
+    mixed = {}
+    for a in tags:
+        for b in tags:
+            r = rng.random()
+            if r < 0.3:
+                mixed[(a, b)] = rng.choice([-2, -1, 1, 2, 3])
+            elif r < 0.8:
+                mixed[(a, b)] = round(rng.uniform(-1.5, 1.5), 3)
+    ints = {(a, b): rng.choice([-1, 0, 1, 2]) for a in tags for b in tags if rng.random() < 0.6}
+    morphs = sorted({w.morph0 for b, _ in lats + slats for ws in b for w in ws if w.morph0})
+    mtab = {}
+    for _ in range(4000):
+        mtab[(rng.choice(morphs + ['BOS']), rng.choice(morphs))] = rng.uniform(-1.0, 1.0)
+    reg = RegularizationScore()
+    tri = SimpleTrigramFeatureScore(enc, coef)
+    composites = {
+        'edge_mid': BeamScoreFunctions(reg, EdgeTableScore(mixed), tri),
+        'edge_first_last': BeamScoreFunctions(EdgeTableScore(mtab, 'morph0'), reg, tri,
+                                              WordPreferenceScore({'Noun': {'사람': 1.5}}),
+                                              EdgeTableScore(ints)),
+        'edge_only_int': BeamScoreFunctions(EdgeTableScore(ints)),
+        'edge_synth': BeamScoreFunctions(RegularizationScore(), EdgeTableScore(mixed),
+                                         SimpleTrigramFeatureScore(SimpleTrigramEncoder(sdic), scoef)),
+    }
+    models = {k: [spec_of(f) for f in v.funcs] for k, v in composites.items()}
+    cases = []
+    for name in ('edge_mid', 'edge_first_last', 'edge_only_int'):
+        for b, c in lats[:16]:
+            cases.append(case(b, c, name, composites[name], tag='plugins'))
+    for b, c in slats:
+        cases.append(case(b, c, 'edge_synth', composites['edge_synth'], tag='plugins_synth'))
+    for b, c in lats[16:20]:
+        cases.append(case(b, c, 'edge_mid', composites['edge_mid'], max_len=12, tag='plugins_wide',
+                          beams=(1, 300)))
+    cases.append(case([], '', 'edge_mid', composites['edge_mid'], tag='plugins_empty'))
+    dump('plugins', models, cases)
 
 
 def W(word, tag, b, e, length=None, is_l=False, morph0=None, morph1=None, tag1=None):

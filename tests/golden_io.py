@@ -10,9 +10,15 @@ import numpy as np
 from lattice_based_tagger_amd import (BeamScoreFunctions, RegularizationScore,
                                       MorphemePreferenceScore, WordPreferenceScore,
                                       SimpleTrigramFeatureScore, SimpleTrigramEncoder, Word)
+from lattice_based_tagger_amd.score_funcs import BeamScoreFunction
+from plugin_defs import edge_from_spec, make_edge_table_class
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 SETS = ('base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'wide')
+# sets whose composites hold user plugins (tests/plugin_defs.py), which the C
+# restatement (oracle/lt_oracle.c) does not evaluate
+PLUGIN_SETS = ('plugins',)
+EdgeTableScore = make_edge_table_class(BeamScoreFunction)
 
 
 def _tup(x):
@@ -34,6 +40,8 @@ def build_funcs(specs):
             dic = {_tup(f): i for i, f in enumerate(sp['features'])}
             coef = np.array([float.fromhex(c) for c in sp['coef']], dtype=np.float64)
             funcs.append(SimpleTrigramFeatureScore(SimpleTrigramEncoder(dic), coef))
+        elif t == 'EdgeTableScore':
+            funcs.append(edge_from_spec(EdgeTableScore, sp))
         else:
             raise ValueError(t)
     return BeamScoreFunctions(*funcs)
