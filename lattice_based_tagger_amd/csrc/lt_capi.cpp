@@ -695,6 +695,10 @@ static void batch_free(lt_batch* b) {
   for (auto& evs : b->ev_rd)
     for (hipEvent_t ev : evs)
       if (ev) (void)hipEventDestroy(ev);
+  for (lt_piece& pc : b->pieces) {               // the k=1 lane schedules (own allocations)
+    dfree(pc.d_sched);
+    dfree(pc.d_wave_off);
+  }
   arena_give(b->ctx, b->arena);
   delete b;
 }
@@ -1059,6 +1063,8 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
   p.span_start = pc.d_span_start;
   p.nodes = pc.d_nodes;
   p.npost = pc.d_post;
+  p.sched = pc.d_sched;
+  p.wave_off = pc.d_wave_off;
   p.n_edges = pc.n_edges;
   p.edge_base = pc.d_edge_base;
   p.edge_val = pc.d_edge_val;
@@ -1120,6 +1126,48 @@ static lt_status wide_scratch(lt_ctx* c, const lt_batch* b, int k, DecodeParams&
   return LT_OK;
 }
 
+// The k=1 lane schedule of every piece of b (lt_viterbi_pk reads which node
+// each lane scores at each macro-step): a static function of the lattice
+// shapes, built on the device at the first beam-1 decode of the batch and
+// kept with it.  Counting launch, exact allocation, filling launch.
+static lt_status k1_schedule(lt_ctx* c, lt_batch* b, const DecodeParams& base) {
+  for (size_t q = 0; q < b->pieces.size(); ++q) {
+    lt_piece& pc = b->pieces[q];
+    if (pc.sched_steps >= 0) continue;
+    DecodeParams p = base;
+    piece_params(b, q, 1, p);
+    const int waves = k1_waves(pc.n_sent);
+    std::vector<int32_t> steps((size_t)waves);
+    std::vector<int64_t> off((size_t)waves + 1, 0);
+    int32_t* d_steps = nullptr;
+    hipError_t e = hipMalloc((void**)&d_steps, std::max<size_t>(1, (size_t)waves * 4));
+    if (e == hipSuccess) e = launch_k1_sched_count(p, d_steps, c->stream);
+    if (e == hipSuccess && waves) e = hipMemcpyAsync(steps.data(), d_steps, (size_t)waves * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree(d_steps);
+    for (int w = 0; w < waves; ++w) off[(size_t)w + 1] = off[(size_t)w] + steps[(size_t)w];
+    if (e == hipSuccess) e = hipMalloc((void**)&pc.d_wave_off, ((size_t)waves + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&pc.d_sched, std::max<size_t>(1, (size_t)off[(size_t)waves] * 64 * 4));
+    if (e == hipSuccess) e = hipMemcpyAsync(pc.d_wave_off, off.data(), ((size_t)waves + 1) * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+      p.sched = pc.d_sched;
+      p.wave_off = pc.d_wave_off;
+      e = launch_k1_sched_fill(p, pc.d_wave_off, pc.d_sched, c->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);      // (off is on this stack)
+    if (e != hipSuccess) {
+      dfree(pc.d_sched);
+      dfree(pc.d_wave_off);
+      pc.d_sched = nullptr;
+      pc.d_wave_off = nullptr;
+      return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "decode: k=1 lane schedule: %s",
+                  hipGetErrorString(e));
+    }
+    pc.sched_steps = off[(size_t)waves];
+  }
+  return LT_OK;
+}
+
 lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
@@ -1127,6 +1175,7 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   HIP_TRY(hipSetDevice(c->device));
   const bool wide = decode_is_wide(b->max_len, k);
   if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
+  if (!wide && beam_template_for(k) == 1 && (st = k1_schedule(c, b, p)) != LT_OK) return st;
   if ((st = next_slot(c, b)) != LT_OK) return st;
   const int r = (int)(c->n_launch % lt_ctx::KRING);
   const size_t P = b->pieces.size();
@@ -1470,6 +1519,7 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
     return fail(LT_EUNSUPPORTED, "lt_count_ops: not collected by the general kernel (max_len > %d or beam > %d)",
                 MAX_SPAN, LT_MAX_BEAM_COMPILED);
   HIP_TRY(hipSetDevice(c->device));
+  if (beam_template_for(k) == 1 && (st = k1_schedule(c, b, p)) != LT_OK) return st;
   if ((st = next_slot(c, b)) != LT_OK) return st;
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
 #ifdef PK_PHASES

@@ -634,6 +634,9 @@ __device__ __forceinline__ double v1_sum(const double (&cf)[6], uint32_t pres6, 
   return t;
 }
 
+#ifndef BM_BRANCHY
+#define BM_BRANCHY 1                    // per-class checks exec-masked (A/B: 1 is faster at k = 2, 5, 16)
+#endif
 // The beam kernels' probes: both candidate slots of every needed probe in
 // one round trip (the flag-free copy of the table, lt_model.d_plain), checked
 // branch-free into cf[q] / pres as v1_check.
@@ -644,7 +647,11 @@ struct BMProbe {
   uint32_t gneed, pres3;
 };
 
-template <bool NARROW>
+// INIT: give the slots of lanes that load nothing a (frozen) value -- needed by
+// branch-free checks; with exec-masked checks it only shapes register
+// allocation (lt_beam_hw spills less with it, lt_beam_pk runs fewer copies
+// without it)
+template <bool NARROW, bool INIT = !BM_BRANCHY>
 __device__ __forceinline__ void bm_issue(BMProbe<NARROW>& P, const Bufs& B, uint32_t slots, uint32_t seed,
                                          const VEntry& h, const Cand& c, uint32_t need, const Aux& aux) {
   using T = Tab<NARROW>;
@@ -661,8 +668,10 @@ __device__ __forceinline__ void bm_issue(BMProbe<NARROW>& P, const Bufs& B, uint
   }
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
-    T::arbitrary(P.s1[q]);
-    T::arbitrary(P.s2[q]);
+    if (INIT) {
+      T::arbitrary(P.s1[q]);
+      T::arbitrary(P.s2[q]);
+    }
     if ((gneed >> q) & 1u) {
       P.s1[q] = T::load(B.tab, T::slot1(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
       P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
@@ -684,9 +693,6 @@ __device__ __forceinline__ bool bm_hit(const typename Tab<NARROW>::S& s, uint32_
   }
 }
 
-#ifndef BM_BRANCHY
-#define BM_BRANCHY 1
-#endif
 template <bool NARROW>
 __device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntry& h, const Cand& c) {
   const V1Keys K = v1_keys(h, c);
@@ -762,6 +768,8 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #define PK_WPB 4
 #endif
 constexpr int P_WPB = PK_WPB;           // waves per block
+// k=1 lane-schedule entries (lt_k1_sched)
+constexpr uint32_t K1_NODE = 0x03FFFFFFu, K1_IDLE = K1_NODE, K1_FIRST = 0x80000000u;
 
 // Stage the records of the wave's packed candidates (lane l's node gn, INV =
 // none) into wave_planes: the 3 x 64 chunks of 16 B form one stream in lane
@@ -806,15 +814,66 @@ __device__ __forceinline__ unsigned long long pk_stamp() {
 #define PK_STAMP(i) do { } while (0)
 #endif
 
-// per-sentence record of one end position (LDS): first candidate (global
-// node index), candidates, first candidate (local index)
-struct alignas(16) SegRec {
-  uint32_t nb, X, a, pad;
-};
 // per-sentence static record (LDS)
 struct alignas(16) SentRec {
-  uint32_t n, bp_lo, bp_hi, in_lds;
+  uint32_t n, bp_lo, bp_hi, nbase;
 };
+
+// ---------------------------------------------------------------------------
+// The k=1 lane schedule (a static function of the lattice shapes, built once
+// per batch on the device by lt_k1_sched, lt_batch's k1 schedule): the
+// candidates of the W sentences of a wave at end position e form one list in
+// sentence order (sentence w: the X_w candidates of its span starts
+// [A_e, A_{e+1}), generation order within); macro-step r of e covers list
+// entries [64r, 64r + 64).  Entry of lane l at a macro-step: the piece-global
+// node (bits 0-25; K1_IDLE = none), the lane's sentence w (bits 26-28), and
+// bit 31 = the first macro-step of a new end position.
+// ---------------------------------------------------------------------------
+template <int W, bool COUNT>
+__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, int32_t* steps, const int64_t* wave_off,
+                                                  uint32_t* sched) {
+  const int wave = blockIdx.x;
+  const int lane = (int)threadIdx.x;
+  const int slot0 = wave * W;
+  if (slot0 >= p.n_sent) return;
+  const bool own = lane < W && slot0 + lane < p.n_sent;
+  const int sid = own ? p.order[slot0 + lane] : 0;
+  const int nw = own ? p.sent_n[sid] : 0;
+  const uint32_t nbase = own ? (uint32_t)p.node_off[sid] : 0u;
+  const int32_t* const ssp = p.span_start + (own ? p.span_off[sid] : 0);
+  int nmax = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) nmax = max(nmax, __builtin_amdgcn_readlane(nw, w));
+  int64_t step = 0;
+  uint32_t* const out = COUNT ? nullptr : sched + wave_off[wave] * 64 + lane;
+  for (int e = 1; e <= nmax; ++e) {
+    const bool live = own && e <= nw;
+    const int lo = live ? ssp[(e - 1) * MAX_SPAN] : 0;     // first node of end e
+    const int X = live ? ssp[min(e, nw) * MAX_SPAN] - lo : 0;
+    int xs[W], st[W], run = 0;
+    uint32_t bw[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      xs[w] = __builtin_amdgcn_readlane(X, w);
+      bw[w] = (uint32_t)__builtin_amdgcn_readlane((int)(nbase + (uint32_t)lo), w);
+      st[w] = run;
+      run += xs[w];
+    }
+    const int rounds = max(1, (run + 63) >> 6);
+    if (!COUNT) {
+      for (int r = 0; r < rounds; ++r) {
+        const int f = 64 * r + lane;
+        uint32_t ent = K1_IDLE;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (f >= st[w] && f < st[w] + xs[w]) ent = (bw[w] + (uint32_t)(f - st[w])) | ((uint32_t)w << 26);
+        out[(step + r) * 64] = r == 0 ? (ent | K1_FIRST) : ent;
+      }
+    }
+    step += rounds;
+  }
+  if (COUNT && lane == 0) steps[wave] = (int32_t)step;
+}
 
 template <int W, bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(64 * P_WPB, (NARROW && W <= 6) ? PK_WAVES : 3)
@@ -823,7 +882,6 @@ lt_viterbi_pk(DecodeParams p) {
   __shared__ VEntry ring[P_WPB][W][RING];
   __shared__ uint32_t bpl[P_WPB][W][BPL];
   __shared__ uint4 stg[P_WPB][3 * 64];
-  __shared__ SegRec seg[P_WPB][2][W];
   __shared__ SentRec srec[P_WPB][W];
   __shared__ unsigned long long amax[P_WPB][2][W];
   __shared__ uint32_t amin[P_WPB][2][W];
@@ -832,7 +890,8 @@ lt_viterbi_pk(DecodeParams p) {
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
-  const int slot0 = (blockIdx.x * P_WPB + wv) * W;
+  const int wave = blockIdx.x * P_WPB + wv;
+  const int slot0 = wave * W;
   if (slot0 >= p.n_sent) return;                // whole wave
   const Bufs B = make_bufs(p);
   const uint32_t slots = p.slots, seed = p.seed;
@@ -845,7 +904,7 @@ lt_viterbi_pk(DecodeParams p) {
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long tstart = pk_stamp();
   unsigned long long tprev = tstart;
-  unsigned long long nsteps = 0;
+  unsigned long long nsteps_done = 0;
 #endif
 
   // lane w < W owns sentence w of the wave
@@ -853,12 +912,11 @@ lt_viterbi_pk(DecodeParams p) {
   const int sid = own ? p.order[slot0 + lane] : 0;
   const int nw = own ? p.sent_n[sid] : 0;
   const uint32_t nbase = own ? (uint32_t)p.node_off[sid] : 0u;
-  const int32_t* const ssp = p.span_start + (own ? p.span_off[sid] : 0);
   if (own) {
     const int64_t bo = p.bp_off[sid];
     SentRec r;
     r.n = (uint32_t)nw; r.bp_lo = (uint32_t)bo; r.bp_hi = (uint32_t)(bo >> 32);
-    r.in_lds = 0u;
+    r.nbase = nbase;
     srec[wv][lane] = r;
     R[lane][0] = v_bos(load_cand(B, nbase));  // beam[0] = [BOS] (beam.py:21-23)
   }
@@ -866,60 +924,33 @@ lt_viterbi_pk(DecodeParams p) {
     amax[wv][0][lane] = 0ull; amax[wv][1][lane] = 0ull;
     amin[wv][0][lane] = INV; amin[wv][1][lane] = INV;
   }
-  int nmax = 0;
-#pragma unroll
-  for (int w = 0; w < W; ++w) nmax = max(nmax, __builtin_amdgcn_readlane(nw, w));
-
-  // span starts A_e = ssp[(min(e, n+1) - 1) * 8] of the owned sentence
-  int A0 = own ? ssp[0] : 0;
-  int A1 = own ? ssp[min(1, nw) * 8] : 0;
-  int A2 = own ? ssp[min(2, nw) * 8] : 0;
-
-  // Lanes of round r of end position e: the candidates of the W sentences
-  // form one list in sentence order (sentence w: X_w = A_{e+1} - A_e of
-  // them, generation order within); round r covers entries [64r, 64r + 64).
-  // `fresh` writes the sentences' records seg[buf][w] (first round of e).
-  // Returns the list length T; sets this lane's sentence (W = idle),
-  // candidate index and global node (INV = none).
-  auto map_round = [&](int e, int r, int Ae, int Ae1, int buf, bool fresh, int& ms, int& mg,
-                       uint32_t& gnode) -> int {
-    const int X = (lane < W && e <= nw) ? Ae1 - Ae : 0;
-    const int f = 64 * r + lane;
-    int run = 0, sidx = 0, pst = 0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      run += __builtin_amdgcn_readlane(X, w);
-      if (f >= run) { sidx = w + 1; pst = run; }
-    }
-    if (fresh && lane < W) {
-      SegRec rec;
-      rec.nb = nbase + (uint32_t)Ae; rec.X = (uint32_t)X; rec.a = (uint32_t)Ae; rec.pad = 0u;
-      seg[wv][buf][lane] = rec;
-    }
-    ms = sidx;
-    mg = f - pst;
-    const SegRec rr = seg[wv][buf][sidx < W ? sidx : 0];   // in order behind the write above
-    gnode = sidx < W ? rr.nb + (uint32_t)mg : INV;
-    return run;
+  // this wave's macro-steps in the lane schedule
+  const int64_t soff = p.wave_off[wave];
+  const int nsteps = (int)(p.wave_off[wave + 1] - soff);
+  const uint32_t* const sch = p.sched + soff * 64 + lane;
+  auto node_of = [](uint32_t ent) -> uint32_t {
+    return (ent & K1_NODE) == K1_NODE ? INV : (ent & K1_NODE);
   };
+  uint32_t ent = sch[0];
+  dma_packed(B, node_of(ent), wst, lane);
 
-  int ms, mg;
-  uint32_t gn;
-  int rounds = (map_round(1, 0, A0, A1, 1, true, ms, mg, gn) + 63) >> 6;
-  dma_packed(B, gn, wst, lane);
-
-  // macro-steps (e, r): round r of end position e
-  int e = 1, r = 0, em9 = 1;
-  while (e <= nmax) {
+  int e = 0, em9 = 0;
+  for (int t = 0; t < nsteps; ++t) {
     PK_STAMP(0);                                 // [0] loop bookkeeping of the previous step
-    __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): staged records, span starts
+    __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): staged records, this step's schedule
     PK_STAMP(1);                                 // [1] wait for the staged records
+    // the next macro-step's schedule entry: arrives under this step's probes
+    const uint32_t ent1 = t + 1 < nsteps ? sch[(int64_t)(t + 1) * 64] : K1_IDLE;
+    const bool first = (__builtin_amdgcn_readfirstlane(ent) & K1_FIRST) != 0;   // a new end position
+    if (first) {
+      ++e;
+      em9 = em9 == RING - 1 ? 0 : em9 + 1;
+    }
     const int dmax = min(e, p.max_len);
     const int cb = e & 1;
-    const bool act = ms < W;
-    const int msr = act ? ms : 0;
-    const SegRec sr = seg[wv][cb][msr];
-    const uint32_t gn0 = gn;
+    const uint32_t gn0 = node_of(ent);
+    const bool act = gn0 != INV;
+    const int msr = act ? (int)((ent >> 26) & 7u) : 0;
     Cand cur;                                    // this lane's staged candidate
     {
       const uint4 q0 = wst[3 * lane], q1 = wst[3 * lane + 1], q2 = wst[3 * lane + 2];
@@ -933,38 +964,23 @@ lt_viterbi_pk(DecodeParams p) {
     const VEntry h0 = R[msr][act ? bm0 : 0];
     const bool skip0 = !act || ((h0.meta & F_UNK) && (cur.mask & F_UNK) && (d0 < dmax));   // beam.py:43-45
 
-    // next macro-step: another round of e, or round 0 of e + 1 (then also the
-    // span start two positions ahead for the owner lanes)
-    const bool last = r + 1 >= rounds;
-    int ms1 = W, mg1 = 0, nrounds = rounds;
-    uint32_t gn1 = INV;
-    // (loaded on every round: a conditional load would make its value a phi,
-    // and the copy at the join would wait for the load right away)
-    const int A3 = own ? ssp[min(e + 2, nw) * 8] : 0;
-    if (last) {
-      if (e < nmax) nrounds = (map_round(e + 1, 0, A1, A2, cb ^ 1, true, ms1, mg1, gn1) + 63) >> 6;
-    } else {
-      map_round(e, r + 1, A0, A1, cb, false, ms1, mg1, gn1);
-    }
-
     V1Probe<NARROW> P;
     const uint32_t need = (!skip0 && has_tri) ? (cur.mask & h0.meta & DQ_ALL) : 0u;
     v1_issue<NARROW>(P, B, slots, seed, h0, cur, need, aux);
 #ifdef PK_PHASES
-    PK_STAMP(2);                                 // [2] records/ring reads, mapping, primary issue
+    PK_STAMP(2);                                 // [2] records/ring reads, primary issue
     __builtin_amdgcn_s_waitcnt(0x0F70);
     PK_STAMP(3);                                 // [3] wait for the primary slots
 #endif
-    // primary slots back: hits, and the secondary loads of misses at flagged
-    // slots -- issued before the next macro-step's records are DMA'd, so the
-    // DMA's latency hides under theirs.  The DMA comes after every LDS read of
-    // this step's scoring: an LDS read issued after a buffer->LDS DMA waits
-    // for it (vmcnt).
+    // primary slots back: hits; the next macro-step's records DMA'd, then the
+    // secondary loads of misses at flagged slots (one wait covers both).  The
+    // DMA comes after every LDS read of this step's scoring: an LDS read
+    // issued after a buffer->LDS DMA waits for it (vmcnt).
     const VEntry h1 = R[msr][act ? bm0 : 0];
     v1_check<NARROW>(P, B, slots, seed, h1, cur, aux);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
-    dma_packed(B, gn1, wst, lane);
+    dma_packed(B, node_of(ent1), wst, lane);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     v1_issue2<NARROW>(P, B, slots, seed, h1, cur, aux);   // secondaries: their wait covers the DMA too
@@ -981,50 +997,44 @@ lt_viterbi_pk(DecodeParams p) {
       best_s = h1.score + increment(p, cur, tri, gn0, h1.jnode);              // beam.py:115
     }
 
-    // per-sentence argmax over the rounds of e (beam.py:112-116): max score
-    // key, then min generation index among the maxima.  A wave's LDS
-    // operations complete in order, so each read sees the updates issued
-    // before it.  A round that raises a sentence's maximum discards the
-    // earlier rounds' minimum (it belonged to a smaller key); ties with an
-    // earlier round keep it (earlier rounds hold smaller indices).
+    // per-sentence argmax over the macro-steps of e (beam.py:112-116): max
+    // score key, then the min node among the maxima -- a sentence's candidates
+    // of one end position are consecutive nodes in generation order, so the
+    // smallest node is the first generated.  A wave's LDS operations complete
+    // in order, so each read sees the updates issued before it.  A step that
+    // raises a sentence's maximum discards the earlier steps' minimum (it
+    // belonged to a smaller key); ties with an earlier step keep it (earlier
+    // steps hold smaller nodes).
     PK_STAMP(6);                                 // [6] numpy-order sum, increment
     const unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
-    const unsigned long long mprev = (key && r > 0) ? amax[wv][cb][msr] : 0ull;
+    const unsigned long long mprev = (key && !first) ? amax[wv][cb][msr] : 0ull;
     if (key) __hip_atomic_fetch_max(&amax[wv][cb][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const unsigned long long mk = key ? amax[wv][cb][msr] : 0ull;
     const bool top = key && key == mk;
     if (top && mk != mprev) amin[wv][cb][msr] = INV;
-    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], (uint32_t)mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], gn0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t mgw = top ? amin[wv][cb][msr] : INV;
     if (lane < W) {                              // reset the other parity for the next position
       amax[wv][cb ^ 1][lane] = 0ull;
       amin[wv][cb ^ 1][lane] = INV;
     }
-    if (top && mgw == (uint32_t)mg) {            // the (round's) winner writes beam[e]
-      R[msr][em9] = v_grow<COUNT>(h1, cur, best_s, sr.a + (uint32_t)mg);   // Sequence.add (beam.py:112-116)
-      const uint32_t bpv = bp_pack(sr.a + (uint32_t)mg, (uint32_t)d0, 0u);
+    if (top && mgw == gn0) {                     // the (step's) winner writes beam[e]
+      const SentRec si = srec[wv][msr];
+      const uint32_t local = gn0 - si.nbase;
+      R[msr][em9] = v_grow<COUNT>(h1, cur, best_s, local);   // Sequence.add (beam.py:112-116)
+      const uint32_t bpv = bp_pack(local, (uint32_t)d0, 0u);
       if (e < BPL) {
         bpl[wv][msr][e] = bpv;
       } else {                                   // positions past the LDS window (long sentences)
-        const SentRec si = srec[wv][msr];
         p.bp[(((int64_t)si.bp_hi << 32) | si.bp_lo) + (int64_t)e * bstride] = bpv;
       }
     }
     __builtin_amdgcn_wave_barrier();
     PK_STAMP(7);                                 // [7] argmax (LDS atomics), ring + backpointer write
 #ifdef PK_PHASES
-    ++nsteps;
+    ++nsteps_done;
 #endif
-    if (last) {
-      A0 = A1; A1 = A2; A2 = A3;
-      ++e;
-      r = 0;
-      em9 = em9 == RING - 1 ? 0 : em9 + 1;
-      rounds = nrounds;
-    } else {
-      ++r;
-    }
-    ms = ms1; mg = mg1; gn = gn1;
+    ent = ent1;
   }
 
   // matures = beam[n] + EOS (beam.py:59-61); backtrace, one owner lane per sentence
@@ -1058,7 +1068,7 @@ lt_viterbi_pk(DecodeParams p) {
   const unsigned long long tend = pk_stamp();
   if (lane == 0) {
     for (int i = 0; i < 8; ++i) atomicAdd(p.counters + 4 + i, ph[i]);
-    atomicAdd(p.counters + 12, nsteps);
+    atomicAdd(p.counters + 12, nsteps_done);
     atomicAdd(p.counters + 13, tend - tstart);
     atomicAdd(p.counters + 14, 1ull);
   }
@@ -1087,7 +1097,8 @@ __device__ __forceinline__ Hyp read_entry(const Entry& e) {
 
 // k=1 kernel: W = 6 sentences per wave (4 and 5 measured within 5 % at
 // 8K-32K sentences, slower at 64K)
-constexpr int P_W = 6;
+constexpr int P_W = K1_W;
+static_assert(P_W <= 8, "k=1 schedule entries hold the sentence in 3 bits");
 
 template <int W, bool NARROW, bool COUNT>
 hipError_t launch_pk(const DecodeParams& p, const Launch& L) {
@@ -1658,7 +1669,7 @@ lt_beam_hw(DecodeParams p) {
         const VEntry h0 = R[hb][hr];
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
         BMProbe<NARROW> P;
-        bm_issue<NARROW>(P, B, slots, seed, h0, c, (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u, aux);
+        bm_issue<NARROW, true>(P, B, slots, seed, h0, c, (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u, aux);
         asm volatile("" ::: "memory");
         const VEntry h1 = R[hb][hr];
         if (!skip) {
@@ -1980,6 +1991,20 @@ int beam_template_for(int k) {
   for (int kt = 2; kt <= LT_MAX_BEAM_COMPILED; kt *= 2)
     if (k <= kt) return kt;
   return -1;
+}
+
+hipError_t launch_k1_sched_count(const DecodeParams& p, int32_t* steps, hipStream_t st) {
+  const int waves = k1_waves(p.n_sent);
+  if (waves == 0) return hipSuccess;
+  hipLaunchKernelGGL((lt_k1_sched<P_W, true>), dim3(waves), dim3(64), 0, st, p, steps, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st) {
+  const int waves = k1_waves(p.n_sent);
+  if (waves == 0) return hipSuccess;
+  hipLaunchKernelGGL((lt_k1_sched<P_W, false>), dim3(waves), dim3(64), 0, st, p, nullptr, wave_off, sched);
+  return hipGetLastError();
 }
 
 hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipEvent_t e0, hipEvent_t e1) {

@@ -53,6 +53,10 @@ struct lt_piece {
   double* d_post = nullptr;
   uint32_t* d_bp = nullptr;
   int64_t edge0 = 0, n_edges = 0;                // the piece's edge values (edge terms)
+  // the k=1 lane schedule (built at the first beam-1 decode, lt_k1_schedule)
+  uint32_t* d_sched = nullptr;                   // [steps * 64]
+  int64_t* d_wave_off = nullptr;                 // [waves + 1]
+  int64_t sched_steps = -1;
   int64_t* d_edge_base = nullptr;                // [n_nodes], rebased to the piece
   double* d_edge_val = nullptr;                  // [n_edge][n_edges]
 };

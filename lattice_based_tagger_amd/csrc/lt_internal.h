@@ -37,6 +37,10 @@ struct DecodeParams {
   int64_t n_edges;
   const int64_t* edge_base;     // [n_nodes]: value of predecessor local node j at edge_base[gn] + j
   const double* edge_val;       // [n_edge][n_edges]
+  // k=1 lane schedule of the piece (launch_k1_sched): wave w's macro-steps are
+  // sched[wave_off[w] * 64 ..] (64 entries each)
+  const uint32_t* sched;
+  const int64_t* wave_off;
   // scratch + results
   uint32_t* bp;
   int64_t bp_bytes;             // bytes of bp (< 2^31: 32-bit buffer offsets)
@@ -172,5 +176,12 @@ const char* kernel_name_for(int k);
 // e0 / e1 (may be NULL): events recorded at the start / end of the kernel.
 hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipEvent_t e0 = nullptr,
                          hipEvent_t e1 = nullptr);
+// k=1 lane schedule of a piece (the kernel's sentence order, K1_W sentences
+// per wave): waves = k1_waves(p.n_sent); steps[w] = macro-steps of wave w
+// (count), then the schedule itself at wave_off (fill).
+constexpr int K1_W = 6;
+inline int k1_waves(int n_sent) { return (n_sent + K1_W - 1) / K1_W; }
+hipError_t launch_k1_sched_count(const DecodeParams& p, int32_t* steps, hipStream_t st);
+hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st);
 
 }  // namespace lt
