@@ -497,6 +497,11 @@ def main():
                 'traffic': traffic[0] if traffic else None,
                 'traffic_unit': 'HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)',
                 'traffic_source': traffic[1] if traffic else None,
+                # the three rates over the same kernel time: algorithmic bytes
+                # (frac: credits every feature tuple of the reference algorithm,
+                # most of which the node pre-filter never loads -- it can pass
+                # 1), bytes the kernel issues, and fabric bytes the counters saw
+                'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
                 'kernel': kernel,
                 'algorithmic_bytes_per_launch': B,
                 'kernel_bytes_per_launch': KB,
@@ -582,7 +587,8 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a):
                      'algorithmic_bytes_per_launch': B, 'kernel_bytes_per_launch': KB,
                      'kernel_bytes_frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                      'traffic': traffic[0] if traffic else None,
-                     'traffic_source': traffic[1] if traffic else None},
+                     'traffic_source': traffic[1] if traffic else None,
+                     'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None},
         'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                            'table_probes': probes, 'table_slot_loads': table_loads},
     }
