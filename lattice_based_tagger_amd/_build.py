@@ -23,6 +23,9 @@ HEADERS = ['lt_common.h', 'lt_internal.h', 'lt_error.h', 'lt_handles.h', 'lt_hos
            os.path.join('..', '..', 'include', 'lattice_pack.h'),
            os.path.join('..', '..', 'include', 'lattice_lookup.h')]
 
+PYOBJ_SRC = os.path.join(CSRC, 'lt_pyobj.c')
+PYOBJ = os.path.join(LIBDIR, '_ltpy.so')
+
 COMMON_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
                 '-Wall', '-Wno-unused-result', '-I' + os.path.join(HERE, '..', 'include')]
 
@@ -34,6 +37,24 @@ def _stale(target, deps):
     return any(os.path.getmtime(dp) > t for dp in deps)
 
 
+def build_pyobj(force=False, verbose=True):
+    """The CPython extension `_ltpy` (csrc/lt_pyobj.c: bulk Word / path
+    construction for the returned Sequences), compiled with the host C
+    compiler against this interpreter's headers."""
+    import sysconfig
+    os.makedirs(LIBDIR, exist_ok=True)
+    if not force and not _stale(PYOBJ, [PYOBJ_SRC, __file__]):
+        return PYOBJ
+    tmp = PYOBJ + '.tmp'
+    cmd = [os.environ.get('CC', 'gcc'), '-O2', '-Wall', '-shared', '-fPIC', '-fno-strict-aliasing',
+           '-I' + sysconfig.get_paths()['include'], PYOBJ_SRC, '-o', tmp]
+    if verbose:
+        print(' '.join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, PYOBJ)
+    return PYOBJ
+
+
 def build(force=False, verbose=True, defines=(), out=None):
     """Compile liblt.so if any source is newer than it.  Returns its path.
     ``defines``/``out``: an experiment build (e.g. ``('PK_WAVES=3',)``) to
@@ -41,6 +62,8 @@ def build(force=False, verbose=True, defines=(), out=None):
     os.makedirs(LIBDIR, exist_ok=True)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [__file__]
     lib = out or LIB
+    if out is None:
+        build_pyobj(force, verbose)
     if not force and not _stale(lib, deps):
         return lib
     objs = []

@@ -19,16 +19,13 @@ import weakref
 
 import numpy as np
 
-from . import _capi
+from . import _capi, _pyobj
 from .lowering import LoweredModel
 from .packer import pack
 from .tagset import Unk
 from .word import Word, bos_word, eos_word
 
-from functools import partial
-from itertools import repeat
 
-_new_word = partial(tuple.__new__, Word)      # Word from a 9-tuple, one C call
 
 __all__ = ['beam_search', 'beam_search_batch', 'Beam', 'Sequence', 'Decoder']
 
@@ -478,36 +475,32 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
     glob = packed.sent_node_off[seg // T] + local
     src = objs[0].src[glob]
     lat = objs[0].words
-    flat = np.empty(total, dtype=object)              # filled by two bulk assignments
+    ext = _pyobj.load()
+    flat = [None] * total
     dic = np.flatnonzero(src >= 0)
     sel = src[dic]
-    # native lattices build their Words in bulk; Word lists hand back the
+    # native lattices build their Words in C; Word lists hand back the
     # caller's own objects (as the reference's paths hold them)
-    words = lat.words_bulk(sel) if hasattr(lat, 'words_bulk') else [lat[i] for i in sel.tolist()]
-    if dic.size:                                       # (fromiter: Words are tuples, kept whole)
-        flat[dic] = np.fromiter(words, dtype=object, count=dic.size)
+    if dic.size:
+        if hasattr(lat, 'words_into'):
+            lat.words_into(flat, dic, sel)
+        else:
+            ext.scatter(flat, dic, [lat[i] for i in sel.tolist()])
     unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
     if unk.size:
         code = -2 - src[unk]
-        bl = (code >> 32).tolist()
-        dl = ((code & 0xFFFFFFFF) + 1).tolist()
-        subs = [chars_list[s][b:b + d] for b, d, s in zip(bl, dl, (seg[unk] // T).tolist())]
-        flat[unk] = np.fromiter(map(_new_word, zip(subs, subs, repeat(None), repeat(Unk), repeat(None), dl, bl,
-                                                   [b + d for b, d in zip(bl, dl)], repeat(False))),
-                                dtype=object, count=unk.size)
-    flat = flat.tolist()
+        chars = chars_list if type(chars_list) is list else list(chars_list)
+        ext.unknowns(Word, flat, unk, chars, seg[unk] // T, code >> 32, (code & 0xFFFFFFFF) + 1, Unk)
     # the sentinels are immutable tuples: one BOS, one EOS per sentence length
     bos, eos = bos_word(), {}
     vals = _typed_scores(model, packed, glob, seg, Lf, first, score[:, :T], n, T, bos, flat)
-    if T == 1:                                          # best path only (Tagger.tag): one comprehension
+    if T == 1:                                          # best path only (Tagger.tag): paths cut in C
         nl = n.tolist()
         for nch in set(nl):
             eos[nch] = eos_word(nch)
-        L1 = L[:, 0]
-        ends = np.cumsum(L1)
-        return [[Sequence([bos] + flat[a:z] + [eos[nch]], sc, 0)] if c else []
-                for a, z, nch, c, sc in zip((ends - L1).tolist(), ends.tolist(), nl,
-                                            (np.minimum(count, 1) > 0).tolist(), vals)]
+        paths = ext.paths(flat, np.cumsum(L[:, 0]), bos, [eos[nch] for nch in nl],
+                          (np.minimum(count, 1) > 0).view(np.uint8))
+        return [[Sequence(p, sc, 0)] if p is not None else [] for p, sc in zip(paths, vals)]
     out = []
     pos = 0
     cnt = np.minimum(count, T).tolist()

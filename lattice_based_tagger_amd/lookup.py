@@ -22,13 +22,12 @@ fall back to the Python lookup.
 """
 
 import ctypes as C
-import functools
 import random
 import sys
 
 import numpy as np
 
-from . import _capi
+from . import _capi, _pyobj
 from .native_packer import Strings, LatticeDesc, Unsupported, _StrTable, _ptr
 from .word import Word
 
@@ -276,9 +275,6 @@ def dictionary_fingerprint(dictionary):
     return tuple(parts)
 
 
-_new_word = functools.partial(tuple.__new__, Word)      # Word from a 9-tuple, one C call
-
-
 def _gather_strings(blob, off, idx):
     """Strings blob[off[i]:off[i+1]] for i in idx (UTF-8), via one gather and
     one decode: the selected byte ranges are joined with NUL separators
@@ -374,17 +370,23 @@ class NativeLattices:
         return self.word(int(i))
 
     def words_bulk(self, idx):
-        """[Word] of global node indices ``idx`` (int array).  Each string
-        field comes back dictionary-coded from one C call (the distinct
-        strings, decoded once, plus an int32 code per node), so a path's
-        repeated tags and words share str objects instead of being decoded
-        per node."""
+        """[Word] of global node indices ``idx`` (int array)."""
+        idx = np.ascontiguousarray(np.asarray(idx, dtype=np.int64))
+        out = [None] * idx.size
+        self.words_into(out, np.arange(idx.size, dtype=np.int64), idx)
+        return out
+
+    def words_into(self, out, pos, idx):
+        """out[pos[i]] = the Word of global node idx[i].  Each string field
+        comes back dictionary-coded from one C call (the distinct strings,
+        decoded once, plus an int32 code per node), so a path's repeated tags
+        and words share str objects; the Word tuples are built in C
+        (`_ltpy.words`, csrc/lt_pyobj.c)."""
         idx = np.ascontiguousarray(np.asarray(idx, dtype=np.int64))
         if idx.size == 0:
-            return []
-        fields = []
-        codes = np.empty(idx.size, dtype=np.int32)
-        lib = self.lib.held
+            return
+        uniqs, codes_all = [], []
+        lib = self.lib                      # (CDLL: the GIL is released during each call)
         # one buffer for the five fields' distinct strings (paths repeat few
         # of them); a field that needs more is coded again into a larger one
         full = max(int(lib.lt_lattices_field_bytes(self.handle, f)) for f in range(5)) + idx.size
@@ -392,6 +394,7 @@ class NativeLattices:
         buf = C.create_string_buffer(cap)
         used, n_u = C.c_int64(), C.c_int64()
         for f, name in enumerate(('word', 'morph0', 'morph1', 'tag0', 'tag1')):
+            codes = np.empty(idx.size, dtype=np.int32)
             st = lib.lt_lattices_strings_coded(self.handle, f, idx.ctypes.data, idx.size,
                                                codes.ctypes.data, buf, cap, C.byref(used), C.byref(n_u))
             if st == -1 and used.value > cap:                   # LT_EINVAL: too small
@@ -401,22 +404,19 @@ class NativeLattices:
                                                    codes.ctypes.data, buf, cap, C.byref(used), C.byref(n_u))
             if st == _capi.LT_EUNSUPPORTED:                     # a NUL inside a string: slice each
                 (blob, off), null = self._columns()[name]
-                vals = [blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()]
+                uniqs.append([blob[int(off[i]):int(off[i + 1])].decode('utf-8') for i in idx.tolist()])
+                codes = np.arange(idx.size, dtype=np.int32)
                 if null is not None:
-                    for j in np.flatnonzero(null[idx]).tolist():
-                        vals[j] = None
-                fields.append(vals)
+                    codes[null[idx] != 0] = -1
+                codes_all.append(codes)
                 continue
             _capi.check(st)
-            uniq = np.empty(n_u.value + 1, dtype=object)        # [-1] -> None
-            uniq[:n_u.value] = C.string_at(buf, used.value).decode('utf-8').split('\0')[:n_u.value]
-            fields.append(uniq[codes].tolist())
+            uniqs.append(C.string_at(buf, used.value).decode('utf-8').split('\0')[:n_u.value])
+            codes_all.append(codes)
         ints = self._int_columns()
-        lens = ints['len'][idx].tolist()
-        bs = ints['b'][idx].tolist()
-        es = ints['e'][idx].tolist()
-        isl = (ints['is_l'][idx] != 0).tolist()
-        return list(map(_new_word, zip(*fields, lens, bs, es, isl)))
+        isl = (ints['is_l'][idx] != 0).view(np.uint8)
+        _pyobj.load().words(Word, out, np.ascontiguousarray(pos, dtype=np.int64), tuple(uniqs), tuple(codes_all),
+                            (ints['len'][idx], ints['b'][idx], ints['e'][idx], isl))
 
     def empty(self, s):
         """True when sentence s has characters but no node: the reference's

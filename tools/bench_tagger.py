@@ -2,13 +2,16 @@
 """End-to-end Tagger throughput: text -> native lattices -> native packer ->
 HIP decode -> best Sequence objects, per phase.
 
-The base-dictionary sentences of tests/golden/lookup.json.gz (the golden
-'base' set's 101 sentences of 10-20 eojeols and 60 random ones, with the
-restricted reference dictionary that answers their lookups exactly) are
-replicated to --sentences; the model is the golden 'base' set's
-(RegularizationScore + SimpleTrigramFeatureScore).  One JSON line.
+Text (--text): 'unique' (default) -- every sentence a fresh seeded draw of
+10-20 eojeols from the 2,087 distinct eojeols of tests/golden/lookup.json.gz's
+base-dictionary sentences (the restricted reference dictionary stored there
+answers their lookups exactly, and a sentence's lattice is the concatenation
+of its eojeols' lattices, `lookup.py:344-369`); 'golden' -- the golden 'base'
+sentences of >= 10 eojeols replicated to --sentences (rounds 1-2).  The model
+is the golden 'base' set's (RegularizationScore + SimpleTrigramFeatureScore).
+One JSON line.
 
-    python tools/bench_tagger.py [--sentences 65536] [--k 1] [--threads 0] [--reps 3]
+    python tools/bench_tagger.py [--sentences 65536] [--k 1] [--text unique] [--threads 0] [--reps 3]
 """
 import argparse
 import gc
@@ -31,11 +34,28 @@ from lattice_based_tagger_amd.beam import Decoder, decode_batch, lowered_model  
 from lattice_based_tagger_amd.native_packer import packer_for  # noqa: E402
 
 
+def unique_text(golden, n, seed):
+    """n distinct sentences of 10-20 eojeols drawn from the golden eojeols."""
+    import numpy as np
+    pool = sorted({w for s in golden for w in s.split()})
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(10, 21, size=n)
+    picks = rng.integers(0, len(pool), size=int(lens.sum()))
+    out, at = [], 0
+    for m in lens:
+        out.append(' '.join(pool[i] for i in picks[at:at + m]))
+        at += m
+    assert len(set(out)) == n
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--sentences', type=int, default=65536)
     ap.add_argument('--k', type=int, default=1)
     ap.add_argument('--threads', type=int, default=0)
+    ap.add_argument('--text', choices=('unique', 'golden'), default='unique')
+    ap.add_argument('--seed', type=int, default=7)
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--chunk', type=int, default=0, help='Tagger.tag_batch pipeline chunk (0: default)')
     ap.add_argument('--profile', action='store_true', help='cProfile the tag_batch call (stderr)')
@@ -43,8 +63,11 @@ def main():
     a = ap.parse_args()
     entry = _fixture()['base']
     funcs = load('base')[0].funcs
-    base = [s for s in entry['sentences'] if len(s.split()) >= 10]
-    sents = (base * (a.sentences // len(base) + 1))[:a.sentences]
+    if a.text == 'golden':
+        base = [s for s in entry['sentences'] if len(s.split()) >= 10]
+        sents = (base * (a.sentences // len(base) + 1))[:a.sentences]
+    else:
+        sents = unique_text(entry['sentences'], a.sentences, a.seed)
     lex = fixture_lexicon(entry)
     tagger = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=lex, score_funcs=funcs)
     tagger.tag_batch(sents[:256], beam_size=a.k)                   # warm: model lowering, device model
@@ -103,7 +126,7 @@ def main():
         pstats.Stats(prof, stream=sys.stderr).sort_stats('tottime').print_stats(25)
     assert len(out) == len(sents) and all(o.score == m[0].score for o, m in zip(out, matures))
     line = {'metric': 'end-to-end Tagger.tag_batch sentences/s (text -> best Sequence)',
-            'sentences': len(sents), 'k': a.k, 'lattice_nodes': n_words,
+            'sentences': len(sents), 'k': a.k, 'text': a.text, 'distinct_sentences': len(set(sents)), 'lattice_nodes': n_words,
             'packed_nodes': int(packed.n_nodes),
             'chars_per_sentence': float(packed.sent_n.mean()),
             'phase_s': best, 'sentences_per_s': {p: len(sents) / v for p, v in best.items()},
