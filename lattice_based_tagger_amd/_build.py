@@ -69,7 +69,8 @@ def build(force=False, verbose=True, defines=(), out=None):
     objs = []
     for src in SOURCES:
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + '.o')
-        cmd = [HIPCC, '--offload-arch=' + ARCH] + COMMON_FLAGS + ['-D' + d for d in defines] + [
+        extra = os.environ.get('LT_EXTRA_FLAGS', '').split() if out is not None else []   # experiment builds only
+        cmd = [HIPCC, '--offload-arch=' + ARCH] + COMMON_FLAGS + extra + ['-D' + d for d in defines] + [
             '-c', os.path.join(CSRC, src), '-o', obj]
         if verbose:
             print(' '.join(cmd), file=sys.stderr)

@@ -1223,14 +1223,21 @@ lt_beam_pk(DecodeParams p) {
     const int M = pre[MAX_SPAN];
 
     // expansion g -> span slot j (d = 8 - j), hypothesis rank r, candidate i
-    auto decode = [&](int g, int& j, int& r, int& i) {
+    // (node ss[j] + i): j is the last slot whose prefix is <= g (pre is
+    // nondecreasing), its prefix, size and first node selected by the same
+    // compare
+    auto decode = [&](int g, int& j, int& r, int& i, int& sj) {
       j = 0;
-#pragma unroll
-      for (int q = 1; q < MAX_SPAN; ++q) j += (g >= pre[q]) ? 1 : 0;
       int pj = pre[0], m = ss[1] - ss[0];
+      sj = ss[0];
 #pragma unroll
-      for (int q = 1; q < MAX_SPAN; ++q)
-        if (j == q) { pj = pre[q]; m = ss[q + 1] - ss[q]; }
+      for (int q = 1; q < MAX_SPAN; ++q) {
+        const bool ge = g >= pre[q];
+        j = ge ? q : j;
+        pj = ge ? pre[q] : pj;
+        m = ge ? ss[q + 1] - ss[q] : m;
+        sj = ge ? ss[q] : sj;
+      }
       const int local = g - pj;
       // local / m through a float reciprocal (local < 2^24), corrected by one
       r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
@@ -1250,10 +1257,10 @@ lt_beam_pk(DecodeParams p) {
         if (base + 64 * t >= M) continue;        // uniform
         const int g = base + 64 * t + lane;
         const bool act = g < M;
-        int j = 0, r = 0, i = 0;
-        if (act) decode(g, j, r, i);
+        int j = 0, r = 0, i = 0, sj = 0;
+        if (act) decode(g, j, r, i, sj);
         const int d = MAX_SPAN - j;
-        const int node = ss[j] + i;
+        const int node = sj + i;
         const int so = node - A0;
         Cand c;
         if (!act) {
@@ -1330,22 +1337,21 @@ lt_beam_pk(DecodeParams p) {
           if (t < R0) mx = myk[t] > mx ? myk[t] : mx;
         // tau from the maxima's high 32 bits (a nonzero key's are nonzero):
         // the k-th largest h_k of them, tau = h_k << 32, still has at least k
-        // entries >= it, at half the compare work of 64-bit keys
-        uint32_t* const MX = reinterpret_cast<uint32_t*>(LK + KTP);   // chunk entries are in registers now
+        // entries >= it.  h_k by a most-significant-bit-first radix select
+        // over the wave: the largest v with #{lanes: mh >= v} >= k, one
+        // compare (ballot) and a scalar popcount per bit -- no LDS round trip
+        // and no 64-lane scan per lane.
         const uint32_t mh = (uint32_t)(mx >> 32);
-        MX[lane] = mh;
-        if (lane == 0) tkey[wv][0] = ~0ull;
-        int gtc = 0;
-#pragma unroll 4
-        for (int q = 0; q < 64; q += 4) {
-          const uint4 m4 = *reinterpret_cast<const uint4*>(&MX[q]);
-          gtc += (m4.x > mh ? 1 : 0) + (m4.y > mh ? 1 : 0) + (m4.z > mh ? 1 : 0) + (m4.w > mh ? 1 : 0);
-        }
         const int nz = __builtin_popcountll(__ballot(mx != 0ull));
-        if (mx != 0ull && gtc < k)
-          __hip_atomic_fetch_min(&tkey[wv][0], (unsigned long long)mh << 32, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        const unsigned long long tau = nz >= k ? tkey[wv][0] : 1ull;
+        uint32_t hk = 0u;
+        if (nz >= k) {
+#pragma unroll
+          for (int b = 31; b >= 0; --b) {
+            const uint32_t cand = hk | (1u << b);
+            if (__builtin_popcountll(__ballot(mh >= cand)) >= k) hk = cand;
+          }
+        }
+        const unsigned long long tau = nz >= k ? (unsigned long long)hk << 32 : 1ull;
         // compact the entries >= tau to the list head (in lane order per slot)
         int nc = 0;
         auto push = [&](unsigned long long key, uint32_t g) {
@@ -1412,9 +1418,9 @@ lt_beam_pk(DecodeParams p) {
     VEntry ne;
     uint32_t bpv = 0;
     const bool writer = wl < nrun;
-    int wj = 0, wr = 0, wi = 0;
-    if (writer) decode((int)LG[KTP - nrun + wl], wj, wr, wi);
-    const int wnode = ss[wj] + wi;
+    int wj = 0, wr = 0, wi = 0, wsj = 0;
+    if (writer) decode((int)LG[KTP - nrun + wl], wj, wr, wi, wsj);
+    const int wnode = wsj + wi;
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
@@ -1621,14 +1627,18 @@ lt_beam_hw(DecodeParams p) {
     const int M = pre[MAX_SPAN];                // this half's expansions
     const int Mmax = gmax(M);
 
-    auto decode = [&](int g, int& j, int& r, int& i) {
+    auto decode = [&](int g, int& j, int& r, int& i, int& sj) {     // (lt_beam_pk)
       j = 0;
-#pragma unroll
-      for (int q = 1; q < MAX_SPAN; ++q) j += (g >= pre[q]) ? 1 : 0;
       int pj = pre[0], m = ss[1] - ss[0];
+      sj = ss[0];
 #pragma unroll
-      for (int q = 1; q < MAX_SPAN; ++q)
-        if (j == q) { pj = pre[q]; m = ss[q + 1] - ss[q]; }
+      for (int q = 1; q < MAX_SPAN; ++q) {
+        const bool ge = g >= pre[q];
+        j = ge ? q : j;
+        pj = ge ? pre[q] : pj;
+        m = ge ? ss[q + 1] - ss[q] : m;
+        sj = ge ? ss[q] : sj;
+      }
       const int local = g - pj;
       r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
       i = local - r * m;
@@ -1647,10 +1657,10 @@ lt_beam_hw(DecodeParams p) {
         if (base + G * t >= Mmax) continue;      // uniform
         const int g = base + G * t + hl;
         const bool act = g < M;
-        int j = 0, r = 0, i = 0;
-        if (act) decode(g, j, r, i);
+        int j = 0, r = 0, i = 0, sj = 0;
+        if (act) decode(g, j, r, i, sj);
         const int d = MAX_SPAN - j;
-        const int node = ss[j] + i;
+        const int node = sj + i;
         const int so = node - A0;
         Cand c;
         if (!act) {
@@ -1774,9 +1784,9 @@ lt_beam_hw(DecodeParams p) {
     VEntry ne;
     uint32_t bpv = 0;
     const bool writer = live && hl < nrun;
-    int wj = 0, wr = 0, wi = 0;
-    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi);
-    const int wnode = ss[wj] + wi;
+    int wj = 0, wr = 0, wi = 0, wsj = 0;
+    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi, wsj);
+    const int wnode = wsj + wi;
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;

@@ -165,6 +165,109 @@ void utf8_append(std::string& out, uint32_t cp) {
   }
 }
 
+// Strict UTF-8 -> code points (false on malformed input).
+bool utf8_cps(std::string_view s, std::vector<uint32_t>& out) {
+  out.clear();
+  for (size_t i = 0; i < s.size();) {
+    const unsigned char c = (unsigned char)s[i];
+    uint32_t cp;
+    size_t n;
+    if (c < 0x80) { cp = c; n = 1; }
+    else if ((c >> 5) == 6) { cp = c & 0x1F; n = 2; }
+    else if ((c >> 4) == 14) { cp = c & 0x0F; n = 3; }
+    else if ((c >> 3) == 30) { cp = c & 0x07; n = 4; }
+    else return false;
+    if (i + n > s.size()) return false;
+    for (size_t k = 1; k < n; ++k) {
+      const unsigned char d = (unsigned char)s[i + k];
+      if ((d >> 6) != 2) return false;
+      cp = (cp << 6) | (d & 0x3F);
+    }
+    static const uint32_t lo[5] = {0, 0, 0x80, 0x800, 0x10000};
+    if (cp < lo[n] || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return false;
+    out.push_back(cp);
+    i += n;
+  }
+  return true;
+}
+
+// The vocabulary keyed by code points, for the synthesised Unknown nodes
+// (beam.py:36-38): their word is chars[b:e] of the sentence, so the packer
+// hashes the characters it already has -- every suffix ending at e in one
+// pass, last character first -- instead of encoding each span to UTF-8 and
+// hashing that.  A string's UTF-8 form and its code points are equal iff the
+// strings are (malformed vocabulary strings cannot equal a decoded sentence
+// and are left out).
+struct CpVocab {
+  struct E {
+    uint64_t h;                                  // 0: empty
+    uint32_t off, n;
+    const WordInfo* wi;
+  };
+  std::vector<uint32_t> pool;
+  std::vector<E> tab;
+  uint64_t mask = 0;
+  static constexpr uint64_t SEED = 0x2545F4914F6CDD1Dull;
+  static uint64_t step(uint64_t h, uint32_t cp) {
+    h = (h ^ cp) * 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 29);
+  }
+  static uint64_t fin(uint64_t h, uint32_t n) {
+    h ^= (uint64_t)n * 0xC2B2AE3D27D4EB4Full;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 32;
+    return h | 1ull;
+  }
+  static uint64_t hash(const uint32_t* s, uint32_t n) {     // last code point first
+    uint64_t h = SEED;
+    for (uint32_t i = n; i-- > 0;) h = step(h, s[i]);
+    return fin(h, n);
+  }
+  void build(const std::vector<std::pair<std::string_view, const WordInfo*>>& words) {
+    size_t cap = 16;
+    while (cap < 2 * words.size() + 16) cap <<= 1;
+    tab.assign(cap, E{0, 0, 0, nullptr});
+    mask = cap - 1;
+    std::vector<uint32_t> cps;
+    for (const auto& w : words) {
+      if (!utf8_cps(w.first, cps)) continue;
+      const uint64_t h = hash(cps.data(), (uint32_t)cps.size());
+      uint64_t i = h & mask;
+      while (tab[i].h) i = (i + 1) & mask;
+      tab[i] = E{h, (uint32_t)pool.size(), (uint32_t)cps.size(), w.second};
+      pool.insert(pool.end(), cps.begin(), cps.end());
+    }
+  }
+  const WordInfo* find(const uint32_t* s, uint32_t n, uint64_t h) const {
+    for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+      const E& e = tab[i];
+      if (e.h == 0) return nullptr;
+      if (e.h == h && e.n == n && std::equal(s, s + n, pool.data() + e.off)) return e.wi;
+    }
+  }
+};
+
+// coefficient by a small non-negative integer (class 4 / 6 lengths): a flat
+// array below SMALL, the map above
+struct LenCoef {
+  static constexpr int64_t SMALL = 64;
+  double v[SMALL];
+  bool has[SMALL] = {};
+  std::unordered_map<int64_t, double> big;
+  void put(int64_t k, double c) {                // first entry wins (emplace)
+    if (k >= 0 && k < SMALL) {
+      if (!has[k]) { has[k] = true; v[k] = c; }
+    } else {
+      big.emplace(k, c);
+    }
+  }
+  const double* get(int64_t k) const {
+    if (k >= 0 && k < SMALL) return has[k] ? &v[k] : nullptr;
+    auto it = big.find(k);
+    return it == big.end() ? nullptr : &it->second;
+  }
+};
+
 }  // namespace
 
 // One pack's output arrays, handed to the caller through lt_packed.owner
@@ -213,13 +316,15 @@ struct lt_packer {
   std::shared_ptr<PackPool> pool = std::make_shared<PackPool>();
   ViewMap<WordInfo> vocab;                          // vocabulary strings and class-5 words
   std::vector<uint32_t> vmask;
-  std::unordered_map<int64_t, double> c4, c6;
+  LenCoef c4, c6;
   std::vector<C5Entry> c5e;                         // grouped by word (WordInfo::c5_lo)
   int32_t n_local = 0, n_pre = 0;
   std::vector<int32_t> kind;
   std::vector<double> reg;                          // 3 per scorer
   std::vector<ViewMap<double>> pref;                // per scorer: (tag, key) -> value
   std::string kb;                                   // key buffer
+  CpVocab cpv;                                      // vocab by code points (Unknown nodes)
+  bool pref_unk = false;                            // a preference entry for tag 'Unknown'
 
   int32_t id_of(std::string_view s) const {
     const WordInfo* v = vocab.get(s);
@@ -239,8 +344,8 @@ lt_status lt_packer_create(const lt_packer_desc* d, lt_packer** out) {
     for (int64_t i = 0; i < d->vocab.n; ++i)
       if (!is_null(d->vocab, i)) p->vocab.put(str_at(d->vocab, i), WordInfo{d->vocab_id[i], 0, 0});
     p->vmask.assign(d->vmask, d->vmask + d->n_vmask);
-    for (int64_t i = 0; i < d->n4; ++i) p->c4.emplace(d->c4_len[i], d->c4_coef[i]);
-    for (int64_t i = 0; i < d->n6; ++i) p->c6.emplace(d->c6_len[i], d->c6_coef[i]);
+    for (int64_t i = 0; i < d->n4; ++i) p->c4.put(d->c4_len[i], d->c4_coef[i]);
+    for (int64_t i = 0; i < d->n6; ++i) p->c6.put(d->c6_len[i], d->c6_coef[i]);
     // class-5 entries grouped by word, in input order within a word (the
     // first of equal keys wins, as the Python dict the entries come from)
     std::vector<int64_t> c5_order((size_t)d->c5_word.n);
@@ -273,7 +378,12 @@ lt_status lt_packer_create(const lt_packer_desc* d, lt_packer** out) {
       }
       p->pref[(size_t)s].put(tuple_key(p->kb, str_at(d->pref_tag, i), str_at(d->pref_key, i)),
                              d->pref_value[i]);
+      if (str_at(d->pref_tag, i) == kUnk) p->pref_unk = true;
     }
+    std::vector<std::pair<std::string_view, const WordInfo*>> words;
+    for (const auto& e : p->vocab.tab)
+      if (e.h) words.emplace_back(std::string_view(e.s, (size_t)e.n), &e.v);
+    p->cpv.build(words);
   } catch (...) {
     delete p;
     return set_error(LT_ENOMEM, "lt_packer_create: out of memory");
@@ -393,8 +503,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       }
       return id;
     };
-    auto add_node = [&](int64_t x, const NodeView& w, int64_t src) {
-      const WordInfo* wi = p->vocab.get(w.word);
+    auto add_node_wi = [&](int64_t x, const NodeView& w, const WordInfo* wi, int64_t src) {
       const int32_t wid = wi ? wi->id : 0, tid = tag_id(w.tag0);
       const int32_t mid = w.morph0.data() == w.word.data() && w.morph0.size() == w.word.size()
                               ? wid : p->id_of(w.morph0);
@@ -403,7 +512,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       if (unk_node) m |= F_UNK;
       if (contextual(w.tag0)) m |= F_CTX;
       double f4 = 0.0, f5 = 0.0, f6 = 0.0;
-      if (auto it = p->c4.find(w.len); it != p->c4.end()) { m |= F_HAS4; f4 = it->second; }
+      if (const double* c = p->c4.get(w.len)) { m |= F_HAS4; f4 = *c; }
       if (wi) {                                          // (word, tag0, is_l) -> coef
         for (int32_t j = wi->c5_lo; j < wi->c5_lo + wi->c5_n; ++j) {
           const C5Entry& c = p->c5e[(size_t)j];
@@ -415,7 +524,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
         }
       }
       if (unk_node) {
-        if (auto it = p->c6.find(w.len < 8 ? w.len : 8); it != p->c6.end()) { m |= F_HAS6; f6 = it->second; }
+        if (const double* c = p->c6.get(w.len < 8 ? w.len : 8)) { m |= F_HAS6; f6 = *c; }
       }
       // node-local scorers in constructor order (lowering.node_terms)
       double pre = 0.0;
@@ -443,6 +552,12 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       q.node_f6[x] = f6;
       q.node_src[x] = src;
     };
+    auto add_node = [&](int64_t x, const NodeView& w, int64_t src) { add_node_wi(x, w, p->vocab.get(w.word), src); };
+    // Unknown nodes by code points (CpVocab) unless a preference scorer has an
+    // entry for the tag 'Unknown' (its value would depend on the string)
+    const bool fast_unk = !p->pref_unk;
+    constexpr int HMAX = 16;
+    uint64_t hs[HMAX + 1];
     for (int64_t s = s_lo; s < s_hi; ++s) {
       const int64_t c0 = L->char_off[s];
       const int32_t n = q.sent_n[s];
@@ -451,7 +566,9 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       NodeView bos{kBOS, kBOS, kBOS, {}, {}, false, false, 0, 0};
       add_node(base, bos, -1);
       int32_t local = 1;
+      const uint32_t* cs = L->chars + c0;
       for (int32_t e = 1; e <= n; ++e) {
+        bool hashed = false;                          // hs[d]: CpVocab hash of chars[e-d:e]
         for (int d = SS; d >= 1; --d) {
           *ss++ = local;
           const int32_t b = e - d;
@@ -475,10 +592,29 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
             any = true;
           }
           if (!any) {                                   // beam.py:36-38: Unknown chars[b:e]
+            const int64_t src = -2 - (((int64_t)b << 32) | (int64_t)(d - 1));
+            if (fast_unk && d <= HMAX) {
+              if (!hashed) {
+                uint64_t h = CpVocab::SEED;
+                for (int k = 1; k <= HMAX && k <= e; ++k) {
+                  h = CpVocab::step(h, cs[e - k]);
+                  hs[k] = CpVocab::fin(h, (uint32_t)k);
+                }
+                hashed = true;
+              }
+              const WordInfo* wi = p->cpv.find(cs + b, (uint32_t)d, hs[d]);
+              if (!wi) {                               // not a vocabulary string: no string needed
+                static constexpr std::string_view none;
+                NodeView u{none, none, kUnk, {}, {}, false, false, (int64_t)d, 0};
+                add_node_wi(base + local, u, nullptr, src);
+                ++local;
+                continue;
+              }
+            }
             unk.clear();
             for (int32_t x = b; x < e; ++x) utf8_append(unk, L->chars[c0 + x]);
             NodeView u{unk, unk, kUnk, {}, {}, false, false, (int64_t)d, 0};
-            add_node(base + local, u, -2 - (((int64_t)b << 32) | (int64_t)(d - 1)));
+            add_node(base + local, u, src);
             ++local;
           }
         }
