@@ -88,7 +88,27 @@ lt_status lt_lexicon_destroy(lt_lexicon* lexicon);
 /* Host only.  n_threads <= 0: OMP_NUM_THREADS, else the hardware concurrency. */
 lt_status lt_lexicon_lookup(const lt_lexicon* lexicon, const lt_text_desc* text, int n_threads,
                             lt_lattices** out);
+/* The UTF-8 columns of lt_lattice_view are built on the first call (the
+ * builder keeps nodes as references into the text, a lemma pool and the tag
+ * names); lt_packer_pack_lattices (lattice_pack.h) and the calls below read
+ * the compact form directly. */
 lt_status lt_lattices_view(const lt_lattices* lattices, lt_lattice_view* view);
+
+/* Offsets and the integer node columns, without building any string column
+ * (valid while the lattices live). */
+typedef struct {
+  int32_t n_sent;
+  int64_t n_words;
+  const uint32_t* chars;          /* [char_off[n_sent]] */
+  const int64_t* char_off;        /* [n_sent + 1] */
+  const int64_t* slot_off;        /* [char_off[n_sent] + 1] */
+  const int64_t* sent_words;      /* [n_sent + 1] */
+  const int32_t* len;             /* [n_words] */
+  const int32_t* b;
+  const int32_t* e;
+  const uint8_t* is_l;
+} lt_lattice_columns;
+lt_status lt_lattices_columns(const lt_lattices* lattices, lt_lattice_columns* columns);
 lt_status lt_lattices_destroy(lt_lattices* lattices);
 /* Bulk string extraction for re-materialising nodes: field 0..4 = word,
  * morph0, morph1, tag0, tag1; the strings of nodes idx[0..n) are written to

@@ -94,6 +94,12 @@ lt_status lt_packer_create(const lt_packer_desc* desc, lt_packer** out);
 lt_status lt_packer_destroy(lt_packer* packer);
 /* max_len as beam_search's (>= 1).  Host only; no GPU needed. */
 lt_status lt_packer_pack(lt_packer* packer, const lt_lattice_desc* lattices, int max_len, lt_packed* out);
+/* The same pack straight from the native lattice builder's output
+ * (lattice_lookup.h): identical arrays, without the UTF-8 columns -- node
+ * strings are hashed as the code points the lattices reference. */
+struct lt_lattices;
+lt_status lt_packer_pack_lattices(lt_packer* packer, const struct lt_lattices* lattices, int max_len,
+                                  lt_packed* out);
 /* Frees one pack's arrays and zeroes *out (NULL or an already released
  * lt_packed: no-op). */
 lt_status lt_packed_release(lt_packed* out);

@@ -29,6 +29,7 @@
 #include "../../include/lattice_lookup.h"
 #include "lt_error.h"
 #include "lt_host.h"
+#include "lt_lattice_store.h"
 
 using lt::Arr;
 
@@ -319,15 +320,6 @@ struct lt_lexicon {
   uint64_t k0 = 0, k1 = 0;
 };
 
-struct lt_lattices {
-  int64_t n_sent = 0, n_words = 0;
-  Arr<uint32_t> chars;
-  Arr<int64_t> char_off, slot_off, sent_words;
-  Arr<char> wb, mb, m1b, tb, t1b;
-  Arr<int64_t> woff, moff, m1off, toff, t1off;
-  Arr<uint8_t> m1null, t1null;
-  Arr<int64_t> len, e, b, is_l;
-};
 
 namespace {
 
@@ -547,14 +539,17 @@ struct Worker {
   }
 };
 
-// Columns of a range of sentences (one worker's share).
+// Compact columns of a range of sentences (one worker's share); lemma morphs
+// in the chunk's pool.
 struct Chunk {
-  std::string wb, mb, m1b, tb, t1b;
-  std::vector<int64_t> woff{0}, moff{0}, m1off{0}, toff{0}, t1off{0};
-  std::vector<uint8_t> m1null, t1null;
-  std::vector<int64_t> len, e, b, is_l;
+  std::vector<uint32_t> w_off, w_len, m0_off, m0_len, m1_off, m1_len;
+  std::vector<int16_t> tag0, tag1;
+  std::vector<int32_t> len, e, b;
+  std::vector<uint8_t> is_l;
+  std::vector<uint32_t> pool;
   std::vector<int64_t> slot_n;      // words per begin slot, sentence-major
   std::vector<int64_t> sent_n;      // words per sentence
+  int64_t field_cps[5] = {0, 0, 0, 0, 0};
   std::string err;
 };
 
@@ -562,23 +557,10 @@ void run_chunk(const lt_lexicon& lx, const lt_text_desc& td, int32_t s0, int32_t
   Worker wk(lx, td.text);
   std::vector<WordRec> words, grouped;
   std::vector<int64_t> cnt;
-  std::string u8;                     // the sentence's text in UTF-8 ...
-  std::vector<uint32_t> u8pos;        // ... and each character's byte offset (+ the end)
+  size_t max_name = 0;
+  for (const std::string& nm : lx.names) max_name = std::max(max_name, nm.size());
   for (int32_t s = s0; s < s1; ++s) {
     const int64_t n = td.char_off[s + 1] - td.char_off[s];
-    // every surface is a substring of the sentence's text: encode it once
-    const int64_t t0 = td.eoj_off[td.sent_eoj[s]], t1 = td.eoj_off[td.sent_eoj[s + 1]];
-    u8.clear();
-    u8pos.clear();
-    for (int64_t x = t0; x < t1; ++x) {
-      u8pos.push_back((uint32_t)u8.size());
-      utf8_append(u8, td.text + x, 1);
-    }
-    u8pos.push_back((uint32_t)u8.size());
-    auto surface = [&](std::string& dst, const WordRec& w) {
-      const uint32_t a = u8pos[w.w_off - t0], z = u8pos[w.w_off - t0 + w.w_len];
-      dst.append(u8, a, z - a);
-    };
     words.clear();
     int32_t offset = 0;
     for (int64_t j = td.sent_eoj[s]; j < td.sent_eoj[s + 1]; ++j) {
@@ -601,76 +583,148 @@ void run_chunk(const lt_lexicon& lx, const lt_text_desc& td, int32_t s0, int32_t
     for (const WordRec& w : words) grouped[(size_t)cnt[(size_t)w.b]++] = w;
     ck.sent_n.push_back((int64_t)words.size());
     for (const WordRec& w : grouped) {
-      surface(ck.wb, w);
-      ck.woff.push_back((int64_t)ck.wb.size());
-      if (w.m0_off < 0) surface(ck.mb, w);
-      else utf8_append(ck.mb, wk.pool.data() + w.m0_off, (size_t)w.m0_len);
-      ck.moff.push_back((int64_t)ck.mb.size());
-      if (w.m1_off >= 0) utf8_append(ck.m1b, wk.pool.data() + w.m1_off, (size_t)w.m1_len);
-      ck.m1off.push_back((int64_t)ck.m1b.size());
-      ck.m1null.push_back(w.m1_off < 0);
-      ck.tb += lx.names[(size_t)w.tag0];
-      ck.toff.push_back((int64_t)ck.tb.size());
-      if (w.tag1 >= 0) ck.t1b += lx.names[(size_t)w.tag1];
-      ck.t1off.push_back((int64_t)ck.t1b.size());
-      ck.t1null.push_back(w.tag1 < 0);
+      ck.w_off.push_back(w.w_off);
+      ck.w_len.push_back(w.w_len);
+      const bool own0 = w.m0_off >= 0, own1 = w.m1_off >= 0;
+      ck.m0_off.push_back(own0 ? (uint32_t)w.m0_off : LT_NOREF);
+      ck.m0_len.push_back(own0 ? (uint32_t)w.m0_len : 0u);
+      ck.m1_off.push_back(own1 ? (uint32_t)w.m1_off : LT_NOREF);
+      ck.m1_len.push_back(own1 ? (uint32_t)w.m1_len : 0u);
+      ck.tag0.push_back((int16_t)w.tag0);
+      ck.tag1.push_back((int16_t)(w.tag1 >= 0 ? w.tag1 : -1));
       ck.len.push_back(w.len);
       ck.e.push_back(w.e);
       ck.b.push_back(w.b);
       ck.is_l.push_back(w.is_l ? 1 : 0);
+      ck.field_cps[0] += w.w_len;
+      ck.field_cps[1] += own0 ? w.m0_len : w.w_len;
+      ck.field_cps[2] += own1 ? w.m1_len : 0;
     }
-    wk.pool.clear();
+    ck.field_cps[3] += (int64_t)(grouped.size() * max_name);
+    ck.field_cps[4] += (int64_t)(grouped.size() * max_name);
   }
-}
-
-lt_strings view_of(const Arr<char>& blob, const Arr<int64_t>& off, const uint8_t* null, int64_t n) {
-  lt_strings s;
-  s.data = blob.data();
-  s.off = off.data();
-  s.null = null;
-  s.n = n;
-  return s;
+  ck.pool.swap(wk.pool);
 }
 
 // Where chunk c's pieces go in the merged arrays.
 struct Base {
-  int64_t words = 0, slots = 0, sents = 0, wb = 0, mb = 0, m1b = 0, tb = 0, t1b = 0;
+  int64_t words = 0, slots = 0, sents = 0, pool = 0;
 };
 
 // Copy chunk c into the merged arrays at base; frees the chunk.
 void merge_chunk(Chunk& c, const Base& at, lt_lattices& L) {
   const int64_t W = (int64_t)c.len.size();
-  auto blob = [](Arr<char>& dst, int64_t base, const std::string& src) {
-    if (!src.empty()) memcpy(dst.data() + base, src.data(), src.size());
-  };
-  blob(L.wb, at.wb, c.wb);
-  blob(L.mb, at.mb, c.mb);
-  blob(L.m1b, at.m1b, c.m1b);
-  blob(L.tb, at.tb, c.tb);
-  blob(L.t1b, at.t1b, c.t1b);
-  auto offs = [&](Arr<int64_t>& dst, const std::vector<int64_t>& src, int64_t base) {
-    int64_t* d = dst.data() + at.words + 1;
-    for (int64_t i = 0; i < W; ++i) d[i] = src[(size_t)i + 1] + base;
-  };
-  offs(L.woff, c.woff, at.wb);
-  offs(L.moff, c.moff, at.mb);
-  offs(L.m1off, c.m1off, at.m1b);
-  offs(L.toff, c.toff, at.tb);
-  offs(L.t1off, c.t1off, at.t1b);
   auto cols = [&](auto& dst, const auto& src) {
     if (W) memcpy(dst.data() + at.words, src.data(), (size_t)W * sizeof(src[0]));
   };
-  cols(L.m1null, c.m1null);
-  cols(L.t1null, c.t1null);
+  cols(L.w_off, c.w_off);
+  cols(L.w_len, c.w_len);
+  cols(L.m0_len, c.m0_len);
+  cols(L.m1_len, c.m1_len);
+  cols(L.tag0, c.tag0);
+  cols(L.tag1, c.tag1);
   cols(L.len, c.len);
   cols(L.e, c.e);
   cols(L.b, c.b);
   cols(L.is_l, c.is_l);
+  const uint32_t pb = (uint32_t)at.pool;                // rebase the pool references
+  for (int64_t i = 0; i < W; ++i) {
+    const uint32_t o0 = c.m0_off[(size_t)i], o1 = c.m1_off[(size_t)i];
+    L.m0_off[at.words + i] = o0 == LT_NOREF ? LT_NOREF : o0 + pb;
+    L.m1_off[at.words + i] = o1 == LT_NOREF ? LT_NOREF : o1 + pb;
+  }
+  if (!c.pool.empty()) memcpy(L.pool.data() + at.pool, c.pool.data(), c.pool.size() * 4);
   int64_t run = at.words;
   for (size_t x = 0; x < c.slot_n.size(); ++x) L.slot_off.data()[at.slots + (int64_t)x + 1] = (run += c.slot_n[x]);
   run = at.words;
   for (size_t x = 0; x < c.sent_n.size(); ++x) L.sent_words.data()[at.sents + (int64_t)x + 1] = (run += c.sent_n[x]);
   c = Chunk();
+}
+
+// UTF-8 of a node's string field (0 word, 1 morph0, 2 morph1, 3 tag0,
+// 4 tag1) appended to out; false for None.
+bool field_utf8(const lt_lattices& L, int field, int64_t i, std::string& out) {
+  switch (field) {
+    case 0: utf8_append(out, L.text.data() + L.w_off[i], L.w_len[i]); return true;
+    case 1: {
+      uint32_t n;
+      const uint32_t* c = L.m0_cps(i, n);
+      utf8_append(out, c, n);
+      return true;
+    }
+    case 2:
+      if (L.m1_off[i] == LT_NOREF) return false;
+      utf8_append(out, L.pool.data() + L.m1_off[i], L.m1_len[i]);
+      return true;
+    case 3: out += L.names[(size_t)L.tag0[i]]; return true;
+    default:
+      if (L.tag1[i] < 0) return false;
+      out += L.names[(size_t)L.tag1[i]];
+      return true;
+  }
+}
+
+// lt_lattices_view's UTF-8 columns (threads over node ranges: each range's
+// blobs, then offsets rebased)
+bool build_utf8(const lt_lattices& L) {
+  std::unique_ptr<lt_lattices::Utf8> u(new (std::nothrow) lt_lattices::Utf8);
+  if (!u) return false;
+  const int64_t W = L.n_words;
+  Arr<char>* blobs[5] = {&u->wb, &u->mb, &u->m1b, &u->tb, &u->t1b};
+  Arr<int64_t>* offs[5] = {&u->woff, &u->moff, &u->m1off, &u->toff, &u->t1off};
+  bool ok = true;
+  for (Arr<int64_t>* a : offs) ok = ok && a->alloc(W + 1);
+  ok = ok && u->m1null.alloc(W) && u->t1null.alloc(W) && u->len.alloc(W) && u->e.alloc(W) && u->b.alloc(W) &&
+       u->is_l.alloc(W);
+  if (!ok) return false;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(lt::host_threads(), W / 4096 + 1));
+  std::vector<std::string> part((size_t)nt * 5);
+  std::vector<std::thread> th;
+  auto work = [&](int t) {
+    const int64_t lo = W * t / nt, hi = W * (t + 1) / nt;
+    for (int f = 0; f < 5; ++f) {
+      std::string& o = part[(size_t)t * 5 + (size_t)f];
+      int64_t* off = offs[f]->data();
+      for (int64_t i = lo; i < hi; ++i) {
+        const bool some = field_utf8(L, f, i, o);
+        off[i + 1] = (int64_t)o.size();                  // part-relative, rebased below
+        if (f == 2) u->m1null[i] = !some;
+        if (f == 4) u->t1null[i] = !some;
+      }
+    }
+    for (int64_t i = lo; i < hi; ++i) {
+      u->len[i] = L.len[i];
+      u->e[i] = L.e[i];
+      u->b[i] = L.b[i];
+      u->is_l[i] = L.is_l[i];
+    }
+  };
+  try {
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (std::thread& x : th) x.join();
+  } catch (...) {
+    for (std::thread& x : th)
+      if (x.joinable()) x.join();
+    return false;
+  }
+  for (int f = 0; f < 5; ++f) {
+    int64_t total = 0;
+    for (int t = 0; t < nt; ++t) total += (int64_t)part[(size_t)t * 5 + (size_t)f].size();
+    if (!blobs[f]->alloc(total)) return false;
+    int64_t* off = offs[f]->data();
+    off[0] = 0;
+    int64_t base = 0;
+    for (int t = 0; t < nt; ++t) {
+      const std::string& o = part[(size_t)t * 5 + (size_t)f];
+      const int64_t lo = W * t / nt, hi = W * (t + 1) / nt;
+      if (!o.empty()) memcpy(blobs[f]->data() + base, o.data(), o.size());
+      for (int64_t i = lo; i < hi; ++i) off[i + 1] += base;
+      base += (int64_t)o.size();
+    }
+  }
+  L.utf8 = std::move(u);
+  return true;
 }
 
 }  // namespace
@@ -832,6 +886,7 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_
   std::unique_ptr<lt_lattices> L(new (std::nothrow) lt_lattices);
   if (!L) return lt::set_error(LT_ENOMEM, "lt_lexicon_lookup: out of host memory");
   const int64_t C = S > 0 ? td->char_off[S] : 0;
+  const int64_t TX = S > 0 ? td->eoj_off[td->sent_eoj[S]] : 0;     // text code points
   // bases of the chunks in the merged arrays
   std::vector<Base> at(ck.size() + 1);
   for (size_t t = 0; t < ck.size(); ++t) {
@@ -841,30 +896,32 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_
     nx.words += (int64_t)c.len.size();
     nx.slots += (int64_t)c.slot_n.size();
     nx.sents += (int64_t)c.sent_n.size();
-    nx.wb += (int64_t)c.wb.size();
-    nx.mb += (int64_t)c.mb.size();
-    nx.m1b += (int64_t)c.m1b.size();
-    nx.tb += (int64_t)c.tb.size();
-    nx.t1b += (int64_t)c.t1b.size();
+    nx.pool += (int64_t)c.pool.size();
+    for (int f = 0; f < 5; ++f) L->field_cps[f] += c.field_cps[f];
   }
   const Base& tot = at.back();
   if (tot.slots != C || tot.sents != S) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup: slot count mismatch");
+  if (tot.pool >= (int64_t)LT_NOREF) return lt::set_error(LT_EUNSUPPORTED, "lt_lexicon_lookup: too many lemmas for one call");
   const int64_t W = tot.words;
   bool ok = L->chars.alloc(C) && L->char_off.alloc(S + 1) && L->slot_off.alloc(C + 1) &&
-            L->sent_words.alloc(S + 1) && L->wb.alloc(tot.wb) && L->mb.alloc(tot.mb) &&
-            L->m1b.alloc(tot.m1b) && L->tb.alloc(tot.tb) && L->t1b.alloc(tot.t1b);
-  for (Arr<int64_t>* a : {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off}) ok = ok && a->alloc(W + 1);
-  ok = ok && L->m1null.alloc(W) && L->t1null.alloc(W);
-  for (Arr<int64_t>* a : {&L->len, &L->e, &L->b, &L->is_l}) ok = ok && a->alloc(W);
+            L->sent_words.alloc(S + 1) && L->text.alloc(TX) && L->pool.alloc(tot.pool);
+  for (Arr<uint32_t>* a : {&L->w_off, &L->w_len, &L->m0_off, &L->m0_len, &L->m1_off, &L->m1_len}) ok = ok && a->alloc(W);
+  ok = ok && L->tag0.alloc(W) && L->tag1.alloc(W) && L->len.alloc(W) && L->e.alloc(W) && L->b.alloc(W) &&
+       L->is_l.alloc(W);
   if (!ok) return lt::set_error(LT_ENOMEM, "lt_lexicon_lookup: out of host memory");
+  try {
+    L->names = lx->names;
+  } catch (...) {
+    return lt::set_error(LT_ENOMEM, "lt_lexicon_lookup: out of host memory");
+  }
   L->n_sent = S;
   L->n_words = W;
   if (C) memcpy(L->chars.data(), td->chars, (size_t)C * 4);
+  if (TX) memcpy(L->text.data(), td->text, (size_t)TX * 4);
   if (S) memcpy(L->char_off.data(), td->char_off, (size_t)(S + 1) * 8);
   else L->char_off.data()[0] = 0;
   L->slot_off.data()[0] = 0;
   L->sent_words.data()[0] = 0;
-  for (Arr<int64_t>* a : {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off}) a->data()[0] = 0;
   {
     std::vector<std::thread> th;
     for (size_t t = 0; t + 1 < ck.size(); ++t)
@@ -876,24 +933,50 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_
   return LT_OK;
 }
 
+lt_status lt_lattices_columns(const lt_lattices* L, lt_lattice_columns* c) {
+  if (!L || !c) return lt::set_error(LT_EINVAL, "lt_lattices_columns: NULL argument");
+  c->n_sent = (int32_t)L->n_sent;
+  c->n_words = L->n_words;
+  c->chars = L->chars.data();
+  c->char_off = L->char_off.data();
+  c->slot_off = L->slot_off.data();
+  c->sent_words = L->sent_words.data();
+  c->len = L->len.data();
+  c->b = L->b.data();
+  c->e = L->e.data();
+  c->is_l = L->is_l.data();
+  return LT_OK;
+}
+
 lt_status lt_lattices_view(const lt_lattices* L, lt_lattice_view* v) {
   if (!L || !v) return lt::set_error(LT_EINVAL, "lt_lattices_view: NULL argument");
+  std::call_once(L->utf8_once, [L] { L->utf8_ok = build_utf8(*L); });
+  if (!L->utf8_ok) return lt::set_error(LT_ENOMEM, "lt_lattices_view: out of host memory");
+  const lt_lattices::Utf8& u = *L->utf8;
   lt_lattice_desc& d = v->lattice;
   const int64_t W = L->n_words;
+  auto view_of = [W](const Arr<char>& blob, const Arr<int64_t>& off, const uint8_t* null) {
+    lt_strings s;
+    s.data = blob.data();
+    s.off = off.data();
+    s.null = null;
+    s.n = W;
+    return s;
+  };
   d.n_sent = (int32_t)L->n_sent;
   d.chars = L->chars.data();
   d.char_off = L->char_off.data();
   d.slot_off = L->slot_off.data();
   d.n_words = W;
-  d.word = view_of(L->wb, L->woff, nullptr, W);
-  d.morph0 = view_of(L->mb, L->moff, nullptr, W);
-  d.tag0 = view_of(L->tb, L->toff, nullptr, W);
-  d.morph1 = view_of(L->m1b, L->m1off, L->m1null.data(), W);
-  d.tag1 = view_of(L->t1b, L->t1off, L->t1null.data(), W);
-  d.len = L->len.data();
-  d.e = L->e.data();
-  d.is_l = L->is_l.data();
-  v->b = L->b.data();
+  d.word = view_of(u.wb, u.woff, nullptr);
+  d.morph0 = view_of(u.mb, u.moff, nullptr);
+  d.tag0 = view_of(u.tb, u.toff, nullptr);
+  d.morph1 = view_of(u.m1b, u.m1off, u.m1null.data());
+  d.tag1 = view_of(u.t1b, u.t1off, u.t1null.data());
+  d.len = u.len.data();
+  d.e = u.e.data();
+  d.is_l = u.is_l.data();
+  v->b = u.b.data();
   v->sent_words = L->sent_words.data();
   return LT_OK;
 }
@@ -902,25 +985,21 @@ lt_status lt_lattices_strings(const lt_lattices* L, int field, const int64_t* id
                               int64_t cap, int64_t* used) {
   if (!L || (n > 0 && !idx) || field < 0 || field > 4)
     return lt::set_error(LT_EINVAL, "lt_lattices_strings: bad argument");
-  const Arr<char>* blobs[] = {&L->wb, &L->mb, &L->m1b, &L->tb, &L->t1b};
-  const Arr<int64_t>* offs[] = {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off};
-  const char* blob = blobs[field]->data();
-  const int64_t* off = offs[field]->data();
-  int64_t need = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t v = idx[i];
-    if (v < 0 || v >= L->n_words) return lt::set_error(LT_EINVAL, "lt_lattices_strings: index %lld", (long long)v);
-    need += off[v + 1] - off[v] + 1;
+  std::string buf;
+  try {
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t v = idx[i];
+      if (v < 0 || v >= L->n_words) return lt::set_error(LT_EINVAL, "lt_lattices_strings: index %lld", (long long)v);
+      field_utf8(*L, field, v, buf);
+      buf.push_back('\0');
+    }
+  } catch (...) {
+    return lt::set_error(LT_ENOMEM, "lt_lattices_strings: out of memory");
   }
+  const int64_t need = (int64_t)buf.size();
   if (used) *used = need;
   if (need > cap || (need > 0 && !out)) return lt::set_error(LT_EINVAL, "lt_lattices_strings: %lld bytes needed", (long long)need);
-  char* p = out;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t v = idx[i], len = off[v + 1] - off[v];
-    memcpy(p, blob + off[v], (size_t)len);
-    p += len;
-    *p++ = '\0';
-  }
+  if (need) memcpy(out, buf.data(), (size_t)need);
   return LT_OK;
 }
 
@@ -929,95 +1008,118 @@ lt_status lt_lattices_strings_coded(const lt_lattices* L, int field, const int64
                                     int64_t* n_unique) {
   if (!L || (n > 0 && (!idx || !codes)) || field < 0 || field > 4)
     return lt::set_error(LT_EINVAL, "lt_lattices_strings_coded: bad argument");
-  const Arr<char>* blobs[] = {&L->wb, &L->mb, &L->m1b, &L->tb, &L->t1b};
-  const Arr<int64_t>* offs[] = {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off};
-  const uint8_t* null = field == 2 ? L->m1null.data() : field == 4 ? L->t1null.data() : nullptr;
-  const char* blob = blobs[field]->data();
-  const int64_t* off = offs[field]->data();
-  // open addressing over (hash, code); the distinct strings in `uniq`.  The
-  // table grows with the distinct strings (load <= 1/2), not with n: paths
-  // repeat few strings, and a small table stays in cache.
-  struct Slot {
-    uint64_t h;                                    // 0: empty
-    int32_t code;
-  };
-  size_t tn = 1024;
-  std::vector<Slot> tab;
-  std::vector<std::string_view> uniq;
+  for (int64_t i = 0; i < n; ++i)
+    if (idx[i] < 0 || idx[i] >= L->n_words)
+      return lt::set_error(LT_EINVAL, "lt_lattices_strings_coded: index %lld", (long long)idx[i]);
+  std::string blob;
+  int64_t nu = 0;
   try {
-    tab.assign(tn, Slot{0, 0});
+    if (field >= 3) {
+      // tags: the lexicon's names, coded in first-appearance order
+      const int16_t* tg = field == 3 ? L->tag0.data() : L->tag1.data();
+      std::vector<int32_t> code_of(L->names.size(), -1);
+      for (int64_t i = 0; i < n; ++i) {
+        const int16_t t = tg[idx[i]];
+        if (t < 0) {
+          codes[i] = -1;
+          continue;
+        }
+        int32_t& c = code_of[(size_t)t];
+        if (c < 0) {
+          const std::string& nm = L->names[(size_t)t];
+          if (nm.find('\0') != std::string::npos)
+            return lt::set_error(LT_EUNSUPPORTED, "lt_lattices_strings_coded: string with a NUL byte");
+          c = (int32_t)nu++;
+          blob += nm;
+          blob.push_back('\0');
+        }
+        codes[i] = c;
+      }
+    } else {
+      // code-point strings: open addressing over (hash, code) on the distinct
+      // strings' (pointer, length); the table grows with the distinct strings
+      struct Ref {
+        const uint32_t* p;
+        uint32_t n;
+      };
+      struct Slot {
+        uint64_t h;                                  // 0: empty
+        int32_t code;
+      };
+      std::vector<Ref> uniq;
+      std::vector<Slot> tab(1024, Slot{0, 0});
+      uint64_t mask = 1023;
+      for (int64_t i = 0; i < n; ++i) {
+        const int64_t v = idx[i];
+        const uint32_t* p;
+        uint32_t m;
+        if (field == 0) {
+          p = L->text.data() + L->w_off[v];
+          m = L->w_len[v];
+        } else if (field == 1) {
+          p = L->m0_cps(v, m);
+        } else {
+          if (L->m1_off[v] == LT_NOREF) {
+            codes[i] = -1;
+            continue;
+          }
+          p = L->pool.data() + L->m1_off[v];
+          m = L->m1_len[v];
+        }
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ m;
+        for (uint32_t k = 0; k < m; ++k) {
+          h = (h ^ p[k]) * 0xBF58476D1CE4E5B9ull;
+          h ^= h >> 31;
+        }
+        h |= 1ull;
+        uint64_t j = h & mask;
+        for (;; j = (j + 1) & mask) {
+          if (tab[j].h == 0) {
+            if (std::find(p, p + m, 0u) != p + m)
+              return lt::set_error(LT_EUNSUPPORTED, "lt_lattices_strings_coded: string with a NUL byte");
+            tab[j] = Slot{h, (int32_t)uniq.size()};
+            uniq.push_back(Ref{p, m});
+            utf8_append(blob, p, m);
+            blob.push_back('\0');
+            if (uniq.size() * 2 > tab.size()) {          // grow: re-place by the stored hashes
+              std::vector<Slot> t2(tab.size() * 2, Slot{0, 0});
+              const uint64_t m2 = t2.size() - 1;
+              for (const Slot& x : tab)
+                if (x.h) {
+                  uint64_t q = x.h & m2;
+                  while (t2[q].h) q = (q + 1) & m2;
+                  t2[q] = x;
+                }
+              tab.swap(t2);
+              mask = m2;
+            }
+            codes[i] = (int32_t)uniq.size() - 1;
+            break;
+          }
+          const Ref& r = uniq[(size_t)tab[j].code];
+          if (tab[j].h == h && r.n == m && std::equal(p, p + m, r.p)) {
+            codes[i] = tab[j].code;
+            break;
+          }
+        }
+      }
+      nu = (int64_t)uniq.size();
+    }
   } catch (...) {
     return lt::set_error(LT_ENOMEM, "lt_lattices_strings_coded: out of memory");
   }
-  uint64_t mask = tn - 1;
-  auto grow = [&]() {
-    std::vector<Slot> t2(tn * 2, Slot{0, 0});
-    const uint64_t m2 = tn * 2 - 1;
-    for (const Slot& x : tab)
-      if (x.h) {
-        uint64_t j = x.h & m2;
-        while (t2[j].h) j = (j + 1) & m2;
-        t2[j] = x;
-      }
-    tab.swap(t2);
-    tn *= 2;
-    mask = m2;
-  };
-  int64_t need = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t v = idx[i];
-    if (v < 0 || v >= L->n_words)
-      return lt::set_error(LT_EINVAL, "lt_lattices_strings_coded: index %lld", (long long)v);
-    if (null && null[v]) {
-      codes[i] = -1;
-      continue;
-    }
-    const std::string_view sv(blob + off[v], (size_t)(off[v + 1] - off[v]));
-    uint64_t h = 0xCBF29CE484222325ull;            // FNV-1a, then a final mix
-    for (unsigned char ch : sv) h = (h ^ ch) * 0x100000001B3ull;
-    h ^= h >> 29;
-    h = (h * 0xBF58476D1CE4E5B9ull) | 1ull;
-    uint64_t j = h & mask;
-    for (;; j = (j + 1) & mask) {
-      if (tab[j].h == 0) {
-        if (std::memchr(sv.data(), 0, sv.size()))   // NUL inside: the NUL-separated form cannot hold it
-          return lt::set_error(LT_EUNSUPPORTED, "lt_lattices_strings_coded: string with a NUL byte");
-        tab[j] = Slot{h, (int32_t)uniq.size()};
-        uniq.push_back(sv);
-        need += (int64_t)sv.size() + 1;
-        if (uniq.size() * 2 > tn) {
-          try {
-            grow();
-          } catch (...) {
-            return lt::set_error(LT_ENOMEM, "lt_lattices_strings_coded: out of memory");
-          }
-          codes[i] = (int32_t)uniq.size() - 1;
-          goto next;
-        }
-        break;
-      }
-      if (tab[j].h == h && uniq[(size_t)tab[j].code] == sv) break;
-    }
-    codes[i] = tab[j].code;
-  next:;
-  }
+  const int64_t need = (int64_t)blob.size();
   if (used) *used = need;
-  if (n_unique) *n_unique = (int64_t)uniq.size();
+  if (n_unique) *n_unique = nu;
   if (need > cap || (need > 0 && !out))
     return lt::set_error(LT_EINVAL, "lt_lattices_strings_coded: %lld bytes needed", (long long)need);
-  char* p = out;
-  for (const std::string_view& sv : uniq) {
-    memcpy(p, sv.data(), sv.size());
-    p += sv.size();
-    *p++ = '\0';
-  }
+  if (need) memcpy(out, blob.data(), (size_t)need);
   return LT_OK;
 }
 
 int64_t lt_lattices_field_bytes(const lt_lattices* L, int field) {
   if (!L || field < 0 || field > 4) return 0;
-  const Arr<int64_t>* offs[] = {&L->woff, &L->moff, &L->m1off, &L->toff, &L->t1off};
-  return L->n_words ? (*offs[field])[L->n_words] : 0;
+  return field < 3 ? 4 * L->field_cps[field] : L->field_cps[field];     // UTF-8: at most 4 bytes per code point
 }
 
 lt_status lt_lattices_destroy(lt_lattices* L) {

@@ -24,6 +24,7 @@
 #include "lt_common.h"
 #include "lt_error.h"
 #include "lt_host.h"
+#include "lt_lattice_store.h"
 
 using namespace lt;
 
@@ -325,6 +326,7 @@ struct lt_packer {
   std::string kb;                                   // key buffer
   CpVocab cpv;                                      // vocab by code points (Unknown nodes)
   bool pref_unk = false;                            // a preference entry for tag 'Unknown'
+  bool has_pref = false;                            // any preference entry
 
   int32_t id_of(std::string_view s) const {
     const WordInfo* v = vocab.get(s);
@@ -379,6 +381,7 @@ lt_status lt_packer_create(const lt_packer_desc* d, lt_packer** out) {
       p->pref[(size_t)s].put(tuple_key(p->kb, str_at(d->pref_tag, i), str_at(d->pref_key, i)),
                              d->pref_value[i]);
       if (str_at(d->pref_tag, i) == kUnk) p->pref_unk = true;
+      p->has_pref = true;
     }
     std::vector<std::pair<std::string_view, const WordInfo*>> words;
     for (const auto& e : p->vocab.tab)
@@ -422,16 +425,104 @@ double lookup(std::string& kb, const ViewMap<double>& m, std::string_view t, std
 
 }  // namespace
 
-lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt_packed* out) {
-  if (!p || !L || !out) return set_error(LT_EINVAL, "lt_packer_pack: NULL argument");
+namespace {
+
+// Node sources of the packer: the generic columnar lattices (UTF-8 strings,
+// lt_lattice_desc) and the native builder's compact lattices (strings as code
+// point references, lt_lattice_store.h).  node() gives a dictionary node's
+// fields, its vocabulary entry and its morph0 id.
+struct DescSrc {
+  const lt_lattice_desc* L;
+  const lt_packer* p;
+  int32_t n_sent() const { return L->n_sent; }
+  int64_t n_words() const { return L->n_words; }
+  const uint32_t* chars() const { return L->chars; }
+  const int64_t* char_off() const { return L->char_off; }
+  const int64_t* slot_off() const { return L->slot_off; }
+  int64_t e(int64_t i) const { return L->e[i]; }
+  struct Buf {};
+  void node(int64_t i, Buf&, NodeView& v, const WordInfo*& wi, int32_t& mid) const {
+    v.word = str_at(L->word, i);
+    v.morph0 = str_at(L->morph0, i);
+    v.tag0 = str_at(L->tag0, i);
+    v.has_morph1 = !is_null(L->morph1, i);
+    v.has_tag1 = !is_null(L->tag1, i);
+    v.morph1 = v.has_morph1 ? str_at(L->morph1, i) : std::string_view();
+    v.tag1 = v.has_tag1 ? str_at(L->tag1, i) : std::string_view();
+    v.len = L->len[i];
+    v.is_l = L->is_l[i];
+    wi = p->vocab.get(v.word);
+    const int32_t wid = wi ? wi->id : 0;
+    mid = v.morph0.data() == v.word.data() && v.morph0.size() == v.word.size() ? wid : p->id_of(v.morph0);
+  }
+};
+
+struct LatSrc {
+  const lt_lattices* L;
+  const lt_packer* p;
+  bool strings;                                  // preference scorers read the node strings
+  int32_t n_sent() const { return (int32_t)L->n_sent; }
+  int64_t n_words() const { return L->n_words; }
+  const uint32_t* chars() const { return L->chars.data(); }
+  const int64_t* char_off() const { return L->char_off.data(); }
+  const int64_t* slot_off() const { return L->slot_off.data(); }
+  int64_t e(int64_t i) const { return L->e[i]; }
+  struct Buf {
+    std::string w, m0, m1;
+  };
+  void node(int64_t i, Buf& buf, NodeView& v, const WordInfo*& wi, int32_t& mid) const {
+    const uint32_t* wc = L->text.data() + L->w_off[i];
+    const uint32_t wn = L->w_len[i];
+    wi = p->cpv.find(wc, wn, CpVocab::hash(wc, wn));
+    const int32_t wid = wi ? wi->id : 0;
+    const bool own0 = L->m0_off[i] != LT_NOREF;
+    if (own0) {
+      const uint32_t* mc = L->pool.data() + L->m0_off[i];
+      const WordInfo* mi = p->cpv.find(mc, L->m0_len[i], CpVocab::hash(mc, L->m0_len[i]));
+      mid = mi ? mi->id : 0;
+    } else {
+      mid = wid;
+    }
+    v.tag0 = L->names[(size_t)L->tag0[i]];
+    v.has_tag1 = L->tag1[i] >= 0;
+    v.tag1 = v.has_tag1 ? std::string_view(L->names[(size_t)L->tag1[i]]) : std::string_view();
+    v.has_morph1 = L->m1_off[i] != LT_NOREF;
+    v.len = L->len[i];
+    v.is_l = L->is_l[i];
+    if (strings) {
+      buf.w.clear();
+      for (uint32_t k = 0; k < wn; ++k) utf8_append(buf.w, wc[k]);
+      v.word = buf.w;
+      if (own0) {
+        buf.m0.clear();
+        for (uint32_t k = 0; k < L->m0_len[i]; ++k) utf8_append(buf.m0, L->pool[L->m0_off[i] + k]);
+        v.morph0 = buf.m0;
+      } else {
+        v.morph0 = v.word;
+      }
+      buf.m1.clear();
+      if (v.has_morph1)
+        for (uint32_t k = 0; k < L->m1_len[i]; ++k) utf8_append(buf.m1, L->pool[L->m1_off[i] + k]);
+      v.morph1 = v.has_morph1 ? std::string_view(buf.m1) : std::string_view();
+    } else {
+      v.word = v.morph0 = v.morph1 = std::string_view();
+    }
+  }
+};
+
+template <class Src>
+lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
   if (max_len < 1) return set_error(LT_EUNSUPPORTED, "lt_packer_pack: max_len %d < 1", max_len);
-  if (L->n_sent < 0 || L->n_words < 0) return set_error(LT_EINVAL, "lt_packer_pack: negative size");
-  const int32_t S = L->n_sent;
-  const int64_t T = S ? L->char_off[S] : 0;
+  if (L.n_sent() < 0 || L.n_words() < 0) return set_error(LT_EINVAL, "lt_packer_pack: negative size");
+  const int32_t S = L.n_sent();
+  const int64_t* const char_off = L.char_off();
+  const int64_t* const slot_off = L.slot_off();
+  const uint32_t* const chars = L.chars();
+  const int64_t T = S ? char_off[S] : 0;
   int64_t longest = 0;
   for (int32_t s = 0; s < S; ++s) {
-    if (L->char_off[s + 1] < L->char_off[s]) return set_error(LT_EINVAL, "lt_packer_pack: char offsets decrease");
-    longest = std::max<int64_t>(longest, L->char_off[s + 1] - L->char_off[s]);
+    if (char_off[s + 1] < char_off[s]) return set_error(LT_EINVAL, "lt_packer_pack: char offsets decrease");
+    longest = std::max<int64_t>(longest, char_off[s + 1] - char_off[s]);
   }
   // a span never exceeds its sentence: max_len beyond max(8, longest) decodes
   // as that (beam.py:29-30), which keeps the span table small
@@ -440,7 +531,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
     return set_error(LT_EUNSUPPORTED, "lt_packer_pack: max_len %d > %d", max_len, LT_MAX_LEN_ANY);
   const int SS = span_slots(max_len);           // span slots per end position
   for (int64_t g = 0; g < T; ++g)
-    if (L->slot_off[g + 1] < L->slot_off[g] || L->slot_off[g + 1] > L->n_words)
+    if (slot_off[g + 1] < slot_off[g] || slot_off[g + 1] > L.n_words())
       return set_error(LT_EINVAL, "lt_packer_pack: bad begin-slot offsets");
   const int n_post = p->n_local - p->n_pre;
 
@@ -448,7 +539,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
   // or one synthesised Unknown node (beam.py:36-38)
   auto span_count = [&](int64_t g, int32_t e) {
     int64_t c = 0;
-    for (int64_t i = L->slot_off[g]; i < L->slot_off[g + 1]; ++i) c += L->e[i] == e;
+    for (int64_t i = slot_off[g]; i < slot_off[g + 1]; ++i) c += L.e(i) == e;
     return c ? c : 1;
   };
   std::unique_ptr<PackOut> o = p->pool->take();
@@ -460,8 +551,8 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
     return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
   parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
     for (int64_t s = lo; s < hi; ++s) {
-      const int64_t c0 = L->char_off[s];
-      const int32_t n = (int32_t)(L->char_off[s + 1] - c0);
+      const int64_t c0 = char_off[s];
+      const int32_t n = (int32_t)(char_off[s + 1] - c0);
       int64_t cnt = 1;                                    // BOS
       for (int32_t e = 1; e <= n; ++e)
         for (int d = 1; d <= max_len && d <= e; ++d) cnt += span_count(c0 + e - d, e);
@@ -488,6 +579,7 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
 
   auto fill = [&](int, int64_t s_lo, int64_t s_hi) {
     std::string kb, unk;
+    typename Src::Buf nbuf;
     // tags are few: remember the last distinct ones (their strings live in
     // the lattice blobs for the whole call)
     std::string_view memo_s[16];
@@ -503,10 +595,8 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       }
       return id;
     };
-    auto add_node_wi = [&](int64_t x, const NodeView& w, const WordInfo* wi, int64_t src) {
+    auto add_node_wi = [&](int64_t x, const NodeView& w, const WordInfo* wi, int32_t mid, int64_t src) {
       const int32_t wid = wi ? wi->id : 0, tid = tag_id(w.tag0);
-      const int32_t mid = w.morph0.data() == w.word.data() && w.morph0.size() == w.word.size()
-                              ? wid : p->id_of(w.morph0);
       uint32_t m = node_mask(p->vm(wid), p->vm(mid), p->vm(tid));
       const bool unk_node = w.tag0 == kUnk;
       if (unk_node) m |= F_UNK;
@@ -552,21 +642,26 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
       q.node_f6[x] = f6;
       q.node_src[x] = src;
     };
-    auto add_node = [&](int64_t x, const NodeView& w, int64_t src) { add_node_wi(x, w, p->vocab.get(w.word), src); };
+    auto add_node = [&](int64_t x, const NodeView& w, int64_t src) {          // (word and morph0 strings)
+      const WordInfo* wi = p->vocab.get(w.word);
+      const int32_t wid = wi ? wi->id : 0;
+      add_node_wi(x, w, wi, w.morph0.data() == w.word.data() && w.morph0.size() == w.word.size()
+                                ? wid : p->id_of(w.morph0), src);
+    };
     // Unknown nodes by code points (CpVocab) unless a preference scorer has an
     // entry for the tag 'Unknown' (its value would depend on the string)
     const bool fast_unk = !p->pref_unk;
     constexpr int HMAX = 16;
     uint64_t hs[HMAX + 1];
     for (int64_t s = s_lo; s < s_hi; ++s) {
-      const int64_t c0 = L->char_off[s];
+      const int64_t c0 = char_off[s];
       const int32_t n = q.sent_n[s];
       const int64_t base = q.sent_node_off[s];
       int32_t* ss = q.span_start.data() + q.sent_span_off[s];
       NodeView bos{kBOS, kBOS, kBOS, {}, {}, false, false, 0, 0};
       add_node(base, bos, -1);
       int32_t local = 1;
-      const uint32_t* cs = L->chars + c0;
+      const uint32_t* cs = chars + c0;
       for (int32_t e = 1; e <= n; ++e) {
         bool hashed = false;                          // hs[d]: CpVocab hash of chars[e-d:e]
         for (int d = SS; d >= 1; --d) {
@@ -575,19 +670,13 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
           if (d > max_len || b < 0) continue;
           const int64_t g = c0 + b;
           bool any = false;
-          for (int64_t i = L->slot_off[g]; i < L->slot_off[g + 1]; ++i) {
-            if (L->e[i] != e) continue;                 // beam.py:33 (w.e == e)
+          for (int64_t i = slot_off[g]; i < slot_off[g + 1]; ++i) {
+            if (L.e(i) != e) continue;                  // beam.py:33 (w.e == e)
             NodeView v;
-            v.word = str_at(L->word, i);
-            v.morph0 = str_at(L->morph0, i);
-            v.tag0 = str_at(L->tag0, i);
-            v.has_morph1 = !is_null(L->morph1, i);
-            v.has_tag1 = !is_null(L->tag1, i);
-            v.morph1 = v.has_morph1 ? str_at(L->morph1, i) : std::string_view();
-            v.tag1 = v.has_tag1 ? str_at(L->tag1, i) : std::string_view();
-            v.len = L->len[i];
-            v.is_l = L->is_l[i];
-            add_node(base + local, v, i);
+            const WordInfo* wi;
+            int32_t mid;
+            L.node(i, nbuf, v, wi, mid);
+            add_node_wi(base + local, v, wi, mid, i);
             ++local;
             any = true;
           }
@@ -606,13 +695,13 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
               if (!wi) {                               // not a vocabulary string: no string needed
                 static constexpr std::string_view none;
                 NodeView u{none, none, kUnk, {}, {}, false, false, (int64_t)d, 0};
-                add_node_wi(base + local, u, nullptr, src);
+                add_node_wi(base + local, u, nullptr, 0, src);
                 ++local;
                 continue;
               }
             }
             unk.clear();
-            for (int32_t x = b; x < e; ++x) utf8_append(unk, L->chars[c0 + x]);
+            for (int32_t x = b; x < e; ++x) utf8_append(unk, chars[c0 + x]);
             NodeView u{unk, unk, kUnk, {}, {}, false, false, (int64_t)d, 0};
             add_node(base + local, u, src);
             ++local;
@@ -655,6 +744,18 @@ lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt
   out->node_src = o->node_src.data();
   out->owner = o.release();
   return LT_OK;
+}
+
+}  // namespace
+
+lt_status lt_packer_pack(lt_packer* p, const lt_lattice_desc* L, int max_len, lt_packed* out) {
+  if (!p || !L || !out) return set_error(LT_EINVAL, "lt_packer_pack: NULL argument");
+  return pack_impl(p, DescSrc{L, p}, max_len, out);
+}
+
+lt_status lt_packer_pack_lattices(lt_packer* p, const lt_lattices* L, int max_len, lt_packed* out) {
+  if (!p || !L || !out) return set_error(LT_EINVAL, "lt_packer_pack_lattices: NULL argument");
+  return pack_impl(p, LatSrc{L, p, p->has_pref}, max_len, out);
 }
 
 lt_status lt_packed_release(lt_packed* out) {

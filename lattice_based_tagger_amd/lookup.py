@@ -50,11 +50,18 @@ class LatticeView(C.Structure):
     _fields_ = [('lattice', LatticeDesc), ('b', C.c_void_p), ('sent_words', C.c_void_p)]
 
 
+class LatticeColumns(C.Structure):
+    _fields_ = [('n_sent', C.c_int32), ('n_words', C.c_int64), ('chars', C.c_void_p), ('char_off', C.c_void_p),
+                ('slot_off', C.c_void_p), ('sent_words', C.c_void_p), ('len', C.c_void_p), ('b', C.c_void_p),
+                ('e', C.c_void_p), ('is_l', C.c_void_p)]
+
+
 _SIGS = {
     'lt_lexicon_create': (C.c_int32, [C.c_void_p, C.POINTER(C.c_void_p)]),
     'lt_lexicon_destroy': (C.c_int32, [C.c_void_p]),
     'lt_lexicon_lookup': (C.c_int32, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     'lt_lattices_view': (C.c_int32, [C.c_void_p, C.POINTER(LatticeView)]),
+    'lt_lattices_columns': (C.c_int32, [C.c_void_p, C.POINTER(LatticeColumns)]),
     'lt_lattices_destroy': (C.c_int32, [C.c_void_p]),
     'lt_py_str_hash': (C.c_int64, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64]),
     'lt_py_set2_second_first': (C.c_int, [C.c_int64, C.c_int64]),
@@ -304,34 +311,38 @@ class NativeLattices:
 
     def __init__(self, lib, handle, chars):
         self.lib, self.handle, self.chars = lib, handle, chars
-        v = LatticeView()
-        _capi.check(lib.lt_lattices_view(handle, C.byref(v)))
-        self.view = v
-        self.desc = v.lattice
-        d = v.lattice
-        S, N = d.n_sent, d.n_words
+        c = LatticeColumns()
+        _capi.check(lib.lt_lattices_columns(handle, C.byref(c)))
+        S, N = c.n_sent, c.n_words
 
-        def arr(p, ct, n):
+        def arr(p, ct, n, dt):
             if n == 0 or not p:
-                return np.zeros(0, dtype=np.int64 if ct is C.c_int64 else np.uint8)
+                return np.zeros(0, dtype=dt)
             return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(n,))
 
         self.n_words = N
-        self.sent_words = arr(v.sent_words, C.c_int64, S + 1)
-        self.slot_off = arr(d.slot_off, C.c_int64, int(arr(d.char_off, C.c_int64, S + 1)[-1]) + 1
-                            if S else 1)
-        self.char_off = arr(d.char_off, C.c_int64, S + 1)
+        self.sent_words = arr(c.sent_words, C.c_int64, S + 1, np.int64)
+        self.char_off = arr(c.char_off, C.c_int64, S + 1, np.int64)
+        self.slot_off = arr(c.slot_off, C.c_int64, int(self.char_off[-1]) + 1 if S else 1, np.int64)
+        # node columns of the compact lattices (int32 / uint8 views, no copies)
+        self._ints = {'len': arr(c.len, C.c_int32, N, np.int32), 'b': arr(c.b, C.c_int32, N, np.int32),
+                      'e': arr(c.e, C.c_int32, N, np.int32), 'is_l': arr(c.is_l, C.c_uint8, N, np.uint8)}
+        self._view = None
         self._cols = None
-        self._ints = None
+
+    @property
+    def desc(self):
+        """The lattices as an lt_lattice_desc (UTF-8 columns, built by the
+        library on first use: the native packer reads the compact lattices
+        directly, lt_packer_pack_lattices)."""
+        if self._view is None:
+            v = LatticeView()
+            _capi.check(self.lib.lt_lattices_view(self.handle, C.byref(v)))
+            self._view = v
+        return self._view.lattice
 
     def _int_columns(self):
         """len / b / e / is_l as views of the library's arrays (no copies)."""
-        if self._ints is None:
-            d, N = self.desc, self.n_words
-
-            def ints(p):
-                return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), shape=(N,)) if N else None
-            self._ints = {'len': ints(d.len), 'b': ints(self.view.b), 'e': ints(d.e), 'is_l': ints(d.is_l)}
         return self._ints
 
     def _columns(self):
@@ -347,11 +358,9 @@ class NativeLattices:
                         if t.null else None)
                 return (blob, off), null
 
-            def ints(p):
-                return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), shape=(N,)) if N else None
             self._cols = {'word': strs(d.word), 'morph0': strs(d.morph0), 'morph1': strs(d.morph1),
-                          'tag0': strs(d.tag0), 'tag1': strs(d.tag1), 'len': ints(d.len),
-                          'b': ints(self.view.b), 'e': ints(d.e), 'is_l': ints(d.is_l)}
+                          'tag0': strs(d.tag0), 'tag1': strs(d.tag1)}
+            self._cols.update(self._ints)
         return self._cols
 
     def word(self, i):
@@ -416,7 +425,7 @@ class NativeLattices:
         ints = self._int_columns()
         isl = (ints['is_l'][idx] != 0).view(np.uint8)
         _pyobj.load().words(Word, out, np.ascontiguousarray(pos, dtype=np.int64), tuple(uniqs), tuple(codes_all),
-                            (ints['len'][idx], ints['b'][idx], ints['e'][idx], isl))
+                            tuple(ints[f][idx].astype(np.int64) for f in ('len', 'b', 'e')) + (isl,))
 
     def empty(self, s):
         """True when sentence s has characters but no node: the reference's

@@ -284,6 +284,17 @@ class NativePacker:
         the sentences' characters.  -> (PackedBatch, node views)."""
         out = Packed()
         _capi.check(self.lib.lt_packer_pack(self.handle, C.byref(desc), int(max_len), C.byref(out)))
+        return self._result(out, words, chars_l)
+
+    def pack_lattices(self, lat, max_len=8):
+        """pack_desc of the native lattice builder's lattices (lookup.NativeLattices),
+        read in their compact form (lt_packer_pack_lattices): the same arrays
+        without building the lattices' UTF-8 columns."""
+        out = Packed()
+        _capi.check(self.lib.lt_packer_pack_lattices(self.handle, lat.handle, int(max_len), C.byref(out)))
+        return self._result(out, lat, lat.chars)
+
+    def _result(self, out, words, chars_l):
         block = _PackBlock(self.lib, out)       # no copies: the arrays are views of the pack
         b = out.batch
         N, S, nspan, npost = b.n_nodes, b.n_sent, b.n_span, b.n_post

@@ -246,7 +246,7 @@ class Tagger:
             lat = lat if lat is not None else lookup(chunk)
             if npk is None:
                 return lat, None, None
-            packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+            packed, views = npk.pack_lattices(lat, max_len=8)
             return lat, packed, views
 
         def upload(i, fut):

@@ -192,3 +192,38 @@ def test_tagger_ignores_lookup_argument_like_the_reference(fix):
     assert calls == sent.split()
     with pytest.raises(TypeError):
         Tagger(dictionary=fixture_dictionary(entry['lexicon']), custom_lookup='not callable')
+
+
+@pytest.mark.parametrize('name', ['base', 'demo'])
+def test_pack_lattices_equals_pack_desc(fix, name):
+    """lt_packer_pack_lattices (the compact lattices, strings hashed as code
+    points) gives exactly lt_packer_pack's arrays over the UTF-8 columns --
+    for composites with and without preference scorers (which read the node
+    strings), and for a model whose vocabulary holds some Unknown spans."""
+    import numpy as np
+    from golden_io import load
+    from lattice_based_tagger_amd.beam import lowered_model
+    from lattice_based_tagger_amd.native_packer import packer_for
+    entry = fix[name]
+    sents = list(entry['sentences']) + ['ㅋㅋ 가\t나다', '😀 이것은']
+    lat = fixture_lexicon(entry).lookup([s for s in sents if s.split()], n_threads=3)
+    seen, models = 0, set()
+    for gname in ('base', 'demo', 'scorers'):
+        for case in load(gname):
+            model = lowered_model(case.funcs)
+            if id(model) in models:
+                continue
+            models.add(id(model))
+            npk = packer_for(model)
+            if npk is None:
+                continue
+            a, _ = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+            b, _ = npk.pack_lattices(lat, max_len=8)
+            for f in ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start', 'node_word', 'node_morph0',
+                      'node_tag', 'node_mask'):
+                assert np.array_equal(getattr(a, f), getattr(b, f)), (gname, f)
+            for f in ('node_pre', 'node_f4', 'node_f5', 'node_f6', 'node_post'):
+                assert np.array_equal(np.asarray(getattr(a, f)).view(np.uint64),
+                                      np.asarray(getattr(b, f)).view(np.uint64)), (gname, f)
+            seen += 1
+    assert seen >= 5
