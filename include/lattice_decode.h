@@ -57,6 +57,9 @@ typedef struct lt_batch lt_batch;
 
 /* ---- library ------------------------------------------------------------ */
 int lt_abi_version(void);
+/* The slot hash of this library's model tables (lt_model_image.hash_version
+ * of the images it builds; an image of another version is refused). */
+uint32_t lt_hash_version(void);
 const char* lt_last_error(void);
 /* Number of visible HIP devices (0 when no GPU). */
 int lt_device_count(void);

@@ -20,7 +20,7 @@ LT_EUNSUPPORTED = -4
 _STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED', -5: 'LT_ERCCL'}
 
 EXPORTED_SYMBOLS = (
-    'lt_abi_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
+    'lt_abi_version', 'lt_hash_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
     'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
     'lt_batch_destroy', 'lt_batch_code_slots', 'lt_batch_pieces', 'lt_set_piece_bytes', 'lt_decode_launch', 'lt_last_kernel_ms',
     'lt_kernel_ms_recent', 'lt_kernel_name',
@@ -162,6 +162,7 @@ def load(path=None):
             'lt_count_ops': (i32, [vp, vp, vp, C.c_int, C.POINTER(i64), C.POINTER(i64),
                                    C.POINTER(i64), C.POINTER(i64)]),
             'lt_comm_library': (C.c_char_p, []),
+            'lt_hash_version': (C.c_uint32, []),
             'lt_comm_unique_id': (i32, [C.c_char_p]),
             'lt_comm_create': (i32, [vp, C.c_int, C.c_int, C.c_char_p, C.POINTER(vp)]),
             'lt_comm_destroy': (i32, [vp]),
@@ -173,6 +174,8 @@ def load(path=None):
             'lt_last_gather_ms': (i32, [vp, C.POINTER(C.c_float)]),
         }
         for name, (res, args) in sig.items():
+            if name in OPTIONAL_CALLS and not hasattr(lib, name):
+                continue                    # (an older experiment build; see OPTIONAL_CALLS)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -192,6 +195,9 @@ def load(path=None):
         _lib = lib
         return lib
 
+
+# entry points an A/B build of an earlier revision may lack (tools/gpu_ab.sh)
+OPTIONAL_CALLS = ('lt_hash_version',)
 
 # lt_* entry points that return in microseconds (see load)
 HELD_CALLS = ('lt_decode_launch', 'lt_result_fetch', 'lt_result_view', 'lt_result_fetch_packed',

@@ -186,6 +186,9 @@ class Decoder:
         dm = model._device_models.get(self.key)
         if dm is None:
             image = getattr(model, 'image', None)           # model pack: no table build
+            lib_hash = getattr(self.ctx._lib, 'lt_hash_version', None)
+            if image is not None and lib_hash is not None and int(image.get('hash_version', 0)) != int(lib_hash()):
+                image = None                                # a pack from another slot hash: rebuild
             if image is None and len(model.keys) and len(model._device_models):
                 image = _built_image(model)                 # second device: build the table once
             if image is not None:

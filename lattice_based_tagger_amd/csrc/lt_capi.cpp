@@ -226,6 +226,7 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
 extern "C" {
 
 int lt_abi_version(void) { return LT_ABI_VERSION; }
+uint32_t lt_hash_version(void) { return HASH_VERSION; }
 
 const char* lt_last_error(void) { return g_err.c_str(); }
 
@@ -384,6 +385,11 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
   const bool narrow = max_id < (1u << NARROW_ID_BITS);
   const int64_t slot_bytes = narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
   int64_t slots = std::max<int64_t>(64, (int64_t)(d->n_keys / 0.45) + 1);   // load factor <= 0.45
+  if (narrow) {                                 // narrow slot hash: a power of two (lt_common.h)
+    int64_t p2 = 64;
+    while (p2 < slots) p2 <<= 1;
+    slots = p2;
+  }
   uint32_t seed = 0x2545F491u;
   bool ok = false;
   for (int attempt = 0; attempt < 24 && !ok; ++attempt) {
@@ -400,7 +406,7 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
     if (dup >= 0) return fail(LT_EINVAL, "lt_model_create: duplicate key %lld", (long long)dup);
     if (!ok) {
       seed = seed * 0x9E3779B1u + 0x7F4A7C15u;
-      if (attempt % 3 == 2) slots = slots + slots / 8;
+      if (attempt % 3 == 2) slots = narrow ? slots * 2 : slots + slots / 8;
     }
   }
   if (!ok) return fail(LT_EINVAL, "lt_model_create: cuckoo table build failed");
@@ -479,6 +485,8 @@ lt_status lt_model_create_from_image(lt_ctx* c, const lt_model_image* v, lt_mode
                 v->hash_version, HASH_VERSION);
   if (v->narrow != 0 && v->narrow != 1) return fail(LT_EINVAL, "model image: bad narrow flag");
   if (v->slots < 64 || !v->table) return fail(LT_EINVAL, "model image: empty table");
+  if (v->narrow && (v->slots & (v->slots - 1)) != 0)
+    return fail(LT_EINVAL, "model image: a narrow table has a power-of-two slot count");
   const int64_t sb = v->narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
   if (v->slots > (((int64_t)1 << 31) - 1) / sb || v->table_bytes != v->slots * sb)
     return fail(LT_EINVAL, "model image: table size %lld does not match %lld slots",

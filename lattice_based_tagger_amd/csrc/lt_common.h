@@ -148,13 +148,17 @@ LT_HD void cuckoo_slots(KeyBase kb, uint32_t seed, uint32_t slots, uint32_t& i1,
   i2 = slot_of(mix1(kb.b2 ^ (seed * 0x9E3779B1u + 0x632BE5ABu)), slots);
 }
 
-// Narrow tables (ids < 2^20) hash with full-rate 24-bit multiplies only:
-// slot = mulhi(mul24(a,Ka) ^ mul24(b,Kb) ^ mul24(c,Kc) ^ cls*Ks, slots), two
-// independent constant sets derived from the table seed (a failed build
-// reseeds, which changes every constant).  No 32-bit multiply per lookup
-// besides the range reduction (v_mul_u32_u24 is full rate; v_mul_lo_u32 is
-// quarter rate).
-constexpr uint32_t HASH_VERSION = 3;     // 3: overflow flags, 3-bit class code
+// Narrow tables (ids < 2^20): one key mix, both slots from it.  Every
+// integer multiply costs about three simple VALU operations on gfx950
+// (tools/valu_rate.hip: v_mul_u32_u24, v_mul_lo_u32 and v_mul_hi_u32 alike),
+// and the beam kernels are VALU-bound, so a lookup spends four multiplies:
+//   x  = mul24(a,Ka) ^ mul24(b,Kb) ^ mul24(c,Kc) ^ cls*Ks
+//   i1 = x >> (32 - log2 slots)
+//   i2 = ((x ^ (x >> 16)) * K2) >> (32 - log2 slots)
+// on a power-of-two table (load factor 0.225-0.45).  Keys with equal x share
+// both slots; a build that meets three of them reseeds, which changes every
+// constant.
+constexpr uint32_t HASH_VERSION = 4;     // 3: overflow flags, 3-bit class code; 4: one mix, 2^n slots
 struct NarrowHash {
   uint32_t k1a, k1b, k1c, k1s, k2a, k2b, k2c, k2s;
 };
@@ -168,17 +172,32 @@ LT_HD NarrowHash narrow_hash(uint32_t seed) {
     y ^= y >> 12;
     y *= 0x297A2D39u;
     y ^= y >> 15;
-    v[i] = (i == 3 || i == 7) ? (y | 1u) : ((y & 0xFFFFFFu) | 0x800001u);
+    v[i] = (i == 3 || i == 7 || i == 4) ? (y | 1u) : ((y & 0xFFFFFFu) | 0x800001u);
   }
   return NarrowHash{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
 }
+LT_HD uint32_t slot_shift(uint32_t slots) {            // slots = 2^n, 16 <= slots <= 2^31
+#if defined(__HIP_DEVICE_COMPILE__)
+  return 32u - (uint32_t)__builtin_ctz(slots);
+#else
+  uint32_t n = 0;
+  while ((1u << n) < slots) ++n;
+  return 32u - n;
+#endif
+}
+LT_HD uint32_t narrow_mix(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls) {
+  // (the products' high bits carry every bit of the ids below them: slot 1
+  // takes the top bits as they are)
+  return mul24(a, h.k1a) ^ mul24(b, h.k1b) ^ mul24(c, h.k1c) ^ (cls * h.k1s);
+}
 LT_HD uint32_t narrow_slot1(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
                             uint32_t slots) {
-  return slot_of(mul24(a, h.k1a) ^ mul24(b, h.k1b) ^ mul24(c, h.k1c) ^ (cls * h.k1s), slots);
+  return narrow_mix(h, a, b, c, cls) >> slot_shift(slots);
 }
 LT_HD uint32_t narrow_slot2(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
                             uint32_t slots) {
-  return slot_of(mul24(a, h.k2a) ^ mul24(b, h.k2b) ^ mul24(c, h.k2c) ^ (cls * h.k2s), slots);
+  const uint32_t x = narrow_mix(h, a, b, c, cls);
+  return ((x ^ (x >> 16)) * h.k2a) >> slot_shift(slots);
 }
 LT_HD void narrow_slots(const NarrowHash& h, uint32_t a, uint32_t b, uint32_t c, uint32_t cls,
                         uint32_t slots, uint32_t& i1, uint32_t& i2) {

@@ -549,13 +549,39 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
   // (span entries: SS n + 1 per sentence)
   if (!o->sent_n.alloc(S) || !o->sent_node_off.alloc((int64_t)S + 1) || !o->sent_span_off.alloc((int64_t)S + 1))
     return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
+  // words per span (b, d) of a sentence from one pass over its words (a
+  // begin slot's words are otherwise rescanned for every end position); too
+  // large a table (long sentences at a large max_len): scan as before
+  auto span_table = [&](int64_t c0, int32_t n, std::vector<uint16_t>& tab) {
+    if ((int64_t)n * max_len > (1 << 20)) return false;
+    tab.assign((size_t)n * (size_t)max_len, 0);
+    for (int32_t b = 0; b < n; ++b)
+      for (int64_t i = slot_off[c0 + b]; i < slot_off[c0 + b + 1]; ++i) {
+        const int64_t d = L.e(i) - b;
+        if (d >= 1 && d <= max_len) {
+          uint16_t& t = tab[(size_t)b * (size_t)max_len + (size_t)(d - 1)];
+          if (t == 0xFFFF) return false;                  // (counts past 16 bits: scan)
+          ++t;
+        }
+      }
+    return true;
+  };
   parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
+    std::vector<uint16_t> tab;
     for (int64_t s = lo; s < hi; ++s) {
       const int64_t c0 = char_off[s];
       const int32_t n = (int32_t)(char_off[s + 1] - c0);
       int64_t cnt = 1;                                    // BOS
-      for (int32_t e = 1; e <= n; ++e)
-        for (int d = 1; d <= max_len && d <= e; ++d) cnt += span_count(c0 + e - d, e);
+      if (span_table(c0, n, tab)) {
+        for (int32_t e = 1; e <= n; ++e)
+          for (int d = 1; d <= max_len && d <= e; ++d) {
+            const uint16_t t = tab[(size_t)(e - d) * (size_t)max_len + (size_t)(d - 1)];
+            cnt += t ? t : 1;
+          }
+      } else {
+        for (int32_t e = 1; e <= n; ++e)
+          for (int d = 1; d <= max_len && d <= e; ++d) cnt += span_count(c0 + e - d, e);
+      }
       o->sent_n[s] = n;
       o->sent_node_off[s + 1] = cnt;
       o->sent_span_off[s + 1] = SS * (int64_t)n + 1;
@@ -580,6 +606,7 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
   auto fill = [&](int, int64_t s_lo, int64_t s_hi) {
     std::string kb, unk;
     typename Src::Buf nbuf;
+    std::vector<uint16_t> tab;
     // tags are few: remember the last distinct ones (their strings live in
     // the lattice blobs for the whole call)
     std::string_view memo_s[16];
@@ -662,6 +689,7 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
       add_node(base, bos, -1);
       int32_t local = 1;
       const uint32_t* cs = chars + c0;
+      const bool tabbed = span_table(c0, n, tab);
       for (int32_t e = 1; e <= n; ++e) {
         bool hashed = false;                          // hs[d]: CpVocab hash of chars[e-d:e]
         for (int d = SS; d >= 1; --d) {
@@ -670,7 +698,8 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
           if (d > max_len || b < 0) continue;
           const int64_t g = c0 + b;
           bool any = false;
-          for (int64_t i = slot_off[g]; i < slot_off[g + 1]; ++i) {
+          const bool empty = tabbed && tab[(size_t)b * (size_t)max_len + (size_t)(d - 1)] == 0;
+          for (int64_t i = empty ? slot_off[g + 1] : slot_off[g]; i < slot_off[g + 1]; ++i) {
             if (L.e(i) != e) continue;                  // beam.py:33 (w.e == e)
             NodeView v;
             const WordInfo* wi;

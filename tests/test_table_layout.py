@@ -28,7 +28,7 @@ def narrow_hash(seed):
         y ^= y >> 12
         y = (y * 0x297A2D39) & 0xFFFFFFFF
         y ^= y >> 15
-        v.append((y | 1) if i in (3, 7) else ((y & 0xFFFFFF) | 0x800001))
+        v.append((y | 1) if i in (3, 4, 7) else ((y & 0xFFFFFF) | 0x800001))
     return v
 
 
@@ -37,9 +37,14 @@ def mul24(x, k):
 
 
 def slot(h, a, b, c, cls, slots, which):
-    o = 0 if which == 1 else 4
-    base = mul24(a, h[o]) ^ mul24(b, h[o + 1]) ^ mul24(c, h[o + 2]) ^ _u32(cls.astype(np.uint64) * np.uint64(h[o + 3]))
-    return ((base * np.uint64(slots)) >> np.uint64(32)).astype(np.int64)
+    """HASH_VERSION 4: one mix x, i1 = x >> s, i2 = ((x ^ x >> 16) * K2) >> s on
+    2^n slots (s = 32 - n)."""
+    assert slots & (slots - 1) == 0
+    shift = np.uint64(32 - (int(slots).bit_length() - 1))
+    x = mul24(a, h[0]) ^ mul24(b, h[1]) ^ mul24(c, h[2]) ^ _u32(cls.astype(np.uint64) * np.uint64(h[3]))
+    if which == 2:
+        x = _u32((x ^ (x >> np.uint64(16))) * np.uint64(h[4]))
+    return (x >> shift).astype(np.int64)
 
 
 def narrow_key(a, b, c, cls):
@@ -77,7 +82,7 @@ def model():
 
 def test_every_key_found_with_primary_first_lookup(model):
     keys, coefs, arr = model
-    assert arr['narrow'] == 1 and arr['hash_version'] == 3
+    assert arr['narrow'] == 1 and arr['hash_version'] == 4
     table = arr['table'].view(np.uint64).reshape(-1, 2)
     h = narrow_hash(arr['seed'])
     a, b, c, cls = keys.T

@@ -82,7 +82,7 @@ def main():
         lat = lex.lookup(sents, n_threads=a.threads)
         t['lookup'] = time.perf_counter() - t0
         t0 = time.perf_counter()
-        packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+        packed, views = npk.pack_lattices(lat, max_len=8)        # (as Tagger.tag_batch packs)
         t['pack'] = time.perf_counter() - t0
         t0 = time.perf_counter()
         dec = Decoder.get(0)

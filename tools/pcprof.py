@@ -68,14 +68,14 @@ def main():
     npk = packer_for(model)
     sents = unique_text(entry['sentences'], a.sentences, 7)
     lat = lex.lookup(sents, n_threads=a.threads)                   # warm
-    npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+    npk.pack_lattices(lat, max_len=8)
     prof.pcprof_start(2000)
     t0 = time.perf_counter()
     for _ in range(3):
         if a.stage in ('lookup', 'both'):
             lat = lex.lookup(sents, n_threads=a.threads)
         if a.stage in ('pack', 'both'):
-            npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+            npk.pack_lattices(lat, max_len=8)
     dt = time.perf_counter() - t0
     prof.pcprof_stop(b'/tmp/pcprof.txt')
     out, total = resolve('/tmp/pcprof.txt')

@@ -61,7 +61,7 @@ def main():
         t0 = time.perf_counter()
         lat = lex.lookup(sents, n_threads=a.threads)
         t1 = time.perf_counter()
-        packed, views = npk.pack_desc(lat.desc, lat, lat.chars, max_len=8)
+        packed, views = npk.pack_lattices(lat, max_len=8)
         t2 = time.perf_counter()
         print('lookup %.3f s  pack %.3f s' % (t1 - t0, t2 - t1), flush=True)
     count, length, score, codes, _, _ = lt_oracle.decode(packed, model.keys, model.coefs, a.k, nthreads=a.threads)
