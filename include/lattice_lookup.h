@@ -92,6 +92,12 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lexicon, const lt_text_desc* text,
  * builder keeps nodes as references into the text, a lemma pool and the tag
  * names); lt_packer_pack_lattices (lattice_pack.h) and the calls below read
  * the compact form directly. */
+/* The same from raw sentences: sentence s is text[sent_off[s] ..
+ * sent_off[s+1]) (UTF-32); its eojeols are sent.split() (runs of CPython
+ * str.isspace() characters separate them, lookup.py:58) and its decode
+ * characters sent.replace(' ', '') (tagger.py:72). */
+lt_status lt_lexicon_lookup_sents(const lt_lexicon* lexicon, const uint32_t* text, const int64_t* sent_off,
+                                  int32_t n_sent, int n_threads, lt_lattices** out);
 lt_status lt_lattices_view(const lt_lattices* lattices, lt_lattice_view* view);
 
 /* Offsets and the integer node columns, without building any string column

@@ -492,8 +492,12 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
     unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
     if unk.size:
         code = -2 - src[unk]
-        chars = chars_list if type(chars_list) is list else list(chars_list)
-        ext.unknowns(Word, flat, unk, chars, seg[unk] // T, code >> 32, (code & 0xFFFFFFFF) + 1, Unk)
+        if hasattr(chars_list, 'cps'):                  # native lattices: straight from their UTF-32 buffer
+            ext.unknowns_cp(Word, flat, unk, chars_list.cps, chars_list.off, seg[unk] // T, code >> 32,
+                            (code & 0xFFFFFFFF) + 1, Unk)
+        else:
+            chars = chars_list if type(chars_list) is list else list(chars_list)
+            ext.unknowns(Word, flat, unk, chars, seg[unk] // T, code >> 32, (code & 0xFFFFFFFF) + 1, Unk)
     # the sentinels are immutable tuples: one BOS, one EOS per sentence length
     bos, eos = bos_word(), {}
     vals = _typed_scores(model, packed, glob, seg, Lf, first, score[:, :T], n, T, bos, flat)

@@ -933,6 +933,79 @@ lt_status lt_lexicon_lookup(const lt_lexicon* lx, const lt_text_desc* td, int n_
   return LT_OK;
 }
 
+// str.isspace() of CPython 3.10 (Py_UNICODE_ISSPACE): the separators of
+// str.split() without arguments
+static inline bool py_isspace(uint32_t c) {
+  if (c <= 0x20) return c == 0x20 || (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x1F);
+  if (c < 0x85) return false;
+  return c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) || c == 0x2028 ||
+         c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+
+lt_status lt_lexicon_lookup_sents(const lt_lexicon* lx, const uint32_t* text, const int64_t* sent_off,
+                                  int32_t n_sent, int n_threads, lt_lattices** out) {
+  if (!lx || !out || n_sent < 0 || (n_sent > 0 && (!sent_off || (!text && sent_off[n_sent] > 0))))
+    return lt::set_error(LT_EINVAL, "lt_lexicon_lookup_sents: bad argument");
+  *out = nullptr;
+  const int32_t S = n_sent;
+  if (S > 0 && sent_off[0] != 0) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup_sents: sent_off[0] != 0");
+  for (int32_t s = 0; s < S; ++s)
+    if (sent_off[s + 1] < sent_off[s]) return lt::set_error(LT_EINVAL, "lt_lexicon_lookup_sents: offsets decrease");
+  // pass 1 (threads): eojeols, eojeol characters and decode characters per sentence
+  std::vector<int64_t> n_eoj((size_t)S + 1, 0), n_tx((size_t)S + 1, 0), n_ch((size_t)S + 1, 0);
+  lt::parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
+    for (int64_t s = lo; s < hi; ++s) {
+      int64_t ne = 0, nt = 0, nc = 0;
+      bool in = false;
+      for (int64_t i = sent_off[s]; i < sent_off[s + 1]; ++i) {
+        const uint32_t c = text[i];
+        const bool sp = py_isspace(c);
+        if (!sp) {
+          ++nt;
+          if (!in) ++ne;
+        }
+        in = !sp;
+        nc += c != 0x20;
+      }
+      n_eoj[(size_t)s + 1] = ne;
+      n_tx[(size_t)s + 1] = nt;
+      n_ch[(size_t)s + 1] = nc;
+    }
+  }, 1024);
+  for (int32_t s = 0; s < S; ++s) {
+    n_eoj[(size_t)s + 1] += n_eoj[(size_t)s];
+    n_tx[(size_t)s + 1] += n_tx[(size_t)s];
+    n_ch[(size_t)s + 1] += n_ch[(size_t)s];
+  }
+  std::vector<uint32_t> tx((size_t)std::max<int64_t>(1, n_tx[(size_t)S])), ch((size_t)std::max<int64_t>(1, n_ch[(size_t)S]));
+  std::vector<int64_t> eoj_off((size_t)n_eoj[(size_t)S] + 1);
+  eoj_off[0] = 0;
+  // pass 2 (threads): the eojeols' text back to back, their ends, the characters
+  lt::parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
+    for (int64_t s = lo; s < hi; ++s) {
+      int64_t t = n_tx[(size_t)s], c = n_ch[(size_t)s], j = n_eoj[(size_t)s];
+      bool in = false;
+      for (int64_t i = sent_off[s]; i < sent_off[s + 1]; ++i) {
+        const uint32_t x = text[i];
+        const bool sp = py_isspace(x);
+        if (sp && in) eoj_off[(size_t)++j] = t;        // an eojeol ends
+        if (!sp) tx[(size_t)t++] = x;
+        in = !sp;
+        if (x != 0x20) ch[(size_t)c++] = x;
+      }
+      if (in) eoj_off[(size_t)++j] = t;
+    }
+  }, 1024);
+  lt_text_desc td;
+  td.n_sent = S;
+  td.text = tx.data();
+  td.eoj_off = eoj_off.data();
+  td.sent_eoj = n_eoj.data();
+  td.chars = ch.data();
+  td.char_off = n_ch.data();
+  return lt_lexicon_lookup(lx, &td, n_threads, out);
+}
+
 lt_status lt_lattices_columns(const lt_lattices* L, lt_lattice_columns* c) {
   if (!L || !c) return lt::set_error(LT_EINVAL, "lt_lattices_columns: NULL argument");
   c->n_sent = (int32_t)L->n_sent;

@@ -17,6 +17,8 @@
  *   unknowns(word_type, out, pos, chars, sent, b, d, unk_tag)
  *       out[pos[i]] = word_type(sub, sub, None, unk_tag, None, d, b, b + d, False),
  *                     sub = chars[sent[i]][b[i]:b[i] + d[i]]
+ *   unknowns_cp(word_type, out, pos, cps, off, sent, b, d, unk_tag)
+ *       as unknowns, sub = the code points cps[off[sent[i]] + b[i] .. + d[i]) as a str
  *   scatter(out, pos, vals)      out[pos[i]] = vals[i]
  *   paths(flat, ends, bos, eos, has)
  *       [[bos] + flat[ends[s-1]:ends[s]] + [eos[s]]  if has[s] else None  for s]
@@ -234,6 +236,82 @@ done:
   return res;
 }
 
+static PyObject* py_unknowns_cp(PyObject* self, PyObject* args) {
+  PyObject *wt, *out, *pos_o, *cps_o, *off_o, *sent_o, *b_o, *d_o, *unk;
+  if (!PyArg_ParseTuple(args, "OO!OOOOOOO", &wt, &PyList_Type, &out, &pos_o, &cps_o, &off_o, &sent_o, &b_o, &d_o,
+                        &unk))
+    return NULL;
+  if (check_word_type(wt) < 0) return NULL;
+  Buf pos = {0}, cb = {0}, ob = {0}, sb = {0}, bb = {0}, db = {0};
+  PyObject* res = NULL;
+  Py_ssize_t n, ns, nc;
+  if (PyObject_GetBuffer(pos_o, &pos.b, PyBUF_C_CONTIGUOUS) < 0) return NULL;
+  pos.ok = 1;
+  if (pos.b.itemsize != 8) {
+    PyErr_SetString(PyExc_ValueError, "_ltpy.unknowns_cp: pos must be int64");
+    goto done;
+  }
+  n = pos.b.len / 8;
+  if (get_buf(cps_o, &cb, 4, 0, "cps") < 0 || get_buf(off_o, &ob, 8, 1, "off") < 0 || get_buf(sent_o, &sb, 8, n, "sent") < 0 ||
+      get_buf(b_o, &bb, 8, n, "b") < 0 || get_buf(d_o, &db, 8, n, "d") < 0)
+    goto done;
+  ns = ob.b.len / 8 - 1;
+  nc = cb.b.len / 4;
+  {
+    const int64_t *P = (const int64_t*)pos.b.buf, *O = (const int64_t*)ob.b.buf, *S = (const int64_t*)sb.b.buf,
+                  *Bg = (const int64_t*)bb.b.buf, *D = (const int64_t*)db.b.buf;
+    const uint32_t* CP = (const uint32_t*)cb.b.buf;
+    const Py_ssize_t nout = PyList_GET_SIZE(out);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (P[i] < 0 || P[i] >= nout || S[i] < 0 || S[i] >= ns || Bg[i] < 0 || D[i] < 1 ||
+          O[S[i]] + Bg[i] + D[i] > O[S[i] + 1] || O[S[i] + 1] > nc) {
+        PyErr_SetString(PyExc_IndexError, "_ltpy.unknowns_cp: span outside its sentence");
+        goto done;
+      }
+    }
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* sub = PyUnicode_FromKindAndData(PyUnicode_4BYTE_KIND, CP + O[S[i]] + Bg[i], D[i]);
+      if (!sub) goto done;
+      PyObject* w = new_tuple((PyTypeObject*)wt, 9);
+      PyObject *ln = PyLong_FromLongLong(D[i]), *b0 = PyLong_FromLongLong(Bg[i]),
+               *e0 = PyLong_FromLongLong(Bg[i] + D[i]);
+      if (!w || !ln || !b0 || !e0) {
+        Py_DECREF(sub);
+        Py_XDECREF(w);
+        Py_XDECREF(ln);
+        Py_XDECREF(b0);
+        Py_XDECREF(e0);
+        goto done;
+      }
+      Py_INCREF(sub);
+      PyTuple_SET_ITEM(w, 0, sub);
+      PyTuple_SET_ITEM(w, 1, sub);
+      Py_INCREF(Py_None);
+      PyTuple_SET_ITEM(w, 2, Py_None);
+      Py_INCREF(unk);
+      PyTuple_SET_ITEM(w, 3, unk);
+      Py_INCREF(Py_None);
+      PyTuple_SET_ITEM(w, 4, Py_None);
+      PyTuple_SET_ITEM(w, 5, ln);
+      PyTuple_SET_ITEM(w, 6, b0);
+      PyTuple_SET_ITEM(w, 7, e0);
+      Py_INCREF(Py_False);
+      PyTuple_SET_ITEM(w, 8, Py_False);
+      PyList_SetItem(out, P[i], w);
+    }
+  }
+  Py_INCREF(Py_None);
+  res = Py_None;
+done:
+  rel(&pos);
+  rel(&cb);
+  rel(&ob);
+  rel(&sb);
+  rel(&bb);
+  rel(&db);
+  return res;
+}
+
 static PyObject* py_paths(PyObject* self, PyObject* args) {
   PyObject *flat, *ends_o, *bos, *eos, *has_o;
   if (!PyArg_ParseTuple(args, "O!OOO!O", &PyList_Type, &flat, &ends_o, &bos, &PyList_Type, &eos, &has_o))
@@ -319,6 +397,7 @@ static PyMethodDef methods[] = {
     {"scatter", py_scatter, METH_VARARGS, "out[pos[i]] = vals[i]."},
     {"words", py_words, METH_VARARGS, "Dictionary Words into out[pos] (see module doc)."},
     {"unknowns", py_unknowns, METH_VARARGS, "Synthesised Unknown Words into out[pos]."},
+    {"unknowns_cp", py_unknowns_cp, METH_VARARGS, "Unknown Words from a UTF-32 buffer into out[pos]."},
     {"paths", py_paths, METH_VARARGS, "Per-sentence path lists [bos] + flat[a:z] + [eos]."},
     {NULL, NULL, 0, NULL}};
 

@@ -60,6 +60,8 @@ _SIGS = {
     'lt_lexicon_create': (C.c_int32, [C.c_void_p, C.POINTER(C.c_void_p)]),
     'lt_lexicon_destroy': (C.c_int32, [C.c_void_p]),
     'lt_lexicon_lookup': (C.c_int32, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    'lt_lexicon_lookup_sents': (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int,
+                                            C.POINTER(C.c_void_p)]),
     'lt_lattices_view': (C.c_int32, [C.c_void_p, C.POINTER(LatticeView)]),
     'lt_lattices_columns': (C.c_int32, [C.c_void_p, C.POINTER(LatticeColumns)]),
     'lt_lattices_destroy': (C.c_int32, [C.c_void_p]),
@@ -229,34 +231,25 @@ class NativeLexicon:
                    eojeol_lookup.prefer_exact_match, hash_key=hash_key)
 
     def lookup(self, sents, n_threads=0):
-        """NativeLattices of ``sents`` (str each)."""
-        eojs, sent_eoj, chars_l = [], [0], []
+        """NativeLattices of ``sents`` (str each).  The sentences travel as one
+        UTF-32 buffer; the library splits the eojeols (``sent.split()``) and
+        drops the spaces (``sent.replace(' ', '')``) on its threads."""
+        sents = sents if type(sents) is list else list(sents)
         for s in sents:
             if type(s) is not str:
                 raise Unsupported('sentences must be str')
-            e = s.split()
-            eojs.extend(e)
-            sent_eoj.append(len(eojs))
-            chars_l.append(s.replace(' ', ''))
         try:
-            text = ''.join(eojs).encode('utf-32-le')
-            chars = ''.join(chars_l).encode('utf-32-le')
+            raw = ''.join(sents).encode('utf-32-le')
         except UnicodeEncodeError:
             raise Unsupported('text not encodable')
-        text = np.frombuffer(text, dtype=np.uint32) if text else np.zeros(1, np.uint32)
-        chars_a = np.frombuffer(chars, dtype=np.uint32) if chars else np.zeros(1, np.uint32)
-        eoj_off = np.zeros(len(eojs) + 1, dtype=np.int64)
-        if eojs:
-            np.cumsum(np.fromiter(map(len, eojs), dtype=np.int64, count=len(eojs)), out=eoj_off[1:])
-        char_off = np.zeros(len(chars_l) + 1, dtype=np.int64)
-        if chars_l:
-            np.cumsum(np.fromiter(map(len, chars_l), dtype=np.int64, count=len(chars_l)), out=char_off[1:])
-        sent_eoj = np.asarray(sent_eoj, dtype=np.int64)
-        td = TextDesc(len(chars_l), text.ctypes.data, eoj_off.ctypes.data, sent_eoj.ctypes.data,
-                      chars_a.ctypes.data, char_off.ctypes.data)
+        text = np.frombuffer(raw, dtype=np.uint32) if raw else np.zeros(1, np.uint32)
+        off = np.zeros(len(sents) + 1, dtype=np.int64)
+        if sents:
+            np.cumsum(np.fromiter(map(len, sents), dtype=np.int64, count=len(sents)), out=off[1:])
         h = C.c_void_p()
-        _capi.check(self.lib.lt_lexicon_lookup(self.handle, C.byref(td), int(n_threads), C.byref(h)))
-        return NativeLattices(self.lib, h, chars_l)
+        _capi.check(self.lib.lt_lexicon_lookup_sents(self.handle, text.ctypes.data, off.ctypes.data, len(sents),
+                                                     int(n_threads), C.byref(h)))
+        return NativeLattices(self.lib, h)
 
     def close(self):
         if self.handle:
@@ -305,12 +298,37 @@ def _gather_strings(blob, off, idx):
     return out.tobytes().decode('utf-8').split('\0')[:n]
 
 
+class SentChars:
+    """The sentences' decode characters as a sequence of str, decoded from the
+    lattices' UTF-32 buffer on access (``cps``, ``off``: the buffer and the
+    sentence offsets, for bulk consumers)."""
+
+    def __init__(self, cps, off):
+        self.cps, self.off = cps, off
+
+    def __len__(self):
+        return len(self.off) - 1
+
+    def __getitem__(self, s):
+        if isinstance(s, slice):
+            return [self[i] for i in range(*s.indices(len(self)))]
+        if s < 0:
+            s += len(self)
+        if not 0 <= s < len(self):
+            raise IndexError(s)
+        return self.cps[int(self.off[s]):int(self.off[s + 1])].tobytes().decode('utf-32-le')
+
+    def __iter__(self):
+        for s in range(len(self)):
+            yield self[s]
+
+
 class NativeLattices:
     """Lattices built by the library: columnar (``desc`` for lt_packer_pack)
     plus lazy ``Word`` materialisation and the reference-shaped ``bindex``."""
 
-    def __init__(self, lib, handle, chars):
-        self.lib, self.handle, self.chars = lib, handle, chars
+    def __init__(self, lib, handle):
+        self.lib, self.handle = lib, handle
         c = LatticeColumns()
         _capi.check(lib.lt_lattices_columns(handle, C.byref(c)))
         S, N = c.n_sent, c.n_words
@@ -329,6 +347,9 @@ class NativeLattices:
                       'e': arr(c.e, C.c_int32, N, np.int32), 'is_l': arr(c.is_l, C.c_uint8, N, np.uint8)}
         self._view = None
         self._cols = None
+        # each sentence's characters (sent.replace(' ', '')), decoded on access
+        self.chars = SentChars(arr(c.chars, C.c_uint32, int(self.char_off[-1]) if S else 0, np.uint32),
+                               self.char_off)
 
     @property
     def desc(self):

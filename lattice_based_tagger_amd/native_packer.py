@@ -320,9 +320,7 @@ class NativePacker:
         if S == 0:
             batch.sent_node_off = np.zeros(1, np.int64)
             batch.sent_span_off = np.zeros(1, np.int64)
-        views = [_NodeView(src, int(batch.sent_node_off[s]), int(batch.sent_node_off[s + 1]), words, chars)
-                 for s, chars in enumerate(chars_l)]
-        return batch, views
+        return batch, _Views(src, batch.sent_node_off, words, chars_l)
 
     def close(self):
         if self.handle:
@@ -336,11 +334,38 @@ class NativePacker:
             pass
 
 
+class _Views:
+    """Per-sentence node views of a pack (sentence s -> _NodeView), made on
+    access: ``views[s][i]`` is the Word of sentence s's local node i."""
+
+    def __init__(self, src, node_off, words, chars_l):
+        self.src, self.node_off, self.words, self.chars_l = src, node_off, words, chars_l
+
+    def __len__(self):
+        return len(self.node_off) - 1
+
+    def __getitem__(self, s):
+        if s < 0:
+            s += len(self)
+        if not 0 <= s < len(self):
+            raise IndexError(s)
+        return _NodeView(self.src, int(self.node_off[s]), int(self.node_off[s + 1]), self.words, self.chars_l, s)
+
+    def __iter__(self):
+        for s in range(len(self)):
+            yield self[s]
+
+
 class _NodeView:
     """Lazy local-node -> Word object of one sentence (as packer.pack's lists)."""
 
-    def __init__(self, src, lo, hi, words, chars):
-        self.src, self.lo, self.hi, self.words, self.chars = src, lo, hi, words, chars
+    def __init__(self, src, lo, hi, words, chars_l, s):
+        self.src, self.lo, self.hi, self.words = src, lo, hi, words
+        self._chars_l, self._s = chars_l, s
+
+    @property
+    def chars(self):
+        return self._chars_l[self._s]
 
     def __len__(self):
         return self.hi - self.lo

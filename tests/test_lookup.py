@@ -227,3 +227,79 @@ def test_pack_lattices_equals_pack_desc(fix, name):
                                       np.asarray(getattr(b, f)).view(np.uint64)), (gname, f)
             seen += 1
     assert seen >= 5
+
+
+def _lookup_textdesc(lex, sents):
+    """The lattices through lt_lexicon_lookup with the split done in Python
+    (sent.split(), sent.replace(' ', '')) -- the reference's own calls."""
+    import ctypes as C
+    import numpy as np
+    eojs, sent_eoj, chars_l = [], [0], []
+    for s in sents:
+        e = s.split()
+        eojs.extend(e)
+        sent_eoj.append(len(eojs))
+        chars_l.append(s.replace(' ', ''))
+
+    def cps(strs):
+        raw = ''.join(strs).encode('utf-32-le')
+        return np.frombuffer(raw, np.uint32) if raw else np.zeros(1, np.uint32)
+
+    def offs(strs):
+        o = np.zeros(len(strs) + 1, np.int64)
+        np.cumsum([len(x) for x in strs], out=o[1:])
+        return o
+    text, chars, eoj_off, char_off = cps(eojs), cps(chars_l), offs(eojs), offs(chars_l)
+    sent_eoj = np.asarray(sent_eoj, np.int64)
+    td = LK.TextDesc(len(sents), text.ctypes.data, eoj_off.ctypes.data, sent_eoj.ctypes.data, chars.ctypes.data,
+                     char_off.ctypes.data)
+    h = C.c_void_p()
+    from lattice_based_tagger_amd import _capi
+    _capi.check(lex.lib.lt_lexicon_lookup(lex.handle, C.byref(td), 2, C.byref(h)))
+    return LK.NativeLattices(lex.lib, h), chars_l
+
+
+def test_sentence_split_in_the_library_matches_python(fix):
+    """lt_lexicon_lookup_sents splits like str.split() (every str.isspace()
+    character) and strips only U+0020 like str.replace(' ', '')."""
+    import numpy as np
+    entry = fix['base']
+    lex = fixture_lexicon(entry)
+    spaces = [chr(c) for c in range(0x110000) if chr(c).isspace()]
+    assert len(spaces) == 29
+    rng = np.random.default_rng(3)
+    words = [w for s in entry['sentences'] for w in s.split()][:300] + ['​', 'ㅋ­', '😀']
+    sents = []
+    for _ in range(200):
+        parts = [words[i] for i in rng.integers(0, len(words), rng.integers(1, 6))]
+        seps = [''.join(rng.choice(spaces, rng.integers(1, 3))) for _ in parts]
+        lead = rng.choice(['', ' ', '\t', '　 '])
+        sents.append(lead + ''.join(p + sp for p, sp in zip(parts, seps)))
+    sents = [s for s in sents if s.split()]
+    a = lex.lookup(sents, n_threads=3)
+    b, chars_l = _lookup_textdesc(lex, sents)
+    assert list(a.chars) == chars_l
+    assert np.array_equal(a.sent_words, b.sent_words) and np.array_equal(a.slot_off, b.slot_off)
+    idx = np.arange(a.n_words, dtype=np.int64)
+    assert [tuple(w) for w in a.words_bulk(idx)] == [tuple(w) for w in b.words_bulk(idx)]
+
+
+def test_unknowns_from_code_points_equal_str_slices(fix):
+    import numpy as np
+    from lattice_based_tagger_amd import _pyobj
+    from lattice_based_tagger_amd.tagset import Unk
+    from lattice_based_tagger_amd.word import Word
+    lat = fixture_lexicon(fix['demo']).lookup(['가나다 라마', '😀a b', 'ㅋ'])
+    chars = list(lat.chars)
+    assert chars == ['가나다라마', '😀ab', 'ㅋ'] and lat.chars[-1] == 'ㅋ' and lat.chars[0:2] == chars[:2]
+    sent = np.array([0, 1, 1, 2], np.int64)
+    b = np.array([1, 0, 1, 0], np.int64)
+    d = np.array([3, 2, 2, 1], np.int64)
+    out1, out2 = [None] * 4, [None] * 4
+    pos = np.arange(4, dtype=np.int64)
+    ext = _pyobj.load()
+    ext.unknowns(Word, out1, pos, chars, sent, b, d, Unk)
+    ext.unknowns_cp(Word, out2, pos, lat.chars.cps, lat.chars.off, sent, b, d, Unk)
+    assert out1 == out2 and [type(w.word) for w in out2] == [str] * 4
+    with pytest.raises(IndexError):
+        ext.unknowns_cp(Word, out2, pos[:1], lat.chars.cps, lat.chars.off, sent[2:3], b[:1], np.array([5], np.int64), Unk)
