@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdarg>
@@ -771,14 +772,29 @@ static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc
   return out;
 }
 
+// LT_TIMING=1: per-phase wall times of lt_batch_create on stderr (diagnostic)
+static bool timing_on() {
+  static const bool on = [] {
+    const char* v = std::getenv("LT_TIMING");
+    return v && *v && *v != '0';
+  }();
+  return on;
+}
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch** out) {
   if (!c || !d || !out) return fail(LT_EINVAL, "lt_batch_create: NULL argument");
   *out = nullptr;
+  const double t_start = timing_on() ? now_s() : 0.0;
+  double t_valid = 0, t_arena = 0, t_recs = 0;
   if (max_k < 1 || max_k > LT_MAX_BEAM_ANY)
     return fail(LT_EUNSUPPORTED, "lt_batch_create: max_k %d not in 1..%d", max_k, LT_MAX_BEAM_ANY);
   int inf_signs = 0;
   lt_status st = validate(d, &inf_signs);
   if (st != LT_OK) return st;
+  if (timing_on()) t_valid = now_s();
   HIP_TRY(hipSetDevice(c->device));
   lt_batch* b = new (std::nothrow) lt_batch;
   if (!b) return fail(LT_ENOMEM, "lt_batch_create: out of host memory");
@@ -886,6 +902,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     delete b;
     return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "lt_batch_create: %s", hipGetErrorString(e));
   }
+  if (timing_on()) t_arena = now_s();
   char* D = b->arena.d;
   char* H = b->arena.h;
   for (size_t q = 0; q < P; ++q) {
@@ -961,6 +978,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       }
     }
   }, 256);
+  if (timing_on()) t_recs = now_s();
   std::vector<std::vector<int64_t>> edge_base_tmp(P);
   for (size_t q = 0; q < P; ++q) {
     const lt_piece& pc = b->pieces[q];
@@ -991,6 +1009,9 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "lt_batch_create: %s",
                 hipGetErrorString(e));
   }
+  if (timing_on())
+    fprintf(stderr, "LT_TIMING batch_create nodes=%lld validate=%.4f arena=%.4f records=%.4f upload=%.4f s\n",
+            (long long)d->n_nodes, t_valid - t_start, t_arena - t_valid, t_recs - t_arena, now_s() - t_recs);
   *out = b;
   return LT_OK;
 }
