@@ -623,10 +623,15 @@ __device__ __forceinline__ double v1_sum(const double (&cf)[6], uint32_t pres6, 
                         ((pres6 & 0x30u) << 3);
   const double v[9] = {cf[0], cf[1], cf[2], cf[3], c.f4, c.f5, h.f6, cf[4], cf[5]};
   if (__builtin_popcount(pres) >= 8) {
-    bool pr[9];
+    // 8 or 9 present: numpy's pairwise block over the first 8 present, then
+    // the 9th.  The one absent feature (miss; 9 = none) by a bit scan, the
+    // compaction r[q] = v[q + (q >= miss)] by one compare per element.
+    const uint32_t miss = (uint32_t)__builtin_ctz(~pres | 0x200u);
+    double r[8];
 #pragma unroll
-    for (int q = 0; q < 9; ++q) pr[q] = (pres >> q) & 1u;
-    return numpy_sum9(v, pr);
+    for (int q = 0; q < 8; ++q) r[q] = ((uint32_t)q < miss) ? v[q] : v[q + 1];
+    const double s8 = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    return miss == 9u ? s8 + v[8] : s8;
   }
   double t = 0.0;
 #pragma unroll
@@ -1516,6 +1521,7 @@ lt_beam_hw(DecodeParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][S][LN];
   __shared__ unsigned long long tkey[WPB][S][KT];
   __shared__ uint32_t tgen[WPB][S][KT];
+  __shared__ __attribute__((aligned(16))) int sst[WPB][S][12];   // each group's span starts of the position
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   Aux aux{nullptr, 0u, p.hk};
@@ -1601,15 +1607,18 @@ lt_beam_hw(DecodeParams p) {
     uint4* const cst = stg[wv];
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
+    // the group's span starts through LDS: lanes j <= 8 of each group write
+    // theirs, every lane reads its group's nine (three reads instead of a
+    // readlane / select per value and group)
+    if (hl <= MAX_SPAN) sst[wv][hf][hl] = pfs;
+    __builtin_amdgcn_wave_barrier();
     int ss[MAX_SPAN + 1];
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) {
-      if constexpr (S == 2) {
-        const int a = __builtin_amdgcn_readlane(pfs, j), b = __builtin_amdgcn_readlane(pfs, 32 + j);
-        ss[j] = hf ? b : a;
-      } else {
-        ss[j] = __shfl(pfs, hf * G + j);
-      }
+    {
+      const int4 s0 = *reinterpret_cast<const int4*>(&sst[wv][hf][0]);
+      const int4 s1 = *reinterpret_cast<const int4*>(&sst[wv][hf][4]);
+      ss[0] = s0.x; ss[1] = s0.y; ss[2] = s0.z; ss[3] = s0.w;
+      ss[4] = s1.x; ss[5] = s1.y; ss[6] = s1.z; ss[7] = s1.w;
+      ss[8] = sst[wv][hf][8];
     }
     __builtin_amdgcn_wave_barrier();
     const bool live = e <= n;
