@@ -485,6 +485,13 @@ __device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c
 // beam_size = 1
 // ===========================================================================
 
+// (e - d) mod RING for 1 <= d <= RING - 1 <= e, from em9 = e mod RING: a
+// compare and an add instead of a signed division by RING per lane
+__device__ __forceinline__ int ring_back(int em9, int d) {
+  const int r = em9 - d;
+  return r < 0 ? r + RING : r;
+}
+
 // Ring entry of the k=1 kernel: the hypothesis (best path ending at one end
 // position) reduced to what scoring an expansion of it needs.
 struct alignas(16) VEntry {
@@ -1223,7 +1230,7 @@ lt_beam_pk(DecodeParams p) {
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
       const int c = (d <= dmax) ? cnt9[(e - d) % RING] : 0;
-      pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
+      pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)(ss[j + 1] - ss[j]));   // (c <= 256, m < 2^21)
     }
     const int M = pre[MAX_SPAN];
 
@@ -1275,7 +1282,7 @@ lt_beam_pk(DecodeParams p) {
         } else {
           c = load_cand(B, nbase + (uint32_t)node);
         }
-        const int hb = act ? (e - d) % RING : 0;
+        const int hb = act ? ring_back(em9, d) : 0;
         const int hr = act ? r : 0;
         const VEntry h0 = R[hb][hr];
         // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
@@ -1429,7 +1436,7 @@ lt_beam_pk(DecodeParams p) {
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
-      ne = v_grow<COUNT>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + wl]), (uint32_t)wnode);
+      ne = v_grow<COUNT>(R[ring_back(em9, d)][wr], c, ord_score(LK[KTP - nrun + wl]), (uint32_t)wnode);
       bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
@@ -1631,7 +1638,7 @@ lt_beam_hw(DecodeParams p) {
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
       const int c = (live && d <= dmax) ? cnt9[(e - d) % RING] : 0;
-      pre[j + 1] = pre[j] + c * (ss[j + 1] - ss[j]);
+      pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)(ss[j + 1] - ss[j]));   // (c <= 256, m < 2^21)
     }
     const int M = pre[MAX_SPAN];                // this half's expansions
     const int Mmax = gmax(M);
@@ -1683,7 +1690,7 @@ lt_beam_hw(DecodeParams p) {
         } else {
           c = load_cand(B, nbase + (uint32_t)node);
         }
-        const int hb = act ? (e - d) % RING : 0;
+        const int hb = act ? ring_back(em9, d) : 0;
         const int hr = act ? r : 0;
         const VEntry h0 = R[hb][hr];
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
@@ -1799,7 +1806,7 @@ lt_beam_hw(DecodeParams p) {
     const bool far = writer && wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       const int d = MAX_SPAN - wj;
-      ne = v_grow<false>(R[(e - d) % RING][wr], c, ord_score(LK[KTP - nrun + hl]), (uint32_t)wnode);
+      ne = v_grow<false>(R[ring_back(em9, d)][wr], c, ord_score(LK[KTP - nrun + hl]), (uint32_t)wnode);
       bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
     };
     auto staged = [&](int r) {
