@@ -508,6 +508,11 @@ def main():
                 'kernel_bytes_frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                 'avg_kernel_ms': avg_kernel_s * 1e3,
                 'launch': 'rank 0 shard' if d.world > 1 else 'whole batch',
+                'frac_note': 'frac = SURVEY 8(d) algorithmic bytes (one 24 B hash slot per reference '
+                             'feature tuple) / kernel time; the kernel resolves feature classes 4-6 '
+                             'per node and class 3 from an LDS table, so it issues fewer bytes and '
+                             'frac can pass 1; kernel_bytes_frac (bytes issued) and traffic_frac '
+                             '(PMC bytes) measure the memory system',
             },
             'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                                'table_probes': probes, 'table_slot_loads': table_loads},

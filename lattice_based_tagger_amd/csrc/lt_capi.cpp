@@ -385,7 +385,15 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
   }
   const bool narrow = max_id < (1u << NARROW_ID_BITS);
   const int64_t slot_bytes = narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
-  int64_t slots = std::max<int64_t>(64, (int64_t)(d->n_keys / 0.45) + 1);   // load factor <= 0.45
+  // load factor <= 0.45 (LT_TABLE_LOAD: a lower bound for table-size
+  // experiments -- fewer keys displaced to their secondary slot, so fewer
+  // flagged primaries, against a larger footprint in the caches)
+  double max_load = 0.45;
+  if (const char* env = std::getenv("LT_TABLE_LOAD")) {
+    const double v = std::atof(env);
+    if (v > 0.0 && v < max_load) max_load = v;
+  }
+  int64_t slots = std::max<int64_t>(64, (int64_t)(d->n_keys / max_load) + 1);
   if (narrow) {                                 // narrow slot hash: a power of two (lt_common.h)
     int64_t p2 = 64;
     while (p2 < slots) p2 <<= 1;

@@ -779,6 +779,12 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #ifndef PK_WPB
 #define PK_WPB 4
 #endif
+#ifndef HW_SPRE
+#define HW_SPRE 1
+#endif
+#ifndef PK_SPRE
+#define PK_SPRE 0
+#endif
 constexpr int P_WPB = PK_WPB;           // waves per block
 // k=1 lane-schedule entries (lt_k1_sched)
 constexpr uint32_t K1_NODE = 0x03FFFFFFu, K1_IDLE = K1_NODE, K1_FIRST = 0x80000000u;
@@ -898,6 +904,13 @@ lt_viterbi_pk(DecodeParams p) {
   __shared__ unsigned long long amax[P_WPB][2][W];
   __shared__ uint32_t amin[P_WPB][2][W];
   __shared__ double d3l[D3_DIM * D3_DIM];
+  // the occupancy the launch bounds ask for must fit a CU's 160 KiB of LDS
+  // (4 SIMDs x PK_WAVES waves in blocks of P_WPB waves); the LDS window PK_BPL
+  // is sized to the last byte of it
+  static_assert(!(NARROW && W <= 6) ||
+                    (sizeof(ring) + sizeof(bpl) + sizeof(stg) + sizeof(srec) + sizeof(amax) + sizeof(amin) +
+                     sizeof(d3l)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
+                "lt_viterbi_pk LDS exceeds the CU's share for PK_WAVES waves per SIMD");
   const Aux aux = stage_aux<NARROW>(p, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1059,7 +1072,9 @@ lt_viterbi_pk(DecodeParams p) {
     int32_t* codes = p.out_codes + p.cum_n[sid];
     const uint32_t* bpg = p.bp + p.bp_off[sid];
     int pos = nw;
-    for (int step = (int)f.depth - 1; step >= 0; --step) {
+    // (pos > 0 and the depth bound hold on a consistent beam; they keep a
+    // corrupted one from chasing backpointers out of the sentence's rows)
+    for (int step = min((int)f.depth, nw) - 1; step >= 0 && pos > 0; --step) {
       const uint32_t v = pos < BPL ? bpl[wv][lane][pos] : bpg[(int64_t)pos * bstride];
       codes[step] = (int32_t)bp_node(v);
       pos -= (int)bp_d(v);
@@ -1136,6 +1151,38 @@ __device__ __forceinline__ double ord_score(unsigned long long k) {
   return __builtin_bit_cast(double, b);
 }
 
+// Rank of key ck at list position ci among the 4-aligned list LK[q0, q1): the
+// entries with a larger key and the equal keys earlier in the list (lt_beam_hw;
+// no generation indices loaded: 2.43 -> 2.36 ms at k=2, 4.70 -> 4.57 at k=5;
+// lt_beam_pk's copy of the loop with the indices measured faster there).
+// Every list the beam kernels rank holds equal keys in generation order (the
+// running top-k in rank order -- key desc, generation asc -- then the chunk's
+// entries in generation order, all younger than the running ones), so the
+// list position stands in for the generation index of the tie-break.
+__device__ __forceinline__ int list_rank(const unsigned long long* LK, int q0, int q1, unsigned long long ck,
+                                         int ci) {
+  int rank = 0;
+#pragma unroll 2
+  for (int q = q0; q < q1; q += 4) {
+    const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
+    const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
+    const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rank += (kq[u] > ck || (kq[u] == ck && q + u < ci)) ? 1 : 0;
+  }
+  return rank;
+}
+
+// Top-k slots TK/TG [0, k) from the list LK[q0, q1) for the entry (ck, cg)
+// at list position ci (ck = 0: none).  (A first pass counting only larger
+// keys, with a read-back of the slot to catch ties, measured slower than the
+// position compare: k=5 4.81 vs 4.57 ms.)
+__device__ __forceinline__ void rank_into(const unsigned long long* LK, int q0, int q1, unsigned long long ck,
+                                          uint32_t cg, int ci, int k, unsigned long long* TK, uint32_t* TG) {
+  const int r = list_rank(LK, q0, q1, ck, ci);
+  if (ck != 0ull && r < k) { TK[r] = ck; TG[r] = cg; }
+}
+
 template <int KT, int WPB, bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(64 * WPB)
 lt_beam_pk(DecodeParams p) {
@@ -1158,6 +1205,10 @@ lt_beam_pk(DecodeParams p) {
   __shared__ uint32_t tgen[WPB][KT];
   constexpr bool USE_D3 = KT <= 4;              // (its 8 KiB would cost a block per CU above)
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
+  // the position's span starts and expansion prefixes, for the decode of an
+  // expansion index (a lane-variable index into wave-uniform values)
+  __shared__ __attribute__((aligned(16))) int sstp[WPB][PK_SPRE ? 12 : 1];
+  __shared__ __attribute__((aligned(16))) int sprep[WPB][PK_SPRE ? 12 : 1];
   Aux aux{nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
 
@@ -1233,12 +1284,28 @@ lt_beam_pk(DecodeParams p) {
       pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)(ss[j + 1] - ss[j]));   // (c <= 256, m < 2^21)
     }
     const int M = pre[MAX_SPAN];
+#if PK_SPRE
+    if (lane <= MAX_SPAN) sstp[wv][lane] = pfs;
+    if (lane == 0) {
+      *reinterpret_cast<int4*>(&sprep[wv][0]) = make_int4(pre[0], pre[1], pre[2], pre[3]);
+      *reinterpret_cast<int4*>(&sprep[wv][4]) = make_int4(pre[4], pre[5], pre[6], pre[7]);
+    }
+    __builtin_amdgcn_wave_barrier();
+#endif
 
     // expansion g -> span slot j (d = 8 - j), hypothesis rank r, candidate i
     // (node ss[j] + i): j is the last slot whose prefix is <= g (pre is
     // nondecreasing), its prefix, size and first node selected by the same
-    // compare
+    // compare -- PK_SPRE: j counted, the three values read from LDS
     auto decode = [&](int g, int& j, int& r, int& i, int& sj) {
+#if PK_SPRE
+      j = 0;
+#pragma unroll
+      for (int q = 1; q < MAX_SPAN; ++q) j += g >= pre[q] ? 1 : 0;
+      const int pj = sprep[wv][j];
+      sj = sstp[wv][j];
+      const int m = sstp[wv][j + 1] - sj;
+#else
       j = 0;
       int pj = pre[0], m = ss[1] - ss[0];
       sj = ss[0];
@@ -1250,6 +1317,7 @@ lt_beam_pk(DecodeParams p) {
         m = ge ? ss[q + 1] - ss[q] : m;
         sj = ge ? ss[q] : sj;
       }
+#endif
       const int local = g - pj;
       // local / m through a float reciprocal (local < 2^24), corrected by one
       r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
@@ -1471,11 +1539,11 @@ lt_beam_pk(DecodeParams p) {
     p.out_len[o] = (int32_t)f.depth;
     int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
     int pos = n, rank = t;
-    for (int step = (int)f.depth - 1; step >= 0; --step) {
+    for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
       const uint32_t v = bp[(int64_t)pos * bstride + rank];
       codes[step] = (int32_t)bp_node(v);
       pos -= (int)bp_d(v);
-      rank = (int)bp_rank(v);
+      rank = min((int)bp_rank(v), k - 1);
     }
     for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;       // padded layout
   }
@@ -1529,6 +1597,7 @@ lt_beam_hw(DecodeParams p) {
   __shared__ unsigned long long tkey[WPB][S][KT];
   __shared__ uint32_t tgen[WPB][S][KT];
   __shared__ __attribute__((aligned(16))) int sst[WPB][S][12];   // each group's span starts of the position
+  __shared__ __attribute__((aligned(16))) int spre[WPB][S][HW_SPRE ? 12 : 1];   // and expansion prefixes
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   Aux aux{nullptr, 0u, p.hk};
@@ -1544,7 +1613,6 @@ lt_beam_hw(DecodeParams p) {
   const int bstride = p.bp_stride;
   const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
-  Counts cnt;
   // this half's sentence (values uniform within the half)
   const bool hv = slot0 + hf < p.n_sent;
   const int s = hv ? p.order[slot0 + hf] : 0;
@@ -1581,6 +1649,7 @@ lt_beam_hw(DecodeParams p) {
     R[0][0] = v_bos(load_cand(B, nbase));
     cnt9[0] = 1;
   }
+  if (HW_SPRE && hl == 0) spre[wv][hf][0] = 0;
   // next position's first STAGE records of every group (chunk c = 64 pl +
   // lane of the wave's stream: group c / CPG, chunk c % CPG of that group's
   // block) and span starts (lane G h + j <= 8: span start j of group h), one
@@ -1633,6 +1702,30 @@ lt_beam_hw(DecodeParams p) {
     const int em9 = e % RING;
     const int A0 = ss[0];
     int pre[MAX_SPAN + 1];
+#if HW_SPRE
+    // span-slot expansion prefix through LDS: lane j < 8 of a group holds
+    // slot j's c_j * m_j, a three-step DPP scan within the group's 16-lane
+    // row makes the inclusive prefix, every lane reads the group's nine
+    // (instead of an eight-step serial prefix in every lane)
+    {
+      int term = 0;
+      if (hl < MAX_SPAN) {
+        const int d = MAX_SPAN - hl;
+        const int c = (live && d <= dmax) ? cnt9[ring_back(em9, d)] : 0;
+        term = (int)__umul24((uint32_t)c, (uint32_t)(sst[wv][hf][hl + 1] - pfs));   // (c <= 256, m < 2^21)
+      }
+      term += __builtin_amdgcn_update_dpp(0, term, 0x111, 0xF, 0xF, true);      // row_shr:1
+      term += __builtin_amdgcn_update_dpp(0, term, 0x112, 0xF, 0xF, true);      // row_shr:2
+      term += __builtin_amdgcn_update_dpp(0, term, 0x114, 0xF, 0xF, true);      // row_shr:4
+      if (hl < MAX_SPAN) spre[wv][hf][hl + 1] = term;
+      __builtin_amdgcn_wave_barrier();
+      const int4 p0 = *reinterpret_cast<const int4*>(&spre[wv][hf][0]);
+      const int4 p1 = *reinterpret_cast<const int4*>(&spre[wv][hf][4]);
+      pre[0] = p0.x; pre[1] = p0.y; pre[2] = p0.z; pre[3] = p0.w;
+      pre[4] = p1.x; pre[5] = p1.y; pre[6] = p1.z; pre[7] = p1.w;
+      pre[8] = spre[wv][hf][8];
+    }
+#else
     pre[0] = 0;
 #pragma unroll
     for (int j = 0; j < MAX_SPAN; ++j) {
@@ -1640,10 +1733,21 @@ lt_beam_hw(DecodeParams p) {
       const int c = (live && d <= dmax) ? cnt9[(e - d) % RING] : 0;
       pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)(ss[j + 1] - ss[j]));   // (c <= 256, m < 2^21)
     }
+#endif
     const int M = pre[MAX_SPAN];                // this half's expansions
     const int Mmax = gmax(M);
 
     auto decode = [&](int g, int& j, int& r, int& i, int& sj) {     // (lt_beam_pk)
+#if HW_SPRE
+      // pre is nondecreasing: the slot is the number of prefixes <= g; its
+      // prefix, first node and size from LDS
+      j = 0;
+#pragma unroll
+      for (int q = 1; q < MAX_SPAN; ++q) j += g >= pre[q] ? 1 : 0;
+      const int pj = spre[wv][hf][j];
+      sj = sst[wv][hf][j];
+      const int m = sst[wv][hf][j + 1] - sj;
+#else
       j = 0;
       int pj = pre[0], m = ss[1] - ss[0];
       sj = ss[0];
@@ -1655,6 +1759,7 @@ lt_beam_hw(DecodeParams p) {
         m = ge ? ss[q + 1] - ss[q] : m;
         sj = ge ? ss[q] : sj;
       }
+#endif
       const int local = g - pj;
       r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
       i = local - r * m;
@@ -1720,18 +1825,7 @@ lt_beam_hw(DecodeParams p) {
         // slots of round 0 (slots past M hold 0 keys)
         const int qe = KTP + ((min(G, max(M - base, 0)) + 3) & ~3);
         const int qmax = gmax(qe);
-        int rank = 0;
-#pragma unroll 2
-        for (int q = KTP; q < qmax; q += 4) {
-          const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
-          const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
-          const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
-          const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
-          const uint32_t gq[4] = {gg.x, gg.y, gg.z, gg.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) rank += (kq[u] > myk[0] || (kq[u] == myk[0] && gq[u] < myg[0])) ? 1 : 0;
-        }
-        if (myk[0] != 0ull && rank < k) { TK[rank] = myk[0]; TG[rank] = myg[0]; }
+        rank_into(LK, KTP, qmax, myk[0], myg[0], KTP + hl, k, TK, TG);
       } else {
         // threshold pruning (lt_beam_pk), per half: tau = the k-th largest of
         // the half's lane maxima
@@ -1768,21 +1862,18 @@ lt_beam_hw(DecodeParams p) {
         const int nc4 = (nc + 3) & ~3;
         if (hl < nc4 - nc) { LK[nc + hl] = 0ull; LG[nc + hl] = INV; }
         const int ncmax = gmax(nc);
-        for (int c0 = 0; c0 < ncmax; c0 += G) {
-          const int c = c0 + hl;
-          const unsigned long long ck = c < nc ? LK[c] : 0ull;
-          const uint32_t cg = c < nc ? LG[c] : INV;
-          int rank = 0;
-          for (int q = 0; q < nc4; q += 4) {
-            const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
-            const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
-            const uint4 gg = *reinterpret_cast<const uint4*>(&LG[q]);
-            const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
-            const uint32_t gq[4] = {gg.x, gg.y, gg.z, gg.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) rank += (kq[u] > ck || (kq[u] == ck && gq[u] < cg)) ? 1 : 0;
+        if (ncmax <= G) {                         // (the usual case: one candidate per lane)
+          const unsigned long long ck = hl < nc ? LK[hl] : 0ull;
+          const uint32_t cg = hl < nc ? LG[hl] : INV;
+          rank_into(LK, 0, nc4, ck, cg, hl, k, TK, TG);
+        } else {
+          for (int c0 = 0; c0 < ncmax; c0 += G) {
+            const int c = c0 + hl;
+            const unsigned long long ck = c < nc ? LK[c] : 0ull;
+            const uint32_t cg = c < nc ? LG[c] : INV;
+            const int rank = list_rank(LK, 0, nc4, ck, c);
+            if (c < nc && rank < k) { TK[rank] = ck; TG[rank] = cg; }
           }
-          if (c < nc && rank < k) { TK[rank] = ck; TG[rank] = cg; }
         }
       }
       nrun = min(k, valid);
@@ -1850,11 +1941,11 @@ lt_beam_hw(DecodeParams p) {
       int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
       const uint32_t* bpg = p.bp + bpo;
       int pos = n, rank = hl;
-      for (int step = (int)f.depth - 1; step >= 0; --step) {
+      for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
         const uint32_t v = bpg[(int64_t)pos * bstride + rank];
         codes[step] = (int32_t)bp_node(v);
         pos -= (int)bp_d(v);
-        rank = (int)bp_rank(v);
+        rank = min((int)bp_rank(v), k - 1);
       }
       for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;     // padded layout
     }
@@ -2309,11 +2400,11 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
       p.out_len[o] = (int32_t)f.depth;
       int pos = n;
       uint32_t rank = (uint32_t)t;
-      for (int step = (int)f.depth - 1; step >= 0; --step) {
+      for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
         const uint64_t v = bp[(int64_t)pos * bstride + rank];
         codes[step] = (int32_t)bpw_node(v);
         pos -= (int)bpw_d(v);
-        rank = bpw_rank(v);
+        rank = min(bpw_rank(v), (uint32_t)k - 1u);
       }
       for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;      // padded layout
     }

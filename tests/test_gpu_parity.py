@@ -88,7 +88,7 @@ def test_kernel_matches_c_oracle_on_synthetic(gpu_decoder, k, n_sent):
     assert (ex, tu) == (o_ex, o_tu)
 
 
-@pytest.mark.parametrize('k', [1, 2, 5])
+@pytest.mark.parametrize('k', [1, 2, 5, 8, 16])
 def test_dense_lattices_with_ties_match_c_oracle(gpu_decoder, k):
     """Dense lattices (about 30 candidates per end position, half of the extra
     ones exact duplicates of the span's first candidate, hence score ties):
