@@ -783,7 +783,7 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #define HW_SPRE 1
 #endif
 #ifndef PK_SPRE
-#define PK_SPRE 0
+#define PK_SPRE 1
 #endif
 constexpr int P_WPB = PK_WPB;           // waves per block
 // k=1 lane-schedule entries (lt_k1_sched)
