@@ -894,7 +894,7 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, int32_t* steps
 }
 
 template <int W, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(64 * P_WPB, (NARROW && W <= 6) ? PK_WAVES : 3)
+__global__ void __launch_bounds__(64 * P_WPB, (NARROW && W <= 8) ? PK_WAVES : 3)
 lt_viterbi_pk(DecodeParams p) {
   constexpr int BPL = PK_BPL;                   // end positions whose backpointer stays in LDS
   __shared__ VEntry ring[P_WPB][W][RING];
@@ -907,7 +907,7 @@ lt_viterbi_pk(DecodeParams p) {
   // the occupancy the launch bounds ask for must fit a CU's 160 KiB of LDS
   // (4 SIMDs x PK_WAVES waves in blocks of P_WPB waves); the LDS window PK_BPL
   // is sized to the last byte of it
-  static_assert(!(NARROW && W <= 6) ||
+  static_assert(!(NARROW && W <= 8) ||
                     (sizeof(ring) + sizeof(bpl) + sizeof(stg) + sizeof(srec) + sizeof(amax) + sizeof(amin) +
                      sizeof(d3l)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
                 "lt_viterbi_pk LDS exceeds the CU's share for PK_WAVES waves per SIMD");

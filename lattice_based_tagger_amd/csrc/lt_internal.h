@@ -179,7 +179,10 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipE
 // k=1 lane schedule of a piece (the kernel's sentence order, K1_W sentences
 // per wave): waves = k1_waves(p.n_sent); steps[w] = macro-steps of wave w
 // (count), then the schedule itself at wave_off (fill).
-constexpr int K1_W = 6;
+#ifndef LT_K1_W
+#define LT_K1_W 6
+#endif
+constexpr int K1_W = LT_K1_W;
 inline int k1_waves(int n_sent) { return (n_sent + K1_W - 1) / K1_W; }
 hipError_t launch_k1_sched_count(const DecodeParams& p, int32_t* steps, hipStream_t st);
 hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st);
