@@ -530,6 +530,8 @@ __device__ __forceinline__ bool v1_hit(const typename Tab<NARROW>::S& s, uint32_
   if constexpr (NARROW) {
     const uint32_t lo = (b << 20) | c;
     const uint32_t hi = (cls_code(cls) << 28) | (a << 8) | (b >> 12);
+    // (two 32-bit compares: the 64-bit compare of the flag-masked key measured
+    // slower here, 0.773 -> 0.781 ms, while it pays in the beams' bm_hit)
     const uint32_t slo = (uint32_t)s.key, shi = (uint32_t)(s.key >> 32) & 0x7FFFFFFFu;
     return (slo == lo) & (shi == hi);
   } else {
@@ -699,7 +701,9 @@ __device__ __forceinline__ bool bm_hit(const typename Tab<NARROW>::S& s, uint32_
   if constexpr (NARROW) {
     const uint32_t lo = (b << 20) | c;
     const uint32_t hi = (cls_code(cls) << 28) | (a << 8) | (b >> 12);
-    return ((uint32_t)s.key == lo) & ((uint32_t)(s.key >> 32) == hi);
+    // one 64-bit compare (was two 32-bit compares and an AND: k=5 4.37 ->
+    // 4.28 ms, k=16 12.08 -> 11.98 ms)
+    return s.key == (((uint64_t)hi << 32) | lo);
   } else {
     return Tab<false>::hit_plain(s, Tab<false>::key(a, b, c, cls));
   }
