@@ -46,6 +46,9 @@ from lattice_based_tagger_amd import _capi, synth  # noqa: E402
 
 METRIC = 'sentences/sec Viterbi decode, 64K-sentence batch; achieved HBM GB/s vs 8 TB/s'
 HBM_PEAK_GBS = 8000.0
+# batch layout of this revision (implicit Unknowns, lattice_decode.h ABI 5): PMC
+# traffic summaries are only matched to a run of the same layout
+LAYOUT = 'abi5-implicit-unk'
 
 
 BASE_SENTENCES = 65536         # lattices generated per seed (config 3); larger batches permute them
@@ -180,18 +183,50 @@ def algorithmic_bytes(piece, n_dict, tuples, length, count, k):
     return 32 * n_dict + int(np.sum(8 * (8 * n + 1) + 4 * 8 * n)) + 24 * tuples + 8 * T * n_dict + out
 
 
-def kernel_bytes(piece, table_loads, k):
-    """Bytes the decode kernel itself issues per launch (not the §8(d)
-    algorithm count): every node record once (48 B), the span starts and
-    per-sentence offsets, 16 B per feature-table slot load (counted by the
-    counting launch: the primary slot of every probe past the pre-filter,
-    the secondary only at flagged slots), the backpointer and padded result
-    writes."""
+PK_BPL = 87                    # k=1: end positions whose backpointers stay in LDS (lt_decode.hip)
+
+
+def kernel_bytes(piece, table_loads, k, prep_bytes, blocks, d3):
+    """The bytes the decode kernel must move per launch -- the roofline's
+    byte model (no kernel reads less): every node record once (48 B; the
+    implicit Unknowns' records are staged from one 384 B block per workgroup),
+    the k=1 lane schedule (``prep_bytes``) or, for beams, the span starts; the
+    per-sentence offsets; 16 B per feature-table slot load actually issued
+    (counted by the counting launch past the node pre-filter); the dense
+    class-3 table staged per workgroup (``blocks`` x 8 KiB, where the model
+    has one, ``d3``, and the kernel stages it); backpointers
+    written and read back in HBM (k=1: only positions past the LDS window);
+    the padded results written."""
     S = piece.n_sent
     n = np.asarray(piece.sent_n, dtype=np.int64)
     chars = int(n.sum())
-    return (48 * piece.n_nodes + 4 * int(len(piece.span_start)) + 36 * S + 16 * table_loads
-            + 4 * int(((n + 1) * k).sum()) + 4 * chars * k + 12 * S * k + 4 * S)
+    if k == 1:
+        meta = 32 * S + prep_bytes                              # order, sent_n, node_off, bp_off, cum_n
+        bp = 8 * int(np.maximum(n - PK_BPL + 1, 0).sum())       # write + backtrace read past the window
+    else:
+        meta = 40 * S + 4 * int(len(piece.span_start))
+        bp = 4 * int(((n + 1) * k).sum()) + 4 * chars * k      # written per (position, rank), read on paths
+    results = 16 * S * k + 4 * chars * k                        # count, length, score; padded codes
+    stage = blocks * (384 + (8192 if d3 and k <= 4 else 0))
+    return 48 * piece.n_nodes + meta + 16 * table_loads + stage + bp + results
+
+
+def has_dense3(keys):
+    """The model gets a dense class-3 table (lt_capi.cpp build_dense3): its
+    class-3 keys' tag values are at most 32."""
+    keys = np.asarray(keys).reshape(-1, 4)
+    c3 = keys[keys[:, 3] == 3]
+    return 0 < len(np.unique(c3[:, :2])) <= 32
+
+
+def workgroups(k, n_sent):
+    """Workgroups of the decode launch (lt_decode.hip launch_k): each stages
+    the dense class-3 table and the implicit-Unknown records."""
+    if k == 1:
+        return -(-n_sent // (6 * 4))                   # W = 6 sentences per wave, 4 waves per block
+    if k <= 8:
+        return -(-n_sent // ((64 // (16 if k <= 3 else 32)) * 4))
+    return -(-n_sent // (1 if k <= 16 else 2))
 
 
 def cpu_baseline(raw, sm, budget_s):
@@ -283,10 +318,11 @@ def cpu_baseline_c(packed, keys, coefs, k, budget_s):
 
 
 def traffic_from_profiles(kernel, k, sentences, features, seed):
-    """HBM bytes per launch of this configuration from the newest committed PMC
-    summary (profiles/*traffic*.json, written by tools/traffic_summary.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
-    FETCH_SIZE doubled per the gfx950 correction), or None."""
+    """Fabric bytes per launch of this configuration from the newest committed
+    PMC summary of this batch layout (profiles/*traffic*.json, written by
+    tools/traffic_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950
+    correction; Infinity-Cache hits included), or None."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*traffic*.json'))):
@@ -295,8 +331,8 @@ def traffic_from_profiles(kernel, k, sentences, features, seed):
         except (OSError, ValueError):
             continue
         for e in entries:
-            if (e.get('kernel'), e.get('k'), e.get('sentences'), e.get('features'), e.get('seed')) == \
-                    (kernel, k, sentences, features, seed):
+            if (e.get('kernel'), e.get('k'), e.get('sentences'), e.get('features'), e.get('seed'),
+                    e.get('layout')) == (kernel, k, sentences, features, seed, LAYOUT):
                 best = (e['traffic_bytes_per_launch'], os.path.relpath(f, ROOT))
     return best
 
@@ -400,7 +436,34 @@ def main():
     elapsed = d.max(t1 - t0)
     kern = ctx.kernel_ms_recent(a.steps)
     gather_ms = comm.gather_ms() if comm else None
-    total_sent = float(a.sentences * a.steps) if strong else d.sum(float(a.sentences * a.steps))
+
+    # fresh batch (k=1): the same step on a batch whose device preparation
+    # (the lane schedule) is not built yet -- what every new chunk of
+    # Tagger.tag_batch costs; lt_batch_reset_prep makes the next decode
+    # rebuild it on the decode stream
+    fresh = None
+    if k == 1:
+        def fresh_step():
+            db.reset_prep()
+            step()
+        for _ in range(max(1, a.warmup)):
+            fresh_step()
+        drain()
+        d.barrier()
+        drain()
+        tf0 = time.perf_counter()
+        for _ in range(a.steps):
+            fresh_step()
+        drain()
+        tf1 = time.perf_counter()
+        d.barrier()
+        fel = d.max(tf1 - tf0)
+        fresh = {'value': total_sent_of(a, d, strong) / fel, 'unit': 'sentences/s',
+                 'ms_per_step': fel / a.steps * 1e3, 'prep_ms_last': db.prep_ms(),
+                 'prep_bytes': db.prep_bytes(),
+                 'step': 'lane-schedule build (lt_k1_sched) + decode + result D2H of a batch not decoded '
+                         'before, batch resident in HBM (H2D excluded, as the headline)'}
+    total_sent = total_sent_of(a, d, strong)
 
     # results of the timed region's last step, checked (untimed)
     check = None
@@ -439,8 +502,12 @@ def main():
     avg_kernel_s = float(np.mean(kern)) / 1e3
     nd = dict_nodes(raw, order, lo, hi)
     B = algorithmic_bytes(piece, nd, tuples, length, count, k)
-    KB = kernel_bytes(piece, table_loads, k)
-    achieved = B / avg_kernel_s / 1e9
+    KB = kernel_bytes(piece, table_loads, k, db.prep_bytes() if k == 1 else 0, workgroups(k, piece.n_sent),
+                      has_dense3(keys))
+    achieved = KB / avg_kernel_s / 1e9
+    # the roofline's byte model is what the kernel must move: it cannot run
+    # faster than HBM moves it
+    assert achieved <= HBM_PEAK_GBS, 'byte model above the HBM peak: %.0f GB/s' % achieved
     al = lambda x: (x + 15) // 16 * 16                      # noqa: E731
     if comm:
         d2h = sum(32 + al(4 * g.n_sent) + al(4 * g.length.size) + al(8 * g.length.size) +
@@ -454,7 +521,7 @@ def main():
         extra = {}
         for kx in extra_ks:
             if kx != k:
-                extra['k%d' % kx] = time_beam(ctx, dm, piece, raw, order, lo, hi, kx, a)
+                extra['k%d' % kx] = time_beam(ctx, dm, piece, raw, order, lo, hi, kx, a, keys)
 
     if root:
         wl = ('config3' if a.sentences == 65536 else 'config4' if a.sentences == 1048576 else 'custom')
@@ -495,28 +562,28 @@ def main():
                 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS,
                 'traffic': traffic[0] if traffic else None,
-                'traffic_unit': 'HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)',
+                'traffic_unit': 'fabric bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE: HBM and '
+                                'Infinity-Cache hits)',
                 'traffic_source': traffic[1] if traffic else None,
-                # the three rates over the same kernel time: algorithmic bytes
-                # (frac: credits every feature tuple of the reference algorithm,
-                # most of which the node pre-filter never loads -- it can pass
-                # 1), bytes the kernel issues, and fabric bytes the counters saw
                 'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
                 'kernel': kernel,
-                'algorithmic_bytes_per_launch': B,
-                'kernel_bytes_per_launch': KB,
-                'kernel_bytes_frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+                'bytes_per_launch': KB,
                 'avg_kernel_ms': avg_kernel_s * 1e3,
                 'launch': 'rank 0 shard' if d.world > 1 else 'whole batch',
-                'frac_note': 'frac = SURVEY 8(d) algorithmic bytes (one 24 B hash slot per reference '
-                             'feature tuple) / kernel time; the kernel resolves feature classes 4-6 '
-                             'per node and class 3 from an LDS table, so it issues fewer bytes and '
-                             'frac can pass 1; kernel_bytes_frac (bytes issued) and traffic_frac '
-                             '(PMC bytes) measure the memory system',
+                'frac_note': 'achieved = bytes the kernel must move per launch (bench.kernel_bytes: node records '
+                             'once, lane schedule, offsets, 16 B per feature-table slot load issued, staged '
+                             'tables, HBM backpointers, results) / average kernel time (HIP events over the '
+                             'timed steps); work_equivalent_frac = SURVEY 8(d) bytes (24 B per reference '
+                             'feature tuple, most never loaded: node pre-filter, class 3 in LDS, classes 4-6 '
+                             'per node) / the same time -- a work rate, not a memory measurement',
+                'work_equivalent_bytes_per_launch': B,
+                'work_equivalent_frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+                'layout': LAYOUT,
             },
             'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                                'table_probes': probes, 'table_slot_loads': table_loads},
             'kernel_only_sentences_per_s': piece.n_sent / avg_kernel_s,
+            'fresh_batch': fresh,
             'd2h': {'bytes_per_step': d2h, 'in_timed_region': True,
                     'how': ('rank 0: every rank\'s packed results (gathered slabs), used bytes to '
                             'pinned host memory on a copy stream' if comm else
@@ -550,7 +617,12 @@ def main():
     d.close()
 
 
-def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a):
+def total_sent_of(a, d, strong):
+    """Sentences all ranks decode in a.steps steps."""
+    return float(a.sentences * a.steps) if strong else d.sum(float(a.sentences * a.steps))
+
+
+def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys):
     """The headline's step (decode + result D2H on the copy stream, batch
     resident in HBM) at beam k on the same batch, same warmup / steps, one
     GPU: BASELINE config 3's k=5 secondary and config 5 (k=16).  Results
@@ -576,7 +648,8 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a):
     kernel = (lib.lt_kernel_name(k) or b'?').decode()
     avg_kernel_s = float(np.mean(kern)) / 1e3
     B = algorithmic_bytes(piece, dict_nodes(raw, order, lo, hi), tuples, length, count, k)
-    KB = kernel_bytes(piece, table_loads, k)
+    KB = kernel_bytes(piece, table_loads, k, 0, workgroups(k, piece.n_sent), has_dense3(keys))
+    assert KB / avg_kernel_s / 1e9 <= HBM_PEAK_GBS, 'byte model above the HBM peak'
     traffic = traffic_from_profiles(kernel, k, piece.n_sent, a.features, a.seed)
     return {
         'beam': k,
@@ -587,10 +660,11 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a):
         'kernel': kernel,
         'avg_kernel_ms': avg_kernel_s * 1e3,
         'kernel_only_sentences_per_s': piece.n_sent / avg_kernel_s,
-        'roofline': {'bound': 'hbm', 'achieved': B / avg_kernel_s / 1e9, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
-                     'algorithmic_bytes_per_launch': B, 'kernel_bytes_per_launch': KB,
-                     'kernel_bytes_frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+        'roofline': {'bound': 'hbm', 'achieved': KB / avg_kernel_s / 1e9, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+                     'bytes_per_launch': KB,
+                     'work_equivalent_bytes_per_launch': B,
+                     'work_equivalent_frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                      'traffic': traffic[0] if traffic else None,
                      'traffic_source': traffic[1] if traffic else None,
                      'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None},

@@ -30,9 +30,11 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 4   /* 2: compact results (slabs), gathers of slabs;
+#define LT_ABI_VERSION 5   /* 2: compact results (slabs), gathers of slabs;
                               3: any max_len / beam (general kernel), lt_trace.exp_link;
-                              4: edge terms (lt_batch_desc.n_edge ...) */
+                              4: edge terms (lt_batch_desc.n_edge ...);
+                              5: implicit Unknown candidates (lt_batch_desc.n_unk ...),
+                                 negative path codes, lt_batch_reset_prep, lt_batch_prep_ms */
 #define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
 #define LT_MAX_BEAM 256    /* largest beam_size of the tuned kernels */
 /* Any other configuration -- max_len > 8 (span slots = max_len) or a beam
@@ -160,15 +162,53 @@ typedef struct {
   const int64_t* sent_edge_off;   /* [n_sent+1] */
   const int64_t* node_edge_base;  /* [n_nodes] */
   const double* edge_val;         /* [n_edge][n_edges] */
+  /* Implicit Unknown candidates (ABI 5).  beam_search synthesises one
+   * Unknown word Word(chars[b:e], chars[b:e], None, 'Unknown', None, e-b, b, e,
+   * False) for every span (b, e) inside the sentence and within max_len that
+   * has no dictionary candidate (beam.py:33-38).  Most lattice spans are such
+   * spans, and the record of a synthesised word whose surface occurs in no
+   * key of the model depends on its length d = e-b alone.  With n_unk = S
+   * (the span slots per end position) an in-range span may hold no node: it
+   * then holds that implicit Unknown, whose record is entry d-1 of the unk_*
+   * arrays (same meaning as the node_* arrays).  n_unk = 0: every in-range
+   * span holds at least one node (the ABI 4 layout).  Not combinable with edge
+   * terms (n_edge > 0).  An implicit Unknown on a decoded path is reported by
+   * the negative code -2 - ((e-1)*S + (S-d)): its span entry in the
+   * sentence's span table (lt_result.codes). */
+  int32_t n_unk;
+  const int32_t* unk_word;        /* [n_unk], entry d-1: span length d */
+  const int32_t* unk_morph0;
+  const int32_t* unk_tag;
+  const uint32_t* unk_mask;
+  const double* unk_pre;
+  const double* unk_f4;
+  const double* unk_f5;
+  const double* unk_f6;
+  const double* unk_post;         /* [n_post][n_unk] or NULL */
 } lt_batch_desc;
 
 /* Copies the batch to the device (H2D) and allocates result buffers for
  * beams up to max_k.  Blocking.  The batch's device buffers are one
  * allocation and its pinned result buffers another; lt_batch_destroy keeps
  * up to two such pairs (each up to 1 GiB) in the ctx for later batches that
- * fit, so per-call decoding frees and allocates nothing. */
+ * fit, so per-call decoding frees and allocates nothing.
+ * Device preparation: the beam-1 decoder reads a lane schedule (which
+ * candidate each lane scores at each step), a function of the lattice shapes
+ * alone.  Its size is counted here on the host and its memory is part of the
+ * batch's allocation; it is built on the device by a kernel -- here, on the
+ * upload stream, when max_k = 1, else queued on the decode stream in front of
+ * the batch's first beam-1 decode.  Neither blocks nor allocates. */
 lt_status lt_batch_create(lt_ctx* ctx, const lt_batch_desc* desc, int max_k, lt_batch** out);
 lt_status lt_batch_destroy(lt_batch* batch);
+/* Benchmark hook: forget the device preparation, so that the next beam-1
+ * decode rebuilds it on the decode stream (a "fresh batch" step). */
+lt_status lt_batch_reset_prep(lt_batch* batch);
+/* Device time (ms, HIP events) of the last device preparation of the batch;
+ * valid once that work is complete (after lt_sync).  0 when none ran. */
+lt_status lt_batch_prep_ms(lt_batch* batch, float* ms);
+/* Bytes of the batch's device preparation (the lane schedules and their wave
+ * offsets) -- what a beam-1 decode reads of them. */
+int64_t lt_batch_prep_bytes(const lt_batch* batch);
 /* Total path-code slots of the results for beam k: k * sum_s n_s. */
 int64_t lt_batch_code_slots(const lt_batch* batch, int k);
 /* Kernel launches per decode of the batch: a batch of any size is decoded in
@@ -201,7 +241,9 @@ const char* lt_kernel_name(int k);
  *   count[s]               number of matures (<= k)
  *   length[s*k + t]        words in mature t, excluding BOS/EOS
  *   score[s*k + t]         float64 path score (after the EOS `+ 0`)
- *   codes[k*off_s + t*n_s + j]  local node index of word j of mature t
+ *   codes[k*off_s + t*n_s + j]  local node index of word j of mature t, or
+ *                          -2 - x for the implicit Unknown of span entry x
+ *                          (lt_batch_desc.n_unk; x = (e-1)*S + (S-d))
  *                          (off_s = sum_{s'<s} n_{s'}); slots j >= length are -1
  * Matures are ordered best first, ties by expansion order (beam.py:85). */
 typedef struct {

@@ -59,6 +59,12 @@ typedef struct {
    * kind MORPH_PREF: (tag, morph) -> value; kind WORD_PREF: (tag, word) -> value */
   lt_strings pref_tag; lt_strings pref_key;
   const int32_t* pref_scorer; const double* pref_value;
+  /* 1: implicit Unknowns (lattice_decode.h n_unk) -- an Unknown whose record
+   * equals the canonical one of its span length (the record of a surface in
+   * no vocabulary entry, class-5 key or preference table) is left out of the
+   * node arrays, and batch.unk_* hold the canonical records.  0: every
+   * Unknown is a node (the ABI 4 layout). */
+  int32_t implicit_unk;
 } lt_packer_desc;
 
 /* Lattices: sentence s has n_s = char_off[s+1] - char_off[s] characters
@@ -79,7 +85,8 @@ typedef struct {
 /* Packed batch.  The arrays belong to `owner`, one block per pack, valid
  * until lt_packed_release (independent of the packer and of later packs, so
  * a pipeline can hold several).  node_src: >= 0 dictionary word index, -1
- * BOS, -2 - (b * 2^32 + d - 1) Unknown node of span (b, b + d).
+ * BOS, -2 - (b * 2^32 + d - 1) Unknown node of span (b, b + d) (an implicit
+ * Unknown is no node: it appears only as a negative path code).
  * batch.max_len is the effective one: min(max_len, max(8, longest sentence))
  * -- spans never exceed the sentence, so the decode is the same -- and the
  * span table has S = max(8, batch.max_len) slots per end position. */

@@ -13,7 +13,7 @@ import numpy as np
 from ._build import LIB
 
 LT_OK = 0
-ABI_VERSION = 4           # include/lattice_decode.h LT_ABI_VERSION
+ABI_VERSION = 5           # include/lattice_decode.h LT_ABI_VERSION
 LT_MAX_BEAM = 256          # tuned kernels (lattice_decode.h)
 LT_MAX_BEAM_ANY = 1 << 20  # the general kernel lt_beam_wide
 LT_EUNSUPPORTED = -4
@@ -22,7 +22,8 @@ _STATUS = {-1: 'LT_EINVAL', -2: 'LT_EHIP', -3: 'LT_ENOMEM', -4: 'LT_EUNSUPPORTED
 EXPORTED_SYMBOLS = (
     'lt_abi_version', 'lt_hash_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
     'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
-    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_batch_pieces', 'lt_set_piece_bytes', 'lt_decode_launch', 'lt_last_kernel_ms',
+    'lt_batch_destroy', 'lt_batch_code_slots', 'lt_batch_pieces', 'lt_set_piece_bytes', 'lt_batch_reset_prep',
+    'lt_batch_prep_ms', 'lt_batch_prep_bytes', 'lt_decode_launch', 'lt_last_kernel_ms',
     'lt_kernel_ms_recent', 'lt_kernel_name',
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
     'lt_result_fetch_packed', 'lt_result_view_packed', 'lt_slab_parse',
@@ -54,7 +55,9 @@ class BatchDesc(C.Structure):
                 ('node_f5', C.c_void_p), ('node_f6', C.c_void_p), ('node_post', C.c_void_p),
                 ('n_edge', C.c_int32), ('n_terms', C.c_int32), ('term_kinds', C.c_uint64),
                 ('n_edges', C.c_int64), ('sent_edge_off', C.c_void_p), ('node_edge_base', C.c_void_p),
-                ('edge_val', C.c_void_p)]
+                ('edge_val', C.c_void_p), ('n_unk', C.c_int32)] + [
+        (f, C.c_void_p) for f in ('unk_word', 'unk_morph0', 'unk_tag', 'unk_mask', 'unk_pre', 'unk_f4',
+                                  'unk_f5', 'unk_f6', 'unk_post')]
 
 
 class Result(C.Structure):
@@ -143,6 +146,9 @@ def load(path=None):
             'lt_batch_code_slots': (i64, [vp, C.c_int]),
             'lt_batch_pieces': (i32, [vp]),
             'lt_set_piece_bytes': (i64, [i64]),
+            'lt_batch_reset_prep': (i32, [vp]),
+            'lt_batch_prep_ms': (i32, [vp, C.POINTER(C.c_float)]),
+            'lt_batch_prep_bytes': (i64, [vp]),
             'lt_decode_launch': (i32, [vp, vp, vp, C.c_int]),
             'lt_last_kernel_ms': (i32, [vp, C.POINTER(C.c_float)]),
             'lt_kernel_ms_recent': (i32, [vp, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
@@ -363,6 +369,8 @@ class DeviceBatch:
     FIELDS = ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start', 'node_word',
               'node_morph0', 'node_tag', 'node_mask', 'node_pre', 'node_f4', 'node_f5',
               'node_f6')
+    UNK_DTYPES = {'unk_word': np.int32, 'unk_morph0': np.int32, 'unk_tag': np.int32, 'unk_mask': np.uint32,
+                  'unk_pre': np.float64, 'unk_f4': np.float64, 'unk_f5': np.float64, 'unk_f6': np.float64}
     DTYPES = {'sent_n': np.int32, 'sent_node_off': np.int64, 'sent_span_off': np.int64,
               'span_start': np.int32, 'node_word': np.int32, 'node_morph0': np.int32,
               'node_tag': np.int32, 'node_mask': np.uint32, 'node_pre': np.float64,
@@ -384,14 +392,22 @@ class DeviceBatch:
             edges = (np.ascontiguousarray(packed.sent_edge_off, dtype=np.int64),
                      np.ascontiguousarray(packed.node_edge_base, dtype=np.int64),
                      np.ascontiguousarray(packed.edge_val, dtype=np.float64))
-        self._keep = (post,) + edges
+        n_unk = int(getattr(packed, 'n_unk', 0))
+        unk = ()
+        if n_unk:                    # implicit Unknowns (lattice_decode.h n_unk)
+            unk = tuple(np.ascontiguousarray(getattr(packed, f), dtype=self.UNK_DTYPES[f])
+                        for f in self.UNK_DTYPES) + (
+                np.ascontiguousarray(packed.unk_post, dtype=np.float64) if n_post else None,)
+        self._keep = (post,) + edges + unk
         desc = BatchDesc(
             self.n_sent, int(packed.max_len), n_post, int(packed.has_trigram),
             int(arr['node_word'].shape[0]), int(arr['span_start'].shape[0]),
             *[_ptr(arr[f]) for f in self.FIELDS], _ptr(post),
             n_edge, int(getattr(packed, 'n_terms', 0)) if n_edge else 0,
             int(getattr(packed, 'term_kinds', 0)) if n_edge else 0,
-            int(edges[2].shape[1]) if n_edge else 0, *[_ptr(x) for x in edges])
+            int(edges[2].shape[1]) if n_edge else 0, *[_ptr(x) for x in edges],
+            n_unk, *([_ptr(x) for x in unk] if n_unk else [None] * 9))
+        self.n_unk = n_unk
         h = C.c_void_p()
         check(ctx._lib.lt_batch_create(ctx.handle, C.byref(desc), int(max_k), C.byref(h)))
         self.handle = h
@@ -406,6 +422,21 @@ class DeviceBatch:
 
     def launch(self, model, k):
         check(self.ctx._lib.held.lt_decode_launch(self.ctx.handle, model.handle, self.handle, int(k)))
+
+    def reset_prep(self):
+        """Forget the device preparation (the k=1 lane schedule): the next
+        beam-1 decode rebuilds it -- a fresh-batch step for benchmarks."""
+        check(self.ctx._lib.lt_batch_reset_prep(self.handle))
+
+    def prep_bytes(self):
+        """Bytes of the device preparation (lane schedules + wave offsets)."""
+        return int(self.ctx._lib.lt_batch_prep_bytes(self.handle))
+
+    def prep_ms(self):
+        """Device time (ms) of the batch's last preparation (after sync)."""
+        v = C.c_float()
+        check(self.ctx._lib.lt_batch_prep_ms(self.handle, C.byref(v)))
+        return float(v.value)
 
     def fetch(self):
         check(self.ctx._lib.held.lt_result_fetch(self.ctx.handle, self.handle))
@@ -464,7 +495,12 @@ class DeviceBatch:
             ns = int(n[s])
             if ns:
                 a = span[span_off[s]:span_off[s] + S * ns + 1]
-                bound[pos_off[s] + 1:pos_off[s] + 1 + ns] = (a[S::S] - a[0:-1:S]) * int(k)
+                cnt = np.diff(a).reshape(ns, S)
+                if self.n_unk:       # an empty in-range span holds its implicit Unknown
+                    e = np.arange(1, ns + 1)[:, None]
+                    d = S - np.arange(S)[None, :]
+                    cnt = np.where((cnt == 0) & (d <= np.minimum(e, self.max_len)), 1, cnt)
+                bound[pos_off[s] + 1:pos_off[s] + 1 + ns] = cnt.sum(axis=1) * int(k)
         exp_off = np.zeros(P + 1, dtype=np.int64)
         np.cumsum(bound, out=exp_off[1:])
         n_exp = int(exp_off[-1])

@@ -21,7 +21,7 @@ import numpy as np
 
 from . import _capi, _pyobj
 from .lowering import LoweredModel
-from .packer import pack
+from .packer import pack, span_slots
 from .tagset import Unk
 from .word import Word, bos_word, eos_word
 
@@ -424,7 +424,6 @@ def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, 
     if objs and hasattr(objs[0], 'src') and hasattr(objs[0], 'words'):      # native packer's views
         return _materialise_bulk(packed, objs, chars_list, T, res, model)
     count, length, score, codes, off = res.count, res.length, res.score, res.codes, res.off
-    masks = np.asarray(packed.node_mask)
     out = []
     for s, chars in enumerate(chars_list):
         n = len(chars)
@@ -433,9 +432,9 @@ def decode_batch(packed, objs, chars_list, model, k, device=0, best_only=False, 
         for t in range(min(int(count[s]), T)):
             a = int(off[s * k + t])
             cs = codes[a:a + int(length[s, t])]
-            path = [nodes[0]] + [nodes[c] for c in cs]
+            path = [nodes[0]] + [nodes[c] for c in cs]       # (a code <= -2: an implicit Unknown)
             if n > 0:
-                hit = bool(np.any(masks[packed.sent_node_off[s] + cs] & _TRI_LOCAL))
+                hit = bool(np.any(packed.masks_of(s, cs) & _TRI_LOCAL))
                 kind = score_kinds(model, 1, [hit], lambda _: path)[0]
                 sc = typed_score(kind, score[s, t])
             else:
@@ -475,8 +474,20 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
     np.cumsum(Lf[:-1], out=first[1:])
     within = np.arange(total, dtype=np.int64) - first[seg]
     local = codes[starts.ravel()[seg] + within].astype(np.int64)
-    glob = packed.sent_node_off[seg // T] + local
+    glob = packed.sent_node_off[seg // T] + np.maximum(local, 0)
     src = objs[0].src[glob]
+    pmask = np.asarray(packed.node_mask)[glob]
+    imp = np.flatnonzero(local < 0)
+    if imp.size:
+        # implicit Unknowns (path code -2 - span entry): the node source code of
+        # their span, -2 - (b << 32 | d - 1), and the canonical mask of d
+        S = span_slots(packed.max_len)
+        x = -2 - local[imp]
+        d = S - x % S
+        b = x // S + 1 - d
+        src = src.copy()
+        src[imp] = -2 - ((b << 32) | (d - 1))
+        pmask[imp] = np.asarray(packed.unk_mask)[d - 1]
     lat = objs[0].words
     ext = _pyobj.load()
     flat = [None] * total
@@ -500,7 +511,7 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
             ext.unknowns(Word, flat, unk, chars, seg[unk] // T, code >> 32, (code & 0xFFFFFFFF) + 1, Unk)
     # the sentinels are immutable tuples: one BOS, one EOS per sentence length
     bos, eos = bos_word(), {}
-    vals = _typed_scores(model, packed, glob, seg, Lf, first, score[:, :T], n, T, bos, flat)
+    vals = _typed_scores(model, pmask, seg, Lf, first, score[:, :T], n, T, bos, flat)
     if T == 1:                                          # best path only (Tagger.tag): paths cut in C
         nl = n.tolist()
         for nch in set(nl):
@@ -525,13 +536,14 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
     return out
 
 
-def _typed_scores(model, packed, glob, seg, Lf, first, score, n, T, bos, flat):
+def _typed_scores(model, pmask, seg, Lf, first, score, n, T, bos, flat):
     """Scores of the S x T paths (flattened) with the reference's types
     (path_score_type): numpy.float64 for every path with a class-4/5 trigram
     feature on some word (all of them in a trained model), the rest
-    replayed; int 0 for an empty sentence."""
+    replayed; int 0 for an empty sentence.  ``pmask``: node_mask of every
+    path word."""
     P = Lf.size
-    hit = np.bincount(seg, weights=(np.asarray(packed.node_mask)[glob] & _TRI_LOCAL) != 0,
+    hit = np.bincount(seg, weights=(pmask & _TRI_LOCAL) != 0,
                       minlength=P) > 0 if P else np.zeros(0, dtype=bool)
     flat_sc = score.reshape(-1)
     empty = np.repeat(n == 0, T)
@@ -588,17 +600,24 @@ def debug_dump(bindex, chars, score_functions, beam_size=5, max_len=8, device=0,
         db.close()
     nodes = objs[0]
     n = len(chars)
+    S = span_slots(packed.max_len)
     paths = {(0, 0): (nodes[0],)}
     off = tr['exp_off']
     node_of = lambda v: v & 0x1FFFFF                # noqa: E731  (csrc/lt_common.h bpw_pack)
     span_of = lambda v: ((v >> 21) & 0x1FFFFF) + 1   # noqa: E731
     rank_of = lambda v: v >> 42                      # noqa: E731
 
+    def word_of(v, e):
+        # the expansion's word ending at e: a node, or (node field UNK_LOCAL,
+        # lt_common.h) the implicit Unknown of its span
+        x = node_of(v)
+        return nodes[x] if x != 0x1FFFFF else nodes[-2 - ((e - 1) * S + (S - span_of(v)))]
+
     def path(pos, rank):
         got = paths.get((pos, rank))
         if got is None:
             v = int(tr['exp_link'][off[pos] + tr['beam_gen'][pos, rank]])
-            got = path(pos - span_of(v), rank_of(v)) + (nodes[node_of(v)],)
+            got = path(pos - span_of(v), rank_of(v)) + (word_of(v, pos),)
             paths[(pos, rank)] = got
         return got
 
@@ -610,7 +629,7 @@ def debug_dump(bindex, chars, score_functions, beam_size=5, max_len=8, device=0,
         sc = tr['exp_score']
         for g in sorted(growns, key=lambda g: -sc[a + g]):      # stable: generation order on ties
             v = int(tr['exp_link'][a + g])
-            words = list(path(e - span_of(v), rank_of(v)) + (nodes[node_of(v)],))
+            words = list(path(e - span_of(v), rank_of(v)) + (word_of(v, e),))
             kind = path_score_type(model, words)
             num_unk = 0
             for w in reversed(words[1:]):

@@ -561,6 +561,14 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
     for (int32_t s = 0; s < d->n_sent; ++s)
       if (d->sent_edge_off[s + 1] < d->sent_edge_off[s]) return fail(LT_EINVAL, "batch: sent_edge_off not monotone");
   }
+  if (d->n_unk != 0) {
+    // implicit Unknowns: one canonical record per span length d = 1..S
+    if (d->n_unk != SS) return fail(LT_EINVAL, "batch: n_unk %d is neither 0 nor the %d span slots", d->n_unk, SS);
+    if (d->n_edge > 0) return fail(LT_EUNSUPPORTED, "batch: implicit Unknowns (n_unk) with edge terms");
+    if (!d->unk_word || !d->unk_morph0 || !d->unk_tag || !d->unk_mask || !d->unk_pre || !d->unk_f4 ||
+        !d->unk_f5 || !d->unk_f6 || (d->n_post > 0 && !d->unk_post))
+      return fail(LT_EINVAL, "batch: NULL implicit-Unknown arrays");
+  }
   if (d->n_span > 0 && !d->span_start) return fail(LT_EINVAL, "batch: NULL span_start");
   if (d->sent_node_off[0] != 0 || d->sent_span_off[0] != 0)
     return fail(LT_EINVAL, "batch: offsets must start at 0");
@@ -608,7 +616,7 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
           const int dd = SS - j;
           if (cnt < 0)
             return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span table not monotone%.0lld%.0lld", s, 0, 0);
-          if (dd <= dmax && cnt == 0)
+          if (dd <= dmax && cnt == 0 && d->n_unk == 0)
             return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span (e=%lld,d=%lld) has no candidate", s, e, dd);
           if (dd > dmax && cnt != 0)
             return note(bad[t], s, LT_EINVAL, "batch: sentence %lld span (e=%lld,d=%lld) is out of range", s, e, dd);
@@ -646,6 +654,20 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
   for (int64_t i = 0; i < (int64_t)d->n_post * d->n_nodes; ++i) {
     if (std::isnan(d->node_post[i])) return fail(LT_EUNSUPPORTED, "batch: NaN post term %lld", (long long)i);
     signs |= inf_sign_bits(d->node_post[i]);
+  }
+  for (int32_t i = 0; i < d->n_unk; ++i) {
+    if (d->unk_word[i] < 0 || d->unk_morph0[i] < 0 || d->unk_tag[i] < 0)
+      return fail(LT_EINVAL, "batch: implicit Unknown %d has a negative id", i);
+    const double v[4] = {d->unk_pre[i], d->unk_f4[i], d->unk_f5[i], d->unk_f6[i]};
+    for (double x : v) {
+      if (std::isnan(x)) return fail(LT_EUNSUPPORTED, "batch: implicit Unknown %d has a NaN score term", i);
+      signs |= inf_sign_bits(x);
+    }
+    for (int32_t t = 0; t < d->n_post; ++t) {
+      const double x = d->unk_post[(int64_t)t * d->n_unk + i];
+      if (std::isnan(x)) return fail(LT_EUNSUPPORTED, "batch: implicit Unknown %d has a NaN post term", i);
+      signs |= inf_sign_bits(x);
+    }
   }
   for (int64_t i = 0; d->n_edge > 0 && i < (int64_t)d->n_edge * d->n_edges; ++i) {
     if (std::isnan(d->edge_val[i])) return fail(LT_EUNSUPPORTED, "batch: NaN edge term %lld", (long long)i);
@@ -712,10 +734,8 @@ static void batch_free(lt_batch* b) {
   for (auto& evs : b->ev_rd)
     for (hipEvent_t ev : evs)
       if (ev) (void)hipEventDestroy(ev);
-  for (lt_piece& pc : b->pieces) {               // the k=1 lane schedules (own allocations)
-    dfree(pc.d_sched);
-    dfree(pc.d_wave_off);
-  }
+  if (b->prep_ev0) (void)hipEventDestroy(b->prep_ev0);
+  if (b->prep_ev1) (void)hipEventDestroy(b->prep_ev1);
   arena_give(b->ctx, b->arena);
   delete b;
 }
@@ -778,6 +798,29 @@ static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc
   }
   if (d->n_sent > s0 || out.empty()) out.emplace_back(s0, d->n_sent);
   return out;
+}
+
+static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p);
+
+// The batch's device preparation, queued on `st` unless done: the k=1 lane
+// schedule of every piece (lt_k1_sched), between the batch's prep events.  No
+// allocation (arena memory) and no wait.
+static hipError_t prep_fill(lt_batch* b, hipStream_t st) {
+  if (!b->has_sched || b->prep_done) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (!b->prep_ev0) e = hipEventCreate(&b->prep_ev0);
+  if (e == hipSuccess && !b->prep_ev1) e = hipEventCreate(&b->prep_ev1);
+  const size_t P = b->pieces.size();
+  for (size_t q = 0; e == hipSuccess && q < P; ++q) {
+    DecodeParams p{};
+    piece_params(b, q, 1, p);
+    p.max_len = b->max_len;
+    p.n_unk = b->n_unk;
+    e = launch_k1_sched_fill(p, b->pieces[q].d_wave_off, b->pieces[q].d_sched, st, q == 0 ? b->prep_ev0 : nullptr,
+                             q + 1 == P ? b->prep_ev1 : nullptr);
+  }
+  if (e == hipSuccess) b->prep_done = true;
+  return e;
 }
 
 // LT_TIMING=1: per-phase wall times of lt_batch_create on stderr (diagnostic)
@@ -863,6 +906,47 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     pc.bp_entries = bp_off[q][n];
     b->bp_entries += pc.bp_entries;
   }
+  // the k=1 lane schedule of every piece (the tuned kernels' layout, max_len
+  // <= 8): each wave's macro-steps counted here from the span tables (threads
+  // over waves), so that the schedule is part of the arena; its entries are
+  // filled on the device (prep_fill)
+  b->has_sched = d->max_len <= MAX_SPAN;
+  b->n_unk = d->n_unk;
+  std::vector<std::vector<int64_t>> wave_off(P);
+  if (b->has_sched) {
+    for (size_t q = 0; q < P; ++q) {
+      lt_piece& pc = b->pieces[q];
+      if (pc.n_nodes >= (int64_t)K1_NODE) {
+        delete b;
+        return fail(LT_EUNSUPPORTED, "lt_batch_create: %lld nodes in one launch piece", (long long)pc.n_nodes);
+      }
+      const int waves = k1_waves(pc.n_sent);
+      std::vector<int64_t>& wo = wave_off[q];
+      wo.assign((size_t)waves + 1, 0);
+      parallel_ranges(waves, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t w = lo; w < hi; ++w) {
+          const int32_t* ssw[K1_W];
+          int nw[K1_W], cnt = 0, nmax = 0;
+          for (int i = 0; i < K1_W && w * K1_W + i < pc.n_sent; ++i, ++cnt) {
+            const int32_t s = pc.s0 + order[q][(size_t)(w * K1_W + i)];
+            ssw[cnt] = d->span_start + d->sent_span_off[s];
+            nw[cnt] = d->sent_n[s];
+            nmax = std::max(nmax, nw[cnt]);
+          }
+          int64_t steps = 0;
+          for (int e = 1; e <= nmax; ++e) {
+            int run = 0;
+            for (int i = 0; i < cnt; ++i)
+              if (e <= nw[i]) run += k1_candidates(ssw[i], e, d->max_len);
+            steps += std::max(1, (run + 63) >> 6);
+          }
+          wo[(size_t)w + 1] = steps;
+        }
+      }, 64);
+      for (int w = 0; w < waves; ++w) wo[(size_t)w + 1] += wo[(size_t)w];
+      pc.sched_steps = wo[(size_t)waves];
+    }
+  }
 
   hipStream_t stm = c->ustream;     // complete when this returns (synchronised below)
   const size_t nres = (size_t)S * max_k;
@@ -870,7 +954,8 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   // the batch's buffers as offsets into one arena
   Carve cv;
   struct PieceOff {
-    size_t order, sent_n, node_off, span_off, bp_off, cum_n, span_start, nodes, post, bp, edge_base, edge_val;
+    size_t order, sent_n, node_off, span_off, bp_off, cum_n, span_start, nodes, post, bp, edge_base, edge_val,
+        sched, wave_off;
   };
   std::vector<PieceOff> po(P);
   for (size_t q = 0; q < P; ++q) {
@@ -882,9 +967,13 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
                      cv.dev((size_t)pc.n_nodes * sizeof(NodeRec)),
                      cv.dev((size_t)d->n_post * (size_t)pc.n_nodes * 8), cv.dev((size_t)pc.bp_entries * 4),
                      cv.dev(ed ? (size_t)pc.n_nodes * 8 : 0),
-                     cv.dev(ed ? (size_t)d->n_edge * (size_t)pc.n_edges * 8 : 0)};
+                     cv.dev(ed ? (size_t)d->n_edge * (size_t)pc.n_edges * 8 : 0),
+                     cv.dev(b->has_sched ? (size_t)std::max<int64_t>(pc.sched_steps, 1) * 64 * 4 : 0),
+                     cv.dev(b->has_sched ? wave_off[q].size() * 8 : 0)};
   }
   const size_t o_sent_n = cv.dev((size_t)S * 4), o_cum_n = cv.dev(((size_t)S + 1) * 8);
+  const size_t o_unk = cv.dev((size_t)d->n_unk * sizeof(NodeRec)),
+               o_unk_post = cv.dev((size_t)d->n_post * (size_t)d->n_unk * 8);
   b->slab_cap = slab_layout(S, max_k, b->total_chars).capacity;
   const uint64_t slab_alloc = slab_alloc_bytes(S, max_k, b->total_chars);
   size_t o_count[2], o_len[2], o_score[2], o_codes[2], o_slab[2];
@@ -927,9 +1016,13 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     pc.d_bp = at<uint32_t>(D, po[q].bp);
     pc.d_edge_base = d->n_edge > 0 ? at<int64_t>(D, po[q].edge_base) : nullptr;
     pc.d_edge_val = d->n_edge > 0 ? at<double>(D, po[q].edge_val) : nullptr;
+    pc.d_sched = at<uint32_t>(D, po[q].sched);
+    pc.d_wave_off = at<int64_t>(D, po[q].wave_off);
   }
   b->d_sent_n = at<int32_t>(D, o_sent_n);
   b->d_cum_n = at<int64_t>(D, o_cum_n);
+  b->d_unk = at<NodeRec>(D, o_unk);
+  b->d_unk_post = at<double>(D, o_unk_post);
   for (int i = 0; i < 2; ++i) {
     b->res[i].count = at<int32_t>(D, o_count[i]);
     b->res[i].len = at<int32_t>(D, o_len[i]);
@@ -987,6 +1080,23 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     }
   }, 256);
   if (timing_on()) t_recs = now_s();
+  // the implicit Unknowns' records, one per span length d (device layout as
+  // the nodes', span-length bits d - 1 up to 8)
+  std::vector<NodeRec> unk_recs((size_t)d->n_unk);
+  for (int32_t i = 0; i < d->n_unk; ++i) {
+    NodeRec& r = unk_recs[(size_t)i];
+    const uint32_t am = d->unk_mask[i];
+    r.word = (uint32_t)d->unk_word[i];
+    r.morph = (uint32_t)d->unk_morph0[i];
+    r.tag = (uint32_t)d->unk_tag[i];
+    r.mask = device_mask(am) | ((uint32_t)(std::min(MAX_SPAN, i + 1) - 1) << D_SHIFT);
+    r.pre = d->unk_pre[i];
+    r.f4 = (am & F_HAS4) ? d->unk_f4[i] : -0.0;
+    r.f5 = (am & F_HAS5) ? d->unk_f5[i] : -0.0;
+    r.f6 = (am & F_HAS6) ? d->unk_f6[i] : -0.0;
+  }
+  up(b->d_unk, unk_recs.data(), unk_recs.size());
+  if (d->n_post > 0) up(b->d_unk_post, d->unk_post, (size_t)d->n_post * (size_t)d->n_unk);
   std::vector<std::vector<int64_t>> edge_base_tmp(P);
   for (size_t q = 0; q < P; ++q) {
     const lt_piece& pc = b->pieces[q];
@@ -1010,7 +1120,11 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       for (int32_t t = 0; t < d->n_edge; ++t)
         up(pc.d_edge_val + (size_t)t * pc.n_edges, d->edge_val + (size_t)t * d->n_edges + pc.edge0, (size_t)pc.n_edges);
     }
+    if (b->has_sched) up(pc.d_wave_off, wave_off[q].data(), wave_off[q].size());
   }
+  // a beam-1 batch gets its lane schedule now, behind its uploads (a
+  // pipeline's upload thread prepares chunk i+1 while chunk i decodes)
+  if (e == hipSuccess && max_k == 1) e = prep_fill(b, stm);
   if (e == hipSuccess) e = hipStreamSynchronize(stm);
   if (e != hipSuccess) {
     batch_free(b);
@@ -1025,6 +1139,27 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
 }
 
 int32_t lt_batch_pieces(const lt_batch* b) { return b ? (int32_t)b->pieces.size() : 0; }
+
+lt_status lt_batch_reset_prep(lt_batch* b) {
+  if (!b) return fail(LT_EINVAL, "lt_batch_reset_prep: NULL batch");
+  b->prep_done = false;
+  return LT_OK;
+}
+
+int64_t lt_batch_prep_bytes(const lt_batch* b) {
+  if (!b || !b->has_sched) return 0;
+  int64_t bytes = 0;
+  for (const lt_piece& pc : b->pieces) bytes += pc.sched_steps * 64 * 4 + ((int64_t)k1_waves(pc.n_sent) + 1) * 8;
+  return bytes;
+}
+
+lt_status lt_batch_prep_ms(lt_batch* b, float* ms) {
+  if (!b || !ms) return fail(LT_EINVAL, "lt_batch_prep_ms: NULL argument");
+  *ms = 0.0f;
+  if (!b->prep_ev0 || !b->prep_ev1) return LT_OK;
+  HIP_TRY(hipEventElapsedTime(ms, b->prep_ev0, b->prep_ev1));
+  return LT_OK;
+}
 
 int64_t lt_set_piece_bytes(int64_t bytes) {
   const int64_t full = ((int64_t)1 << 31) - 1;
@@ -1084,6 +1219,9 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.bp_stride = b->max_k;
   p.counters = c->d_counters;
   p.span_slots = span_slots(b->max_len);
+  p.n_unk = b->n_unk;
+  p.unk = b->d_unk;
+  p.unk_post = b->d_unk_post;
   return LT_OK;
 }
 
@@ -1163,48 +1301,6 @@ static lt_status wide_scratch(lt_ctx* c, const lt_batch* b, int k, DecodeParams&
   return LT_OK;
 }
 
-// The k=1 lane schedule of every piece of b (lt_viterbi_pk reads which node
-// each lane scores at each macro-step): a static function of the lattice
-// shapes, built on the device at the first beam-1 decode of the batch and
-// kept with it.  Counting launch, exact allocation, filling launch.
-static lt_status k1_schedule(lt_ctx* c, lt_batch* b, const DecodeParams& base) {
-  for (size_t q = 0; q < b->pieces.size(); ++q) {
-    lt_piece& pc = b->pieces[q];
-    if (pc.sched_steps >= 0) continue;
-    DecodeParams p = base;
-    piece_params(b, q, 1, p);
-    const int waves = k1_waves(pc.n_sent);
-    std::vector<int32_t> steps((size_t)waves);
-    std::vector<int64_t> off((size_t)waves + 1, 0);
-    int32_t* d_steps = nullptr;
-    hipError_t e = hipMalloc((void**)&d_steps, std::max<size_t>(1, (size_t)waves * 4));
-    if (e == hipSuccess) e = launch_k1_sched_count(p, d_steps, c->stream);
-    if (e == hipSuccess && waves) e = hipMemcpyAsync(steps.data(), d_steps, (size_t)waves * 4, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    dfree(d_steps);
-    for (int w = 0; w < waves; ++w) off[(size_t)w + 1] = off[(size_t)w] + steps[(size_t)w];
-    if (e == hipSuccess) e = hipMalloc((void**)&pc.d_wave_off, ((size_t)waves + 1) * 8);
-    if (e == hipSuccess) e = hipMalloc((void**)&pc.d_sched, std::max<size_t>(1, (size_t)off[(size_t)waves] * 64 * 4));
-    if (e == hipSuccess) e = hipMemcpyAsync(pc.d_wave_off, off.data(), ((size_t)waves + 1) * 8, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) {
-      p.sched = pc.d_sched;
-      p.wave_off = pc.d_wave_off;
-      e = launch_k1_sched_fill(p, pc.d_wave_off, pc.d_sched, c->stream);
-    }
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);      // (off is on this stack)
-    if (e != hipSuccess) {
-      dfree(pc.d_sched);
-      dfree(pc.d_wave_off);
-      pc.d_sched = nullptr;
-      pc.d_wave_off = nullptr;
-      return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "decode: k=1 lane schedule: %s",
-                  hipGetErrorString(e));
-    }
-    pc.sched_steps = off[(size_t)waves];
-  }
-  return LT_OK;
-}
-
 lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
@@ -1212,7 +1308,9 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   HIP_TRY(hipSetDevice(c->device));
   const bool wide = decode_is_wide(b->max_len, k);
   if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
-  if (!wide && beam_template_for(k) == 1 && (st = k1_schedule(c, b, p)) != LT_OK) return st;
+  // the k=1 lane schedule, if the batch has not got it yet: queued in front
+  // of the decode on its stream (lt_batch_create builds it for max_k = 1)
+  if (!wide && beam_template_for(k) == 1) HIP_TRY(prep_fill(b, c->stream));
   if ((st = next_slot(c, b)) != LT_OK) return st;
   const int r = (int)(c->n_launch % lt_ctx::KRING);
   const size_t P = b->pieces.size();
@@ -1556,7 +1654,7 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
     return fail(LT_EUNSUPPORTED, "lt_count_ops: not collected by the general kernel (max_len > %d or beam > %d)",
                 MAX_SPAN, LT_MAX_BEAM_COMPILED);
   HIP_TRY(hipSetDevice(c->device));
-  if (beam_template_for(k) == 1 && (st = k1_schedule(c, b, p)) != LT_OK) return st;
+  if (beam_template_for(k) == 1) HIP_TRY(prep_fill(b, c->stream));
   if ((st = next_slot(c, b)) != LT_OK) return st;
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
 #ifdef PK_PHASES

@@ -240,6 +240,16 @@ LT_HD uint32_t bp_node(uint32_t v) { return v >> 11; }
 LT_HD uint32_t bp_d(uint32_t v) { return ((v >> 8) & 7u) + 1u; }
 LT_HD uint32_t bp_rank(uint32_t v) { return v & 255u; }
 constexpr int64_t MAX_LOCAL_NODES = (int64_t)1 << 21;     // nodes per sentence
+// The node field of a backpointer (and of a decoder's local node) naming the
+// implicit Unknown of the span instead of a node (lattice_decode.h n_unk):
+// local nodes are < MAX_LOCAL_NODES - 1, so the all-ones value is free.
+constexpr uint32_t UNK_LOCAL = (uint32_t)MAX_LOCAL_NODES - 1u;
+// Result code of the implicit Unknown of span (e - d, e), S span slots per
+// end position: -2 - (its entry in the sentence's span table).
+LT_HD int32_t unk_code(int e, int d, int S) { return -2 - ((e - 1) * S + (S - d)); }
+LT_HD int32_t path_code(uint32_t node, int e, int d, int S) {
+  return node == UNK_LOCAL ? unk_code(e, d, S) : (int32_t)node;
+}
 // General-kernel backpointer (two words): local node (21 b) | span d-1 (21 b)
 // | parent rank (22 b) -- spans and beams above the tuned kernels' 3 / 8 bits
 LT_HD uint64_t bpw_pack(uint32_t node, uint32_t d, uint32_t r) {

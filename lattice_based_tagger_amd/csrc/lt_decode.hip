@@ -100,6 +100,34 @@ __device__ __forceinline__ Cand load_cand(const Bufs& B, uint32_t gn) {
   return c;
 }
 
+// The implicit Unknown of span length d (lattice_decode.h n_unk; beam.py:36-38:
+// the synthesised Word of a span with no dictionary candidate).
+__device__ __forceinline__ Cand unk_cand(const DecodeParams& p, int d) {
+  const NodeRec r = p.unk[d - 1];
+  return Cand{r.word, r.morph, r.tag, r.mask, r.pre, r.f4, r.f5, r.f6};
+}
+// Local node `node` of the sentence whose first node is nbase, or (UNK_LOCAL)
+// the implicit Unknown of span length d.
+__device__ __forceinline__ Cand cand_at(const Bufs& B, const DecodeParams& p, uint32_t nbase, uint32_t node, int d) {
+  return node == UNK_LOCAL ? unk_cand(p, d) : load_cand(B, nbase + node);
+}
+// The tuned kernels' copy of the 8 implicit-Unknown records in LDS (record
+// d - 1 at chunks 3(d - 1) .. 3(d - 1) + 2; zeros without implicit Unknowns).
+// Every thread of the block calls it before any early exit.
+__device__ __forceinline__ void stage_unk(const DecodeParams& p, uint4* ul) {
+  if (threadIdx.x < 3 * MAX_SPAN)
+    ul[threadIdx.x] = p.n_unk ? reinterpret_cast<const uint4*>(p.unk)[threadIdx.x] : make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+}
+__device__ __forceinline__ Cand cand_lds(const uint4* q) {
+  const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
+  Cand c;
+  c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
+  c.pre = dbl(q1.x, q1.y); c.f4 = dbl(q1.z, q1.w);
+  c.f5 = dbl(q2.x, q2.y); c.f6 = dbl(q2.z, q2.w);
+  return c;
+}
+
 // Buffer -> LDS DMA of a block of consecutive node records.  A group of G
 // lanes stages the records [first, first + G) of its sentence: instruction p
 // (p = 0..2) has lane l fetch the contiguous 16 B chunk p*G + l of the block,
@@ -460,12 +488,15 @@ __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_
 // inc = ((0 + pre...) + tri) + post...   (score_funcs.py:50-54).  With edge
 // terms (p.n_edge > 0) the terms after `pre` follow the composite's order
 // (term_kinds): the trigram, node-local rows, and edge rows -- the value of the
-// edge from wj (local node jl) to the candidate gn.
+// edge from wj (local node jl) to the candidate gn.  unk_d > 0: the candidate
+// is the implicit Unknown of that span length (its post terms from p.unk_post;
+// a batch with implicit Unknowns has no edge terms).
 __device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c, double tri,
-                                            uint32_t gn, uint32_t jl) {
+                                            uint32_t gn, uint32_t jl, int unk_d = 0) {
   if (p.n_edge == 0) {
     double inc = c.pre + tri;
-    for (int t = 0; t < p.n_post; ++t) inc += p.npost[(int64_t)t * p.n_nodes + gn];
+    for (int t = 0; t < p.n_post; ++t)
+      inc += unk_d ? p.unk_post[(int64_t)t * p.n_unk + unk_d - 1] : p.npost[(int64_t)t * p.n_nodes + gn];
     return inc;
   }
   double inc = c.pre;
@@ -793,8 +824,7 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #define PK_SPRE 1
 #endif
 constexpr int P_WPB = PK_WPB;           // waves per block
-// k=1 lane-schedule entries (lt_k1_sched)
-constexpr uint32_t K1_NODE = 0x03FFFFFFu, K1_IDLE = K1_NODE, K1_FIRST = 0x80000000u;
+// (k=1 lane-schedule entries: K1_* in lt_internal.h)
 
 // Stage the records of the wave's packed candidates (lane l's node gn, INV =
 // none) into wave_planes: the 3 x 64 chunks of 16 B form one stream in lane
@@ -845,18 +875,19 @@ struct alignas(16) SentRec {
 };
 
 // ---------------------------------------------------------------------------
-// The k=1 lane schedule (a static function of the lattice shapes, built once
-// per batch on the device by lt_k1_sched, lt_batch's k1 schedule): the
-// candidates of the W sentences of a wave at end position e form one list in
-// sentence order (sentence w: the X_w candidates of its span starts
-// [A_e, A_{e+1}), generation order within); macro-step r of e covers list
-// entries [64r, 64r + 64).  Entry of lane l at a macro-step: the piece-global
-// node (bits 0-25; K1_IDLE = none), the lane's sentence w (bits 26-28), and
-// bit 31 = the first macro-step of a new end position.
+// The k=1 lane schedule (a static function of the lattice shapes, filled on
+// the device once per batch by lt_k1_sched into memory sized by the host,
+// lt_batch_create): the candidates of the W sentences of a wave at end
+// position e form one list in sentence order, each sentence's in generation
+// order (beam.py:31-42 -- span slot j = 8 - d ascending, i.e. begin ascending;
+// the slot's nodes in bindex order, or its implicit Unknown); macro-step r of
+// e covers list entries [64r, 64r + 64).  Entry of lane l: lt_internal.h K1_*.
 // ---------------------------------------------------------------------------
-template <int W, bool COUNT>
-__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, int32_t* steps, const int64_t* wave_off,
-                                                  uint32_t* sched) {
+template <int W>
+__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
+  static_assert(W < 8, "the sentence field holds W - 1");
+  __shared__ int spre[W][MAX_SPAN + 1];         // sentence w at e: candidate prefix over its span slots
+  __shared__ int sfirst[W][MAX_SPAN + 1];       // and each slot's first piece-global node
   const int wave = blockIdx.x;
   const int lane = (int)threadIdx.x;
   const int slot0 = wave * W;
@@ -870,34 +901,61 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, int32_t* steps
 #pragma unroll
   for (int w = 0; w < W; ++w) nmax = max(nmax, __builtin_amdgcn_readlane(nw, w));
   int64_t step = 0;
-  uint32_t* const out = COUNT ? nullptr : sched + wave_off[wave] * 64 + lane;
+  uint32_t* const out = sched + wave_off[wave] * 64 + lane;
   for (int e = 1; e <= nmax; ++e) {
-    const bool live = own && e <= nw;
-    const int lo = live ? ssp[(e - 1) * MAX_SPAN] : 0;     // first node of end e
-    const int X = live ? ssp[min(e, nw) * MAX_SPAN] - lo : 0;
-    int xs[W], st[W], run = 0;
-    uint32_t bw[W];
+    // the owner lane of each sentence: its slots' candidates and first nodes
+    int X = 0;
+    if (lane < W) {
+      const bool live = own && e <= nw;
+      const int dmax = min(e, p.max_len);
+      int run = 0;
+#pragma unroll
+      for (int j = 0; j <= MAX_SPAN; ++j) {
+        const int a = live ? ssp[(e - 1) * MAX_SPAN + j] : 0;
+        sfirst[lane][j] = (int)nbase + a;
+        spre[lane][j] = run;
+        if (j < MAX_SPAN) {
+          const int c = live ? ssp[(e - 1) * MAX_SPAN + j + 1] - a : 0;
+          run += (live && c == 0 && MAX_SPAN - j <= dmax) ? 1 : c;     // empty in-range slot: implicit Unknown
+        }
+      }
+      X = run;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    int st[W], run = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
-      xs[w] = __builtin_amdgcn_readlane(X, w);
-      bw[w] = (uint32_t)__builtin_amdgcn_readlane((int)(nbase + (uint32_t)lo), w);
       st[w] = run;
-      run += xs[w];
+      run += __builtin_amdgcn_readlane(X, w);
     }
     const int rounds = max(1, (run + 63) >> 6);
-    if (!COUNT) {
-      for (int r = 0; r < rounds; ++r) {
-        const int f = 64 * r + lane;
-        uint32_t ent = K1_IDLE;
+    for (int r = 0; r < rounds; ++r) {
+      const int f = 64 * r + lane;
+      uint32_t ent = K1_IDLE;
+      if (f < run) {
+        // sentence w: the last with st[w] <= f (empty sentences share their
+        // successor's start); its slot j: the last with spre[w][j] <= i
+        int w = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (f >= st[w] && f < st[w] + xs[w]) ent = (bw[w] + (uint32_t)(f - st[w])) | ((uint32_t)w << 26);
-        out[(step + r) * 64] = r == 0 ? (ent | K1_FIRST) : ent;
+        for (int q = 1; q < W; ++q) w += st[q] <= f ? 1 : 0;
+        int sw = st[0];
+#pragma unroll
+        for (int q = 1; q < W; ++q) sw = q == w ? st[q] : sw;
+        const int ix = f - sw;
+        int j = 0;
+#pragma unroll
+        for (int q = 1; q < MAX_SPAN; ++q) j += spre[w][q] <= ix ? 1 : 0;
+        const int a = sfirst[w][j], cnt = sfirst[w][j + 1] - a;
+        ent = cnt == 0 ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - j))                 // d - 1 = 7 - j
+                       : (uint32_t)(a + (ix - spre[w][j]));
+        ent |= (uint32_t)w << 26;
       }
+      out[(step + r) * 64] = r == 0 ? (ent | K1_FIRST) : ent;
     }
     step += rounds;
+    __builtin_amdgcn_wave_barrier();             // the LDS tables are rewritten at the next position
   }
-  if (COUNT && lane == 0) steps[wave] = (int32_t)step;
 }
 
 template <int W, bool NARROW, bool COUNT>
@@ -911,13 +969,15 @@ lt_viterbi_pk(DecodeParams p) {
   __shared__ unsigned long long amax[P_WPB][2][W];
   __shared__ uint32_t amin[P_WPB][2][W];
   __shared__ double d3l[D3_DIM * D3_DIM];
+  __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
   // the occupancy the launch bounds ask for must fit a CU's 160 KiB of LDS
   // (4 SIMDs x PK_WAVES waves in blocks of P_WPB waves); the LDS window PK_BPL
   // is sized to the last byte of it
   static_assert(!(NARROW && W <= 8) ||
                     (sizeof(ring) + sizeof(bpl) + sizeof(stg) + sizeof(srec) + sizeof(amax) + sizeof(amin) +
-                     sizeof(d3l)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
+                     sizeof(d3l) + sizeof(ucan)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
                 "lt_viterbi_pk LDS exceeds the CU's share for PK_WAVES waves per SIMD");
+  stage_unk(p, ucan);
   const Aux aux = stage_aux<NARROW>(p, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -960,10 +1020,11 @@ lt_viterbi_pk(DecodeParams p) {
   const int64_t soff = p.wave_off[wave];
   const int nsteps = (int)(p.wave_off[wave + 1] - soff);
   const uint32_t* const sch = p.sched + soff * 64 + lane;
+  // the node whose record a lane stages (INV: idle, or an implicit Unknown)
   auto node_of = [](uint32_t ent) -> uint32_t {
-    return (ent & K1_NODE) == K1_NODE ? INV : (ent & K1_NODE);
+    return ((ent & K1_NODE) == K1_NODE || (ent & K1_UNK)) ? INV : (ent & K1_NODE);
   };
-  uint32_t ent = sch[0];
+  uint32_t ent = nsteps > 0 ? sch[0] : K1_IDLE;   // (a wave of empty sentences has no step)
   dma_packed(B, node_of(ent), wst, lane);
 
   int e = 0, em9 = 0;
@@ -981,15 +1042,11 @@ lt_viterbi_pk(DecodeParams p) {
     const int dmax = min(e, p.max_len);
     const int cb = e & 1;
     const uint32_t gn0 = node_of(ent);
-    const bool act = gn0 != INV;
+    const bool imp = (ent & K1_UNK) != 0;        // an implicit Unknown (its record from ucan)
+    const bool act = gn0 != INV || imp;
     const int msr = act ? (int)((ent >> 26) & 7u) : 0;
-    Cand cur;                                    // this lane's staged candidate
-    {
-      const uint4 q0 = wst[3 * lane], q1 = wst[3 * lane + 1], q2 = wst[3 * lane + 2];
-      cur.word = q0.x; cur.morph = q0.y; cur.tag = q0.z; cur.mask = q0.w;
-      cur.pre = dbl(q1.x, q1.y); cur.f4 = dbl(q1.z, q1.w);
-      cur.f5 = dbl(q2.x, q2.y); cur.f6 = dbl(q2.z, q2.w);
-    }
+    // this lane's candidate: its staged record, or the implicit Unknown's
+    const Cand cur = cand_lds(imp ? ucan + 3u * (ent & 7u) : wst + 3 * lane);
     const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
     int bm0 = em9 - d0;
     bm0 += bm0 < 0 ? RING : 0;
@@ -1026,33 +1083,35 @@ lt_viterbi_pk(DecodeParams p) {
       v1_second<NARROW>(P, h1, cur);
       const double tri = has_tri ? v1_sum(P.cf, P.pres, cur, h1) : 0.0;
       if (COUNT) v_count(cnt, h1, cur, need, __builtin_popcount(P.gneed) + __builtin_popcount(P.need2));
-      best_s = h1.score + increment(p, cur, tri, gn0, h1.jnode);              // beam.py:115
+      best_s = h1.score + increment(p, cur, tri, gn0, h1.jnode, imp ? d0 : 0);   // beam.py:115
     }
 
     // per-sentence argmax over the macro-steps of e (beam.py:112-116): max
-    // score key, then the min node among the maxima -- a sentence's candidates
-    // of one end position are consecutive nodes in generation order, so the
-    // smallest node is the first generated.  A wave's LDS operations complete
-    // in order, so each read sees the updates issued before it.  A step that
-    // raises a sentence's maximum discards the earlier steps' minimum (it
-    // belonged to a smaller key); ties with an earlier step keep it (earlier
-    // steps hold smaller nodes).
+    // score key, then the min schedule position among the maxima -- the
+    // schedule lists a sentence's candidates of one end position in
+    // generation order over consecutive macro-steps, so the smallest position
+    // (t * 64 + lane) is the first generated.  A wave's LDS operations
+    // complete in order, so each read sees the updates issued before it.  A
+    // step that raises a sentence's maximum discards the earlier steps'
+    // minimum (it belonged to a smaller key); ties with an earlier step keep
+    // it (earlier steps hold smaller positions).
     PK_STAMP(6);                                 // [6] numpy-order sum, increment
+    const uint32_t gk = (uint32_t)t * 64u + (uint32_t)lane;
     const unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
     const unsigned long long mprev = (key && !first) ? amax[wv][cb][msr] : 0ull;
     if (key) __hip_atomic_fetch_max(&amax[wv][cb][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const unsigned long long mk = key ? amax[wv][cb][msr] : 0ull;
     const bool top = key && key == mk;
     if (top && mk != mprev) amin[wv][cb][msr] = INV;
-    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], gn0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], gk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t mgw = top ? amin[wv][cb][msr] : INV;
     if (lane < W) {                              // reset the other parity for the next position
       amax[wv][cb ^ 1][lane] = 0ull;
       amin[wv][cb ^ 1][lane] = INV;
     }
-    if (top && mgw == gn0) {                     // the (step's) winner writes beam[e]
+    if (top && mgw == gk) {                      // the (step's) winner writes beam[e]
       const SentRec si = srec[wv][msr];
-      const uint32_t local = gn0 - si.nbase;
+      const uint32_t local = imp ? UNK_LOCAL : gn0 - si.nbase;
       R[msr][em9] = v_grow<COUNT>(h1, cur, best_s, local);   // Sequence.add (beam.py:112-116)
       const uint32_t bpv = bp_pack(local, (uint32_t)d0, 0u);
       if (e < BPL) {
@@ -1083,7 +1142,7 @@ lt_viterbi_pk(DecodeParams p) {
     // corrupted one from chasing backpointers out of the sentence's rows)
     for (int step = min((int)f.depth, nw) - 1; step >= 0 && pos > 0; --step) {
       const uint32_t v = pos < BPL ? bpl[wv][lane][pos] : bpg[(int64_t)pos * bstride];
-      codes[step] = (int32_t)bp_node(v);
+      codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
       pos -= (int)bp_d(v);
     }
     for (int j = (int)f.depth; j < nw; ++j) codes[j] = -1;      // padded layout
@@ -1216,6 +1275,8 @@ lt_beam_pk(DecodeParams p) {
   // expansion index (a lane-variable index into wave-uniform values)
   __shared__ __attribute__((aligned(16))) int sstp[WPB][PK_SPRE ? 12 : 1];
   __shared__ __attribute__((aligned(16))) int sprep[WPB][PK_SPRE ? 12 : 1];
+  __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
+  stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
 
@@ -1288,7 +1349,8 @@ lt_beam_pk(DecodeParams p) {
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
       const int c = (d <= dmax) ? cnt9[(e - d) % RING] : 0;
-      pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)(ss[j + 1] - ss[j]));   // (c <= 256, m < 2^21)
+      // (an empty in-range slot holds its implicit Unknown)
+      pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)max(ss[j + 1] - ss[j], 1));   // (c <= 256, m < 2^21)
     }
     const int M = pre[MAX_SPAN];
 #if PK_SPRE
@@ -1301,17 +1363,18 @@ lt_beam_pk(DecodeParams p) {
 #endif
 
     // expansion g -> span slot j (d = 8 - j), hypothesis rank r, candidate i
-    // (node ss[j] + i): j is the last slot whose prefix is <= g (pre is
-    // nondecreasing), its prefix, size and first node selected by the same
-    // compare -- PK_SPRE: j counted, the three values read from LDS
-    auto decode = [&](int g, int& j, int& r, int& i, int& sj) {
+    // (node ss[j] + i, or the slot's implicit Unknown: imp): j is the last
+    // slot whose prefix is <= g (pre is nondecreasing), its prefix, size and
+    // first node selected by the same compare -- PK_SPRE: j counted, the three
+    // values read from LDS
+    auto decode = [&](int g, int& j, int& r, int& i, int& sj, bool& imp) {
 #if PK_SPRE
       j = 0;
 #pragma unroll
       for (int q = 1; q < MAX_SPAN; ++q) j += g >= pre[q] ? 1 : 0;
       const int pj = sprep[wv][j];
       sj = sstp[wv][j];
-      const int m = sstp[wv][j + 1] - sj;
+      int m = sstp[wv][j + 1] - sj;
 #else
       j = 0;
       int pj = pre[0], m = ss[1] - ss[0];
@@ -1325,6 +1388,8 @@ lt_beam_pk(DecodeParams p) {
         sj = ge ? ss[q] : sj;
       }
 #endif
+      imp = m == 0;                             // (a slot holding expansion g is in range)
+      m = imp ? 1 : m;
       const int local = g - pj;
       // local / m through a float reciprocal (local < 2^24), corrected by one
       r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
@@ -1345,15 +1410,16 @@ lt_beam_pk(DecodeParams p) {
         const int g = base + 64 * t + lane;
         const bool act = g < M;
         int j = 0, r = 0, i = 0, sj = 0;
-        if (act) decode(g, j, r, i, sj);
+        bool imp = false;
+        if (act) decode(g, j, r, i, sj, imp);
         const int d = MAX_SPAN - j;
         const int node = sj + i;
         const int so = node - A0;
         Cand c;
         if (!act) {
           c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
-        } else if (so < STAGE) {
-          c = read_block<64>(cst, 0, so);
+        } else if (imp || so < STAGE) {
+          c = imp ? cand_lds(ucan + 3 * (d - 1)) : read_block<64>(cst, 0, so);
         } else {
           c = load_cand(B, nbase + (uint32_t)node);
         }
@@ -1370,7 +1436,7 @@ lt_beam_pk(DecodeParams p) {
         if (!skip) {
           const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
           if (COUNT) v_count(cnt, h1, c, need, 2 * __builtin_popcount(P.gneed));
-          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode);   // beam.py:115
+          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
         }
@@ -1506,18 +1572,22 @@ lt_beam_pk(DecodeParams p) {
     uint32_t bpv = 0;
     const bool writer = wl < nrun;
     int wj = 0, wr = 0, wi = 0, wsj = 0;
-    if (writer) decode((int)LG[KTP - nrun + wl], wj, wr, wi, wsj);
-    const int wnode = wsj + wi;
-    const bool far = writer && wnode - A0 >= STAGE;
+    bool wimp = false;
+    if (writer) decode((int)LG[KTP - nrun + wl], wj, wr, wi, wsj, wimp);
+    const int wd = MAX_SPAN - wj;
+    const uint32_t wnode = wimp ? UNK_LOCAL : (uint32_t)(wsj + wi);
+    const bool far = writer && !wimp && (int)wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
-      const int d = MAX_SPAN - wj;
-      ne = v_grow<COUNT>(R[ring_back(em9, d)][wr], c, ord_score(LK[KTP - nrun + wl]), (uint32_t)wnode);
-      bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
+      ne = v_grow<COUNT>(R[ring_back(em9, wd)][wr], c, ord_score(LK[KTP - nrun + wl]), wnode);
+      bpv = bp_pack(wnode, (uint32_t)wd, (uint32_t)wr);
+    };
+    auto near = [&]() {                          // staged record or implicit Unknown
+      return cand_lds(wimp ? ucan + 3 * (wd - 1) : cst + 3 * min((int)wnode - A0, STAGE - 1));
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
-      if (writer) build(read_block<64>(cst, 0, min(wnode - A0, STAGE - 1)));
+      if (writer) build(near());
     } else if (writer) {
-      build(far ? load_cand(B, nbase + (uint32_t)wnode) : read_block<64>(cst, 0, min(wnode - A0, STAGE - 1)));
+      build(far ? load_cand(B, nbase + wnode) : near());
     }
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][wl] = ne;
@@ -1548,7 +1618,7 @@ lt_beam_pk(DecodeParams p) {
     int pos = n, rank = t;
     for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
       const uint32_t v = bp[(int64_t)pos * bstride + rank];
-      codes[step] = (int32_t)bp_node(v);
+      codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
       pos -= (int)bp_d(v);
       rank = min((int)bp_rank(v), k - 1);
     }
@@ -1607,6 +1677,8 @@ lt_beam_hw(DecodeParams p) {
   __shared__ __attribute__((aligned(16))) int spre[WPB][S][HW_SPRE ? 12 : 1];   // and expansion prefixes
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
+  __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
+  stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
 
@@ -1719,7 +1791,8 @@ lt_beam_hw(DecodeParams p) {
       if (hl < MAX_SPAN) {
         const int d = MAX_SPAN - hl;
         const int c = (live && d <= dmax) ? cnt9[ring_back(em9, d)] : 0;
-        term = (int)__umul24((uint32_t)c, (uint32_t)(sst[wv][hf][hl + 1] - pfs));   // (c <= 256, m < 2^21)
+        // (an empty in-range slot holds its implicit Unknown)
+        term = (int)__umul24((uint32_t)c, (uint32_t)max(sst[wv][hf][hl + 1] - pfs, 1));   // (c <= 256, m < 2^21)
       }
       term += __builtin_amdgcn_update_dpp(0, term, 0x111, 0xF, 0xF, true);      // row_shr:1
       term += __builtin_amdgcn_update_dpp(0, term, 0x112, 0xF, 0xF, true);      // row_shr:2
@@ -1738,13 +1811,13 @@ lt_beam_hw(DecodeParams p) {
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
       const int c = (live && d <= dmax) ? cnt9[(e - d) % RING] : 0;
-      pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)(ss[j + 1] - ss[j]));   // (c <= 256, m < 2^21)
+      pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)max(ss[j + 1] - ss[j], 1));   // (c <= 256, m < 2^21)
     }
 #endif
     const int M = pre[MAX_SPAN];                // this half's expansions
     const int Mmax = gmax(M);
 
-    auto decode = [&](int g, int& j, int& r, int& i, int& sj) {     // (lt_beam_pk)
+    auto decode = [&](int g, int& j, int& r, int& i, int& sj, bool& imp) {     // (lt_beam_pk)
 #if HW_SPRE
       // pre is nondecreasing: the slot is the number of prefixes <= g; its
       // prefix, first node and size from LDS
@@ -1753,7 +1826,7 @@ lt_beam_hw(DecodeParams p) {
       for (int q = 1; q < MAX_SPAN; ++q) j += g >= pre[q] ? 1 : 0;
       const int pj = spre[wv][hf][j];
       sj = sst[wv][hf][j];
-      const int m = sst[wv][hf][j + 1] - sj;
+      int m = sst[wv][hf][j + 1] - sj;
 #else
       j = 0;
       int pj = pre[0], m = ss[1] - ss[0];
@@ -1767,6 +1840,8 @@ lt_beam_hw(DecodeParams p) {
         sj = ge ? ss[q] : sj;
       }
 #endif
+      imp = m == 0;                             // (a slot holding expansion g is in range)
+      m = imp ? 1 : m;
       const int local = g - pj;
       r = (int)((float)local * __builtin_amdgcn_rcpf((float)m));
       i = local - r * m;
@@ -1786,19 +1861,16 @@ lt_beam_hw(DecodeParams p) {
         const int g = base + G * t + hl;
         const bool act = g < M;
         int j = 0, r = 0, i = 0, sj = 0;
-        if (act) decode(g, j, r, i, sj);
+        bool imp = false;
+        if (act) decode(g, j, r, i, sj, imp);
         const int d = MAX_SPAN - j;
         const int node = sj + i;
         const int so = node - A0;
         Cand c;
         if (!act) {
           c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
-        } else if (so < STAGE) {
-          const uint4* q = cst + CPG * hf + 3 * so;
-          const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
-          c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
-          c.pre = dbl(q1.x, q1.y); c.f4 = dbl(q1.z, q1.w);
-          c.f5 = dbl(q2.x, q2.y); c.f6 = dbl(q2.z, q2.w);
+        } else if (imp || so < STAGE) {
+          c = cand_lds(imp ? ucan + 3 * (d - 1) : cst + CPG * hf + 3 * so);
         } else {
           c = load_cand(B, nbase + (uint32_t)node);
         }
@@ -1812,7 +1884,7 @@ lt_beam_hw(DecodeParams p) {
         const VEntry h1 = R[hb][hr];
         if (!skip) {
           const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
-          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode);   // beam.py:115
+          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
         }
@@ -1899,27 +1971,22 @@ lt_beam_hw(DecodeParams p) {
     uint32_t bpv = 0;
     const bool writer = live && hl < nrun;
     int wj = 0, wr = 0, wi = 0, wsj = 0;
-    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi, wsj);
-    const int wnode = wsj + wi;
-    const bool far = writer && wnode - A0 >= STAGE;
+    bool wimp = false;
+    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi, wsj, wimp);
+    const int wd = MAX_SPAN - wj;
+    const uint32_t wnode = wimp ? UNK_LOCAL : (uint32_t)(wsj + wi);
+    const bool far = writer && !wimp && (int)wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
-      const int d = MAX_SPAN - wj;
-      ne = v_grow<false>(R[ring_back(em9, d)][wr], c, ord_score(LK[KTP - nrun + hl]), (uint32_t)wnode);
-      bpv = bp_pack((uint32_t)wnode, (uint32_t)d, (uint32_t)wr);
+      ne = v_grow<false>(R[ring_back(em9, wd)][wr], c, ord_score(LK[KTP - nrun + hl]), wnode);
+      bpv = bp_pack(wnode, (uint32_t)wd, (uint32_t)wr);
     };
-    auto staged = [&](int r) {
-      const uint4* q = cst + CPG * hf + 3 * r;
-      const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
-      Cand c;
-      c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
-      c.pre = dbl(q1.x, q1.y); c.f4 = dbl(q1.z, q1.w);
-      c.f5 = dbl(q2.x, q2.y); c.f6 = dbl(q2.z, q2.w);
-      return c;
+    auto near = [&]() {                          // staged record or implicit Unknown
+      return cand_lds(wimp ? ucan + 3 * (wd - 1) : cst + CPG * hf + 3 * min((int)wnode - A0, STAGE - 1));
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
-      if (writer) build(staged(min(wnode - A0, STAGE - 1)));
+      if (writer) build(near());
     } else if (writer) {
-      build(far ? load_cand(B, nbase + (uint32_t)wnode) : staged(min(wnode - A0, STAGE - 1)));
+      build(far ? load_cand(B, nbase + wnode) : near());
     }
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][hl] = ne;
@@ -1950,7 +2017,7 @@ lt_beam_hw(DecodeParams p) {
       int pos = n, rank = hl;
       for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
         const uint32_t v = bpg[(int64_t)pos * bstride + rank];
-        codes[step] = (int32_t)bp_node(v);
+        codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
         pos -= (int)bp_d(v);
         rank = min((int)bp_rank(v), k - 1);
       }
@@ -2117,17 +2184,15 @@ int beam_template_for(int k) {
   return -1;
 }
 
-hipError_t launch_k1_sched_count(const DecodeParams& p, int32_t* steps, hipStream_t st) {
+hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st,
+                                hipEvent_t e0, hipEvent_t e1) {
   const int waves = k1_waves(p.n_sent);
-  if (waves == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_k1_sched<P_W, true>), dim3(waves), dim3(64), 0, st, p, steps, nullptr, nullptr);
-  return hipGetLastError();
-}
-
-hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st) {
-  const int waves = k1_waves(p.n_sent);
-  if (waves == 0) return hipSuccess;
-  hipLaunchKernelGGL((lt_k1_sched<P_W, false>), dim3(waves), dim3(64), 0, st, p, nullptr, wave_off, sched);
+  if (waves == 0) {
+    hipError_t e = e0 ? hipEventRecord(e0, st) : hipSuccess;
+    if (e == hipSuccess && e1) e = hipEventRecord(e1, st);
+    return e;
+  }
+  hipExtLaunchKernelGGL((lt_k1_sched<P_W>), dim3(waves), dim3(64), 0, st, e0, e1, 0, p, wave_off, sched);
   return hipGetLastError();
 }
 
@@ -2191,24 +2256,27 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
       const int d = S - j;
       const int b = e - d;
       const int lo = ssp[(int64_t)(e - 1) * S + j], hi = ssp[(int64_t)(e - 1) * S + j + 1];
+      const bool imp = lo == hi && p.n_unk;     // the span's implicit Unknown (beam.py:36-38)
+      const int hi1 = imp ? lo + 1 : hi;
       const int nb = t.beam_count[po + b];
       for (int r = 0; r < nb; ++r) {
         const Hyp h = read_entry(ent[(int64_t)b * k + r]);
-        for (int node = lo; node < hi; ++node, ++g) {
+        for (int node = lo; node < hi1; ++node, ++g) {
           if (xo + g >= xe) {                   // the caller's slots are too few: report, stop
             t.exp_count[po + e] = -1;
             return;
           }
-          const Cand c = load_cand(B, nbase + (uint32_t)node);
+          const uint32_t nd = imp ? UNK_LOCAL : (uint32_t)node;
+          const Cand c = cand_at(B, p, nbase, nd, d);
           const bool skip = (h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax);   // beam.py:43-45
           double sc = 0.0;
           if (!skip) {
             const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux) : 0.0;
-            sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode);      // beam.py:115
+            sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode, imp ? d : 0);   // beam.py:115
           }
           t.exp_score[xo + g] = sc;
-          t.exp_node[xo + g] = wide ? (uint32_t)node : bp_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
-          if (t.exp_link) t.exp_link[xo + g] = bpw_pack((uint32_t)node, (uint32_t)d, (uint32_t)r);
+          t.exp_node[xo + g] = wide ? nd : bp_pack(nd, (uint32_t)d, (uint32_t)r);
+          if (t.exp_link) t.exp_link[xo + g] = bpw_pack(nd, (uint32_t)d, (uint32_t)r);
           t.exp_skip[xo + g] = skip ? 1 : 0;
         }
       }
@@ -2238,7 +2306,7 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
       const int r = t.exp_link ? (int)bpw_rank(v) : (int)bp_rank(v32);
       const int node = t.exp_link ? (int)bpw_node(v) : (int)bp_node(v32);
       const Entry& h = ent[(int64_t)(e - d) * k + r];
-      const Cand c = load_cand(B, nbase + (uint32_t)node);
+      const Cand c = cand_at(B, p, nbase, (uint32_t)node, d);
       Entry ne;
       ne.score = t.exp_score[xo + bg]; ne.f6 = c.f6;
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
@@ -2347,16 +2415,19 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
       for (int j = S - dmax; j < S; ++j) {      // span j: d = S - j, b = e - d ascending
         const int d = S - j, b = e - d;
         const int lo = ssp[(int64_t)(e - 1) * S + j], hi = ssp[(int64_t)(e - 1) * S + j + 1];
+        const bool imp = lo == hi && p.n_unk;   // the span's implicit Unknown (beam.py:36-38)
+        const int hi1 = imp ? lo + 1 : hi;
         const int bs = b % RW;
         const int nb = cnt[bs];
         for (int r = 0; r < nb; ++r) {
           const Hyp h = read_entry(R[(int64_t)bs * k + r]);
-          for (int node = lo; node < hi; ++node, ++g) {
-            const Cand c = load_cand(B, nbase + (uint32_t)node);
+          for (int node = lo; node < hi1; ++node, ++g) {
+            const uint32_t nd = imp ? UNK_LOCAL : (uint32_t)node;
+            const Cand c = cand_at(B, p, nbase, nd, d);
             if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;    // beam.py:43-45
             const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cn, aux) : 0.0;
-            const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode);   // beam.py:115
-            const WItem it{ord_key(sc), g, (uint32_t)node, (uint32_t)d, (uint32_t)r};
+            const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode, imp ? d : 0);   // beam.py:115
+            const WItem it{ord_key(sc), g, nd, (uint32_t)d, (uint32_t)r};
             if (hn < k) {
               H[hn] = it;
               wheap_up(H, hn);
@@ -2378,7 +2449,7 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
       for (int t = 0; t < hn; ++t) {
         const WItem it = H[t];
         const Entry& h = R[(int64_t)((e - (int)it.d) % RW) * k + it.r];
-        const Cand c = load_cand(B, nbase + it.node);
+        const Cand c = cand_at(B, p, nbase, it.node, (int)it.d);
         Entry ne;
         ne.score = ord_score(it.key); ne.f6 = c.f6;
         ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
@@ -2409,7 +2480,7 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
       uint32_t rank = (uint32_t)t;
       for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
         const uint64_t v = bp[(int64_t)pos * bstride + rank];
-        codes[step] = (int32_t)bpw_node(v);
+        codes[step] = path_code(bpw_node(v), pos, (int)bpw_d(v), S);
         pos -= (int)bpw_d(v);
         rank = min(bpw_rank(v), (uint32_t)k - 1u);
       }

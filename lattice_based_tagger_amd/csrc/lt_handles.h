@@ -53,10 +53,11 @@ struct lt_piece {
   double* d_post = nullptr;
   uint32_t* d_bp = nullptr;
   int64_t edge0 = 0, n_edges = 0;                // the piece's edge values (edge terms)
-  // the k=1 lane schedule (built at the first beam-1 decode, lt_k1_schedule)
-  uint32_t* d_sched = nullptr;                   // [steps * 64]
+  // the k=1 lane schedule (arena memory sized at lt_batch_create; built on the
+  // device by the fill kernel, lt_batch_create or the first beam-1 decode)
+  uint32_t* d_sched = nullptr;                   // [sched_steps * 64]
   int64_t* d_wave_off = nullptr;                 // [waves + 1]
-  int64_t sched_steps = -1;
+  int64_t sched_steps = 0;
   int64_t* d_edge_base = nullptr;                // [n_nodes], rebased to the piece
   double* d_edge_val = nullptr;                  // [n_edge][n_edges]
 };
@@ -69,6 +70,15 @@ struct lt_batch {
   int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
   int inf_signs = 0;                  // +inf (1) / -inf (2) among the node score terms
   int last_k = 0;
+  // implicit Unknown records (lt_batch_desc.n_unk): device AoS [n_unk] with
+  // the span-length bits, post terms [n_post][n_unk]; shared by the pieces
+  int32_t n_unk = 0;
+  lt::NodeRec* d_unk = nullptr;
+  double* d_unk_post = nullptr;
+  // device preparation (the k=1 lane schedules of the pieces): has_sched = the
+  // batch has them (max_len <= 8); prep_done = the fill kernels are queued
+  bool has_sched = false, prep_done = false;
+  hipEvent_t prep_ev0 = nullptr, prep_ev1 = nullptr;   // around the last fill
   // device inputs, per launch piece (lt_batch_create: node records and
   // backpointers of a piece stay below 2^31 B)
   std::vector<lt_piece> pieces;

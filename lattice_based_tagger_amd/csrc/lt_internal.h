@@ -30,6 +30,13 @@ struct DecodeParams {
   const int32_t* span_start;
   const NodeRec* nodes;         // AoS node records; mask + span length bits (D_SHIFT)
   const double* npost;
+  // implicit Unknown candidates (lattice_decode.h n_unk): an in-range span with
+  // no node holds one, whose record is unk[d-1] (d = span length) and whose
+  // node-local post terms are unk_post[t * n_unk + d - 1]; its local node is
+  // UNK_LOCAL.  n_unk = 0: none.
+  int32_t n_unk;
+  const NodeRec* unk;
+  const double* unk_post;
   // edge terms (lt_batch_desc.n_edge; 0 = none): increment = ((pre + t_0) + t_1)...
   int32_t n_edge;
   int32_t n_terms;
@@ -177,14 +184,34 @@ const char* kernel_name_for(int k);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipEvent_t e0 = nullptr,
                          hipEvent_t e1 = nullptr);
 // k=1 lane schedule of a piece (the kernel's sentence order, K1_W sentences
-// per wave): waves = k1_waves(p.n_sent); steps[w] = macro-steps of wave w
-// (count), then the schedule itself at wave_off (fill).
+// per wave): waves = k1_waves(p.n_sent); wave w's macro-steps start at
+// wave_off[w] (counted on the host, k1_wave_steps), the fill kernel writes
+// the entries.  A wave's candidates at end position e: its sentences' in
+// order, each sentence's in generation order (span slot j = 8 - d ascending,
+// the slot's nodes, or its implicit Unknown); 64 per macro-step.
 #ifndef LT_K1_W
 #define LT_K1_W 6
 #endif
 constexpr int K1_W = LT_K1_W;
 inline int k1_waves(int n_sent) { return (n_sent + K1_W - 1) / K1_W; }
-hipError_t launch_k1_sched_count(const DecodeParams& p, int32_t* steps, hipStream_t st);
-hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st);
+// entry of a lane at a macro-step: bits 0-25 the piece-global node (all ones:
+// idle lane) or, with K1_UNK, d - 1 of the lane's implicit Unknown; bits
+// 26-28 the lane's sentence in the wave; bit 31 the first macro-step of a new
+// end position
+constexpr uint32_t K1_NODE = 0x03FFFFFFu, K1_IDLE = K1_NODE, K1_UNK = 0x40000000u, K1_FIRST = 0x80000000u;
+// candidates of a sentence at end position e (1 <= e <= n) from its span
+// table `ss` (8 slots per position): every slot's nodes, and one implicit
+// Unknown for an empty slot within max_len
+__host__ __device__ inline int k1_candidates(const int32_t* ss, int e, int max_len) {
+  const int dmax = e < max_len ? e : max_len;
+  int x = 0;
+  for (int j = 0; j < MAX_SPAN; ++j) {
+    const int c = ss[(e - 1) * MAX_SPAN + j + 1] - ss[(e - 1) * MAX_SPAN + j];
+    x += (c == 0 && MAX_SPAN - j <= dmax) ? 1 : c;
+  }
+  return x;
+}
+hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st,
+                                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 }  // namespace lt

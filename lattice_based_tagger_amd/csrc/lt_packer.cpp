@@ -282,12 +282,18 @@ struct PackOut {
   Arr<int64_t> sent_node_off, sent_span_off, node_src;
   Arr<uint32_t> node_mask;
   Arr<double> node_pre, node_f4, node_f5, node_f6, node_post;
+  // the implicit Unknowns' canonical records (lattice_decode.h n_unk) and the
+  // pass-1 verdict per span entry: 1 = its Unknown is a node
+  Arr<int32_t> unk_word, unk_morph0, unk_tag;
+  Arr<uint32_t> unk_mask;
+  Arr<double> unk_pre, unk_f4, unk_f5, unk_f6, unk_post;
+  Arr<uint8_t> unk_node;
   std::shared_ptr<PackPool> pool;             // while handed out
   size_t bytes() const {
     return sent_n.bytes() + span_start.bytes() + node_word.bytes() + node_morph0.bytes() +
            node_tag.bytes() + sent_node_off.bytes() + sent_span_off.bytes() + node_src.bytes() +
            node_mask.bytes() + node_pre.bytes() + node_f4.bytes() + node_f5.bytes() + node_f6.bytes() +
-           node_post.bytes();
+           node_post.bytes() + unk_node.bytes();
   }
 };
 struct PackPool {
@@ -327,6 +333,7 @@ struct lt_packer {
   CpVocab cpv;                                      // vocab by code points (Unknown nodes)
   bool pref_unk = false;                            // a preference entry for tag 'Unknown'
   bool has_pref = false;                            // any preference entry
+  bool implicit = false;                            // implicit Unknowns (lt_packer_desc.implicit_unk)
 
   int32_t id_of(std::string_view s) const {
     const WordInfo* v = vocab.get(s);
@@ -368,6 +375,7 @@ lt_status lt_packer_create(const lt_packer_desc* d, lt_packer** out) {
     }
     p->n_local = d->n_local;
     p->n_pre = d->n_pre;
+    p->implicit = d->implicit_unk != 0;
     p->kind.assign(d->local_kind, d->local_kind + d->n_local);
     p->reg.assign(d->reg_params, d->reg_params + 3 * (size_t)d->n_local);
     p->pref.resize((size_t)d->n_local);
@@ -421,6 +429,65 @@ double regularization(const double* prm, const NodeView& w) {
 double lookup(std::string& kb, const ViewMap<double>& m, std::string_view t, std::string_view k) {
   const double* v = m.get(tuple_key(kb, t, k));
   return v ? *v : 0.0;
+}
+
+// A node's packed record (packer.py _record: node_record + node_terms).
+struct Rec {
+  int32_t wid, mid, tid;
+  uint32_t m;
+  double pre, f4, f5, f6;
+};
+
+// The record of node w: its word's vocabulary entry wi (null: none), morph0 id
+// mid and tag0 id tid; post[t]: the node-local terms after the trigram.
+// nostr: w's strings equal no preference-table key (the canonical Unknown's
+// surface, packer.py _NOSTR).
+void node_rec(const lt_packer* p, std::string& kb, const NodeView& w, const WordInfo* wi, int32_t mid,
+              int32_t tid, Rec& r, double* post, bool nostr = false) {
+  const int32_t wid = wi ? wi->id : 0;
+  uint32_t m = node_mask(p->vm(wid), p->vm(mid), p->vm(tid));
+  const bool unk_node = w.tag0 == kUnk;
+  if (unk_node) m |= F_UNK;
+  if (contextual(w.tag0)) m |= F_CTX;
+  double f4 = 0.0, f5 = 0.0, f6 = 0.0;
+  if (const double* c = p->c4.get(w.len)) { m |= F_HAS4; f4 = *c; }
+  if (wi) {                                          // (word, tag0, is_l) -> coef
+    for (int32_t j = wi->c5_lo; j < wi->c5_lo + wi->c5_n; ++j) {
+      const C5Entry& c = p->c5e[(size_t)j];
+      if (c.is_l == w.is_l && c.tag == w.tag0) {
+        m |= F_HAS5;
+        f5 = c.coef;
+        break;
+      }
+    }
+  }
+  if (unk_node) {
+    if (const double* c = p->c6.get(w.len < 8 ? w.len : 8)) { m |= F_HAS6; f6 = *c; }
+  }
+  // node-local scorers in constructor order (lowering.node_terms)
+  double pre = 0.0;
+  for (int t = 0; t < p->n_local; ++t) {
+    double v;
+    switch (p->kind[(size_t)t]) {
+      case LT_SCORER_REGULARIZATION: v = regularization(&p->reg[3 * (size_t)t], w); break;
+      case LT_SCORER_MORPH_PREF:                   // score_funcs.py:84-88
+        v = nostr ? 0.0 : lookup(kb, p->pref[(size_t)t], w.tag0, w.morph0);
+        if (w.has_tag1) v = v + (w.has_morph1 ? lookup(kb, p->pref[(size_t)t], w.tag1, w.morph1) : 0.0);
+        break;
+      default:                                     // WordPreference, score_funcs.py:99-100
+        v = nostr ? 0.0 : lookup(kb, p->pref[(size_t)t], w.tag0, w.word);
+    }
+    if (t < p->n_pre) pre = pre + v;
+    else post[t - p->n_pre] = v;
+  }
+  r = Rec{wid, mid, tid, m, pre, f4, f5, f6};
+}
+
+// bit-identical records (floats compared as bit patterns: -0.0 kept)
+bool same_rec(const Rec& a, const double* pa, const Rec& b, const double* pb, int n_post) {
+  return a.wid == b.wid && a.mid == b.mid && a.tid == b.tid && a.m == b.m &&
+         std::memcmp(&a.pre, &b.pre, 4 * sizeof(double)) == 0 &&
+         (n_post == 0 || std::memcmp(pa, pb, (size_t)n_post * sizeof(double)) == 0);
 }
 
 }  // namespace
@@ -535,20 +602,52 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
       return set_error(LT_EINVAL, "lt_packer_pack: bad begin-slot offsets");
   const int n_post = p->n_local - p->n_pre;
 
-  // candidates of span (b, e) in begin slot g: words with w.e == e (beam.py:33),
-  // or one synthesised Unknown node (beam.py:36-38)
+  // dictionary candidates of span (b, e) in begin slot g: words with w.e == e (beam.py:33)
   auto span_count = [&](int64_t g, int32_t e) {
     int64_t c = 0;
     for (int64_t i = slot_off[g]; i < slot_off[g + 1]; ++i) c += L.e(i) == e;
-    return c ? c : 1;
+    return c;
   };
   std::unique_ptr<PackOut> o = p->pool->take();
   if (!o) return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
   o->pool = p->pool;
-  // pass 1: nodes per sentence (threads over sentences) -> offsets
-  // (span entries: SS n + 1 per sentence)
   if (!o->sent_n.alloc(S) || !o->sent_node_off.alloc((int64_t)S + 1) || !o->sent_span_off.alloc((int64_t)S + 1))
     return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
+  // span entries: SS n + 1 per sentence
+  o->sent_span_off[0] = 0;
+  for (int32_t s = 0; s < S; ++s) o->sent_span_off[s + 1] = o->sent_span_off[s] + SS * (char_off[s + 1] - char_off[s]) + 1;
+  const int64_t NSP = o->sent_span_off[S];
+  // implicit Unknowns: the canonical record of every span length (an Unknown
+  // whose surface is in no vocabulary entry: packer.py unknown_records)
+  const bool implicit = p->implicit;
+  const int32_t unk_tid = p->id_of(kUnk);
+  std::vector<Rec> canon;
+  std::vector<double> canon_post;
+  if (implicit) {
+    if (!o->unk_word.alloc(SS) || !o->unk_morph0.alloc(SS) || !o->unk_tag.alloc(SS) || !o->unk_mask.alloc(SS) ||
+        !o->unk_pre.alloc(SS) || !o->unk_f4.alloc(SS) || !o->unk_f5.alloc(SS) || !o->unk_f6.alloc(SS) ||
+        !o->unk_post.alloc((int64_t)n_post * SS))
+      return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
+    canon.resize((size_t)SS);
+    canon_post.assign((size_t)SS * (size_t)n_post, 0.0);
+    std::string kb;
+    static constexpr std::string_view none;
+    for (int d = 1; d <= SS; ++d) {
+      const NodeView u{none, none, kUnk, {}, {}, false, false, (int64_t)d, 0};
+      Rec& r = canon[(size_t)d - 1];
+      node_rec(p, kb, u, nullptr, 0, unk_tid, r, canon_post.data() + (size_t)(d - 1) * n_post, true);
+      o->unk_word[d - 1] = r.wid;
+      o->unk_morph0[d - 1] = r.mid;
+      o->unk_tag[d - 1] = r.tid;
+      o->unk_mask[d - 1] = r.m;
+      o->unk_pre[d - 1] = r.pre;
+      o->unk_f4[d - 1] = r.f4;
+      o->unk_f5[d - 1] = r.f5;
+      o->unk_f6[d - 1] = r.f6;
+      for (int t = 0; t < n_post; ++t) o->unk_post[(int64_t)t * SS + d - 1] = canon_post[(size_t)(d - 1) * n_post + t];
+    }
+    if (!o->unk_node.alloc(NSP)) return set_error(LT_ENOMEM, "lt_packer_pack: out of memory");
+  }
   // words per span (b, d) of a sentence from one pass over its words (a
   // begin slot's words are otherwise rescanned for every end position); too
   // large a table (long sentences at a large max_len): scan as before
@@ -566,35 +665,90 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
       }
     return true;
   };
+  // Unknown nodes by code points (CpVocab) unless a preference scorer has an
+  // entry for the tag 'Unknown' (its value would depend on the string)
+  const bool fast_unk = !p->pref_unk;
+  constexpr int HMAX = 16;
+  // The Unknown of span (b, e) of the sentence at c0 (beam.py:36-38): its
+  // vocabulary entry (null: none), found by the code points of chars[b:e]
+  // (hs: CpVocab hashes of the suffixes ending at e, computed on first use),
+  // or by its UTF-8 string `unk` (built when the fast path cannot answer).
+  struct UnkProbe {
+    uint64_t hs[HMAX + 1];
+    bool hashed = false;
+    bool have_str = false;
+    std::string unk;
+  };
+  auto unk_entry = [&](UnkProbe& u, int64_t c0, int32_t e, int d, const WordInfo*& wi) {
+    const uint32_t* cs = chars + c0;
+    const int32_t b = e - d;
+    if (fast_unk && d <= HMAX) {
+      if (!u.hashed) {
+        uint64_t h = CpVocab::SEED;
+        for (int k = 1; k <= HMAX && k <= e; ++k) {
+          h = CpVocab::step(h, cs[e - k]);
+          u.hs[k] = CpVocab::fin(h, (uint32_t)k);
+        }
+        u.hashed = true;
+      }
+      wi = p->cpv.find(cs + b, (uint32_t)d, u.hs[d]);
+      if (!wi) return;                                  // not a vocabulary string: no string needed
+    }
+    u.unk.clear();
+    for (int32_t x = b; x < e; ++x) utf8_append(u.unk, cs[x]);
+    u.have_str = true;
+    wi = p->vocab.get(u.unk);
+  };
+  // pass 1: nodes per sentence (threads over sentences) -> offsets; with
+  // implicit Unknowns, the verdict on every empty span's Unknown (unk_node)
   parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
     std::vector<uint16_t> tab;
+    std::string kb;
+    std::vector<double> post((size_t)std::max(n_post, 1));
     for (int64_t s = lo; s < hi; ++s) {
       const int64_t c0 = char_off[s];
       const int32_t n = (int32_t)(char_off[s + 1] - c0);
       int64_t cnt = 1;                                    // BOS
-      if (span_table(c0, n, tab)) {
-        for (int32_t e = 1; e <= n; ++e)
-          for (int d = 1; d <= max_len && d <= e; ++d) {
-            const uint16_t t = tab[(size_t)(e - d) * (size_t)max_len + (size_t)(d - 1)];
-            cnt += t ? t : 1;
+      const bool tabbed = span_table(c0, n, tab);
+      uint8_t* const un = implicit ? o->unk_node.data() + o->sent_span_off[s] : nullptr;
+      for (int32_t e = 1; e <= n; ++e) {
+        UnkProbe u;
+        for (int d = std::min<int>(max_len, e); d >= 1; --d) {
+          const int64_t c = tabbed ? tab[(size_t)(e - d) * (size_t)max_len + (size_t)(d - 1)]
+                                   : span_count(c0 + e - d, e);
+          if (c) {
+            cnt += c;
+            continue;
           }
-      } else {
-        for (int32_t e = 1; e <= n; ++e)
-          for (int d = 1; d <= max_len && d <= e; ++d) cnt += span_count(c0 + e - d, e);
+          if (!implicit) {
+            ++cnt;
+            continue;
+          }
+          // the Unknown is implicit iff its record is the canonical one of d
+          const WordInfo* wi = nullptr;
+          u.have_str = false;
+          unk_entry(u, c0, e, d, wi);
+          bool node = false;
+          if (wi || u.have_str) {
+            const std::string_view sv = u.have_str ? std::string_view(u.unk) : std::string_view();
+            const NodeView v{sv, sv, kUnk, {}, {}, false, false, (int64_t)d, 0};
+            Rec r;
+            node_rec(p, kb, v, wi, wi ? wi->id : 0, unk_tid, r, post.data());
+            node = !same_rec(r, post.data(), canon[(size_t)d - 1], canon_post.data() + (size_t)(d - 1) * n_post,
+                             n_post);
+          }
+          un[(e - 1) * SS + (SS - d)] = node ? 1 : 0;
+          cnt += node ? 1 : 0;
+        }
       }
       o->sent_n[s] = n;
       o->sent_node_off[s + 1] = cnt;
-      o->sent_span_off[s + 1] = SS * (int64_t)n + 1;
     }
   }, 256);
   o->sent_node_off[0] = 0;
-  o->sent_span_off[0] = 0;
-  for (int32_t s = 0; s < S; ++s) {
-    o->sent_node_off[s + 1] += o->sent_node_off[s];
-    o->sent_span_off[s + 1] += o->sent_span_off[s];
-  }
+  for (int32_t s = 0; s < S; ++s) o->sent_node_off[s + 1] += o->sent_node_off[s];
   const int64_t N = o->sent_node_off[S];
-  if (!o->span_start.alloc(o->sent_span_off[S]) || !o->node_word.alloc(N) || !o->node_morph0.alloc(N) ||
+  if (!o->span_start.alloc(NSP) || !o->node_word.alloc(N) || !o->node_morph0.alloc(N) ||
       !o->node_tag.alloc(N) || !o->node_mask.alloc(N) || !o->node_pre.alloc(N) || !o->node_f4.alloc(N) ||
       !o->node_f5.alloc(N) || !o->node_f6.alloc(N) || !o->node_src.alloc(N) ||
       !o->node_post.alloc((int64_t)n_post * N))
@@ -604,9 +758,10 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
   PackOut& q = *o;
 
   auto fill = [&](int, int64_t s_lo, int64_t s_hi) {
-    std::string kb, unk;
+    std::string kb;
     typename Src::Buf nbuf;
     std::vector<uint16_t> tab;
+    std::vector<double> post((size_t)std::max(n_post, 1));
     // tags are few: remember the last distinct ones (their strings live in
     // the lattice blobs for the whole call)
     std::string_view memo_s[16];
@@ -622,76 +777,38 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
       }
       return id;
     };
-    auto add_node_wi = [&](int64_t x, const NodeView& w, const WordInfo* wi, int32_t mid, int64_t src) {
-      const int32_t wid = wi ? wi->id : 0, tid = tag_id(w.tag0);
-      uint32_t m = node_mask(p->vm(wid), p->vm(mid), p->vm(tid));
-      const bool unk_node = w.tag0 == kUnk;
-      if (unk_node) m |= F_UNK;
-      if (contextual(w.tag0)) m |= F_CTX;
-      double f4 = 0.0, f5 = 0.0, f6 = 0.0;
-      if (const double* c = p->c4.get(w.len)) { m |= F_HAS4; f4 = *c; }
-      if (wi) {                                          // (word, tag0, is_l) -> coef
-        for (int32_t j = wi->c5_lo; j < wi->c5_lo + wi->c5_n; ++j) {
-          const C5Entry& c = p->c5e[(size_t)j];
-          if (c.is_l == w.is_l && c.tag == w.tag0) {
-            m |= F_HAS5;
-            f5 = c.coef;
-            break;
-          }
-        }
-      }
-      if (unk_node) {
-        if (const double* c = p->c6.get(w.len < 8 ? w.len : 8)) { m |= F_HAS6; f6 = *c; }
-      }
-      // node-local scorers in constructor order (lowering.node_terms)
-      double pre = 0.0;
-      for (int t = 0; t < p->n_local; ++t) {
-        double v;
-        switch (p->kind[(size_t)t]) {
-          case LT_SCORER_REGULARIZATION: v = regularization(&p->reg[3 * (size_t)t], w); break;
-          case LT_SCORER_MORPH_PREF:                   // score_funcs.py:84-88
-            v = lookup(kb, p->pref[(size_t)t], w.tag0, w.morph0);
-            if (w.has_tag1) v = v + (w.has_morph1 ? lookup(kb, p->pref[(size_t)t], w.tag1, w.morph1) : 0.0);
-            break;
-          default:                                     // WordPreference, score_funcs.py:99-100
-            v = lookup(kb, p->pref[(size_t)t], w.tag0, w.word);
-        }
-        if (t < p->n_pre) pre = pre + v;
-        else q.node_post[(int64_t)(t - p->n_pre) * N + x] = v;
-      }
-      q.node_word[x] = wid;
-      q.node_morph0[x] = mid;
-      q.node_tag[x] = tid;
-      q.node_mask[x] = m;
-      q.node_pre[x] = pre;
-      q.node_f4[x] = f4;
-      q.node_f5[x] = f5;
-      q.node_f6[x] = f6;
+    auto put = [&](int64_t x, const Rec& r, int64_t src) {
+      for (int t = 0; t < n_post; ++t) q.node_post[(int64_t)t * N + x] = post[(size_t)t];
+      q.node_word[x] = r.wid;
+      q.node_mask[x] = r.m;
+      q.node_morph0[x] = r.mid;
+      q.node_tag[x] = r.tid;
+      q.node_pre[x] = r.pre;
+      q.node_f4[x] = r.f4;
+      q.node_f5[x] = r.f5;
+      q.node_f6[x] = r.f6;
       q.node_src[x] = src;
     };
-    auto add_node = [&](int64_t x, const NodeView& w, int64_t src) {          // (word and morph0 strings)
-      const WordInfo* wi = p->vocab.get(w.word);
-      const int32_t wid = wi ? wi->id : 0;
-      add_node_wi(x, w, wi, w.morph0.data() == w.word.data() && w.morph0.size() == w.word.size()
-                                ? wid : p->id_of(w.morph0), src);
+    auto add_node_wi = [&](int64_t x, const NodeView& w, const WordInfo* wi, int32_t mid, int64_t src) {
+      Rec r;
+      node_rec(p, kb, w, wi, mid, tag_id(w.tag0), r, post.data());
+      put(x, r, src);
     };
-    // Unknown nodes by code points (CpVocab) unless a preference scorer has an
-    // entry for the tag 'Unknown' (its value would depend on the string)
-    const bool fast_unk = !p->pref_unk;
-    constexpr int HMAX = 16;
-    uint64_t hs[HMAX + 1];
     for (int64_t s = s_lo; s < s_hi; ++s) {
       const int64_t c0 = char_off[s];
       const int32_t n = q.sent_n[s];
       const int64_t base = q.sent_node_off[s];
       int32_t* ss = q.span_start.data() + q.sent_span_off[s];
+      const uint8_t* const un = implicit ? q.unk_node.data() + q.sent_span_off[s] : nullptr;
       NodeView bos{kBOS, kBOS, kBOS, {}, {}, false, false, 0, 0};
-      add_node(base, bos, -1);
+      {
+        const WordInfo* wi = p->vocab.get(bos.word);
+        add_node_wi(base, bos, wi, wi ? wi->id : 0, -1);
+      }
       int32_t local = 1;
-      const uint32_t* cs = chars + c0;
       const bool tabbed = span_table(c0, n, tab);
       for (int32_t e = 1; e <= n; ++e) {
-        bool hashed = false;                          // hs[d]: CpVocab hash of chars[e-d:e]
+        UnkProbe u;
         for (int d = SS; d >= 1; --d) {
           *ss++ = local;
           const int32_t b = e - d;
@@ -709,32 +826,18 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
             ++local;
             any = true;
           }
-          if (!any) {                                   // beam.py:36-38: Unknown chars[b:e]
-            const int64_t src = -2 - (((int64_t)b << 32) | (int64_t)(d - 1));
-            if (fast_unk && d <= HMAX) {
-              if (!hashed) {
-                uint64_t h = CpVocab::SEED;
-                for (int k = 1; k <= HMAX && k <= e; ++k) {
-                  h = CpVocab::step(h, cs[e - k]);
-                  hs[k] = CpVocab::fin(h, (uint32_t)k);
-                }
-                hashed = true;
-              }
-              const WordInfo* wi = p->cpv.find(cs + b, (uint32_t)d, hs[d]);
-              if (!wi) {                               // not a vocabulary string: no string needed
-                static constexpr std::string_view none;
-                NodeView u{none, none, kUnk, {}, {}, false, false, (int64_t)d, 0};
-                add_node_wi(base + local, u, nullptr, 0, src);
-                ++local;
-                continue;
-              }
-            }
-            unk.clear();
-            for (int32_t x = b; x < e; ++x) utf8_append(unk, chars[c0 + x]);
-            NodeView u{unk, unk, kUnk, {}, {}, false, false, (int64_t)d, 0};
-            add_node(base + local, u, src);
-            ++local;
-          }
+          if (any) continue;
+          // beam.py:36-38: Unknown chars[b:e] -- implicit (no node) unless the
+          // pass-1 verdict made it one
+          if (implicit && !un[(e - 1) * SS + (SS - d)]) continue;
+          const int64_t src = -2 - (((int64_t)b << 32) | (int64_t)(d - 1));
+          const WordInfo* wi = nullptr;
+          u.have_str = false;
+          unk_entry(u, c0, e, d, wi);
+          const std::string_view sv = u.have_str ? std::string_view(u.unk) : std::string_view();
+          const NodeView w{sv, sv, kUnk, {}, {}, false, false, (int64_t)d, 0};
+          add_node_wi(base + local, w, wi, wi ? wi->id : 0, src);
+          ++local;
         }
       }
       *ss = local;
@@ -770,6 +873,18 @@ lt_status pack_impl(lt_packer* p, const Src& L, int max_len, lt_packed* out) {
   b.node_f5 = o->node_f5.data();
   b.node_f6 = o->node_f6.data();
   b.node_post = n_post ? o->node_post.data() : nullptr;
+  if (implicit) {
+    b.n_unk = SS;
+    b.unk_word = o->unk_word.data();
+    b.unk_morph0 = o->unk_morph0.data();
+    b.unk_tag = o->unk_tag.data();
+    b.unk_mask = o->unk_mask.data();
+    b.unk_pre = o->unk_pre.data();
+    b.unk_f4 = o->unk_f4.data();
+    b.unk_f5 = o->unk_f5.data();
+    b.unk_f6 = o->unk_f6.data();
+    b.unk_post = n_post ? o->unk_post.data() : nullptr;
+  }
   out->node_src = o->node_src.data();
   out->owner = o.release();
   return LT_OK;

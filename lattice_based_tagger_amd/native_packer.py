@@ -20,7 +20,7 @@ from operator import itemgetter
 import numpy as np
 
 from . import _capi
-from .packer import PackedBatch
+from .packer import PackedBatch, span_slots, unknown_word
 from .tagset import Unk
 from .word import Word, bos_word
 
@@ -46,7 +46,7 @@ class PackerDesc(C.Structure):
                 ('n_local', C.c_int32), ('local_kind', C.c_void_p), ('reg_params', C.c_void_p),
                 ('n_pre', C.c_int32),
                 ('pref_tag', Strings), ('pref_key', Strings), ('pref_scorer', C.c_void_p),
-                ('pref_value', C.c_void_p)]
+                ('pref_value', C.c_void_p), ('implicit_unk', C.c_int32)]
 
 
 class LatticeDesc(C.Structure):
@@ -158,9 +158,10 @@ def _number(v):
 
 
 class NativePacker:
-    """The lowered model in native tables (one per LoweredModel)."""
+    """The lowered model in native tables (one per LoweredModel and
+    ``implicit_unk`` setting: packer.pack's implicit Unknowns)."""
 
-    def __init__(self, model):
+    def __init__(self, model, implicit_unk=True):
         self.lib = _capi.load()
         keep = []
         vocab = [(v, i) for v, i in model.vocab.items() if type(v) is str]
@@ -229,7 +230,7 @@ class NativePacker:
                           self.c6[0].size, _ptr(self.c6[0]), _ptr(self.c6[1]),
                           c5w.c(), c5t.c(), _ptr(c5i), _ptr(c5c),
                           len(funcs), _ptr(kinds), _ptr(reg), len(model.pre_funcs),
-                          pt.c(), pk.c(), _ptr(ps), _ptr(pv))
+                          pt.c(), pk.c(), _ptr(ps), _ptr(pv), 1 if implicit_unk else 0)
         h = C.c_void_p()
         _capi.check(self.lib.lt_packer_create(C.byref(desc), C.byref(h)))
         self.handle = h
@@ -316,11 +317,24 @@ class NativePacker:
             node_post=(arr(b.node_post, C.c_double, npost * N, np.float64).reshape(npost, N)
                        if npost else np.zeros((0, N))),
         )
+        nu = int(b.n_unk)
+        batch.unk_n = nu
+        if nu:                                  # implicit Unknowns (lattice_decode.h n_unk)
+            batch.unk_word = arr(b.unk_word, C.c_int32, nu, np.int32)
+            batch.unk_morph0 = arr(b.unk_morph0, C.c_int32, nu, np.int32)
+            batch.unk_tag = arr(b.unk_tag, C.c_int32, nu, np.int32)
+            batch.unk_mask = arr(b.unk_mask, C.c_uint32, nu, np.uint32)
+            batch.unk_pre = arr(b.unk_pre, C.c_double, nu, np.float64)
+            batch.unk_f4 = arr(b.unk_f4, C.c_double, nu, np.float64)
+            batch.unk_f5 = arr(b.unk_f5, C.c_double, nu, np.float64)
+            batch.unk_f6 = arr(b.unk_f6, C.c_double, nu, np.float64)
+            batch.unk_post = (arr(b.unk_post, C.c_double, npost * nu, np.float64).reshape(npost, nu)
+                              if npost else np.zeros((0, nu)))
         src = arr(out.node_src, C.c_int64, N, np.int64)
         if S == 0:
             batch.sent_node_off = np.zeros(1, np.int64)
             batch.sent_span_off = np.zeros(1, np.int64)
-        return batch, _Views(src, batch.sent_node_off, words, chars_l)
+        return batch, _Views(src, batch.sent_node_off, words, chars_l, span_slots(int(b.max_len)))
 
     def close(self):
         if self.handle:
@@ -338,8 +352,9 @@ class _Views:
     """Per-sentence node views of a pack (sentence s -> _NodeView), made on
     access: ``views[s][i]`` is the Word of sentence s's local node i."""
 
-    def __init__(self, src, node_off, words, chars_l):
+    def __init__(self, src, node_off, words, chars_l, S=8):
         self.src, self.node_off, self.words, self.chars_l = src, node_off, words, chars_l
+        self.S = S
 
     def __len__(self):
         return len(self.node_off) - 1
@@ -349,7 +364,8 @@ class _Views:
             s += len(self)
         if not 0 <= s < len(self):
             raise IndexError(s)
-        return _NodeView(self.src, int(self.node_off[s]), int(self.node_off[s + 1]), self.words, self.chars_l, s)
+        return _NodeView(self.src, int(self.node_off[s]), int(self.node_off[s + 1]), self.words, self.chars_l, s,
+                         self.S)
 
     def __iter__(self):
         for s in range(len(self)):
@@ -357,11 +373,12 @@ class _Views:
 
 
 class _NodeView:
-    """Lazy local-node -> Word object of one sentence (as packer.pack's lists)."""
+    """Lazy local-node -> Word object of one sentence (as packer.pack's lists;
+    a negative index is the path code of an implicit Unknown)."""
 
-    def __init__(self, src, lo, hi, words, chars_l, s):
+    def __init__(self, src, lo, hi, words, chars_l, s, S=8):
         self.src, self.lo, self.hi, self.words = src, lo, hi, words
-        self._chars_l, self._s = chars_l, s
+        self._chars_l, self._s, self.S = chars_l, s, S
 
     @property
     def chars(self):
@@ -372,6 +389,8 @@ class _NodeView:
 
     def __getitem__(self, i):
         i = int(i)
+        if i <= -2:
+            return unknown_word(self.chars, i, self.S)
         if not 0 <= i < self.hi - self.lo:
             raise IndexError(i)
         v = int(self.src[self.lo + i])
@@ -385,14 +404,16 @@ class _NodeView:
         return Word(sub, sub, None, Unk, None, d, b, b + d, False)
 
 
-def packer_for(model):
+def packer_for(model, implicit_unk=True):
     """The model's NativePacker (cached on the LoweredModel), or None when
     the model cannot be represented natively."""
-    np_ = getattr(model, '_native_packer', False)
+    cache = model.__dict__.setdefault('_native_packers', {})
+    key = bool(implicit_unk)
+    np_ = cache.get(key, False)
     if np_ is False:
         try:
-            np_ = NativePacker(model)
+            np_ = NativePacker(model, key)
         except Unsupported:
             np_ = None
-        model._native_packer = np_
+        cache[key] = np_
     return np_

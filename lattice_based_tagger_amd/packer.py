@@ -27,10 +27,22 @@ layout described in DESIGN.md §Data layout:
   predecessor local node j, ``node_edge_base = base`` (``sent_edge_off``
   delimits each sentence's block).
 
+* implicit Unknowns (``implicit_unk``, lattice_decode.h ``n_unk``): the
+  synthesised Unknown of a span is not stored as a node when its record
+  equals the *canonical* record of its length d -- the record of an Unknown
+  whose surface occurs in no key of the model and in no preference table
+  (``unknown_records``).  Its span then holds no node, and the decoder takes
+  the record from ``unk_*[d-1]``; a path through it reports the negative code
+  ``-2 - span_entry`` (``unknown_word`` rebuilds its Word).  Most spans of a
+  lattice are such spans.  Not with edge terms or user node-local plugins
+  (whose values the canonical record could not stand for).
+
 The packer never reorders candidates: duplicates, ``len != e-b`` nodes and
 nodes filed under a begin slot other than their ``b`` field are kept exactly
 as the reference would see them.
 """
+
+import struct
 
 import numpy as np
 
@@ -77,6 +89,31 @@ class PackedBatch:
 
     NODE_FIELDS = ('node_word', 'node_morph0', 'node_tag', 'node_mask', 'node_pre', 'node_f4',
                    'node_f5', 'node_f6')
+    UNK_FIELDS = ('unk_word', 'unk_morph0', 'unk_tag', 'unk_mask', 'unk_pre', 'unk_f4', 'unk_f5',
+                  'unk_f6', 'unk_post')
+
+    @property
+    def n_unk(self):
+        return int(getattr(self, 'unk_n', 0))
+
+    def _unk_of(self, out):
+        """The implicit-Unknown records (batch-wide) into a sub-batch's fields."""
+        out['unk_n'] = self.n_unk
+        if self.n_unk:
+            for f in self.UNK_FIELDS:
+                out[f] = getattr(self, f)
+
+    def masks_of(self, s, codes):
+        """node_mask of the path codes of sentence s (an implicit Unknown's
+        from unk_mask)."""
+        codes = np.asarray(codes, dtype=np.int64)
+        m = np.asarray(self.node_mask)[self.sent_node_off[s] + np.maximum(codes, 0)]
+        neg = codes < 0
+        if neg.any():
+            S = span_slots(self.max_len)
+            m = m.copy()
+            m[neg] = np.asarray(self.unk_mask)[S - 1 - ((-2 - codes[neg]) % S)]
+        return m
 
     @property
     def n_edge(self):
@@ -115,6 +152,7 @@ class PackedBatch:
         for f in self.NODE_FIELDS:
             out[f] = getattr(self, f)[n0:n1]
         self._edges_of(out, np.arange(n0, n1), np.arange(s0, s1))
+        self._unk_of(out)
         return PackedBatch(**out)
 
     # backpointer bytes of one launch: lt_batch_create takes sum_s (n_s + 1) * k
@@ -164,6 +202,7 @@ class PackedBatch:
         for f in self.NODE_FIELDS:
             out[f] = getattr(self, f)[ni]
         self._edges_of(out, ni, order)
+        self._unk_of(out)
         return PackedBatch(**out)
 
 
@@ -199,14 +238,87 @@ def node_record(model, w):
     return wid, mid, tid, m, c4, c5, c6
 
 
-def pack(sentences, model, max_len=8):
+class _NoString:
+    """A surface equal to no value of any key or table (the canonical
+    Unknown's, ``unknown_records``)."""
+    __slots__ = ()
+
+    def __eq__(self, other):
+        return self is other
+
+    def __hash__(self):
+        return 0x5EED
+
+
+_NOSTR = _NoString()
+KNOWN_NODE_SCORERS = ('RegularizationScore', 'MorphemePreferenceScore', 'WordPreferenceScore')
+
+
+def implicit_unk_ok(model):
+    """True when the model's Unknown records can stand for each other:
+    no edge terms, and node-local terms only from the three built-in scorers
+    (whose value for an Unknown depends on its length and on table entries
+    for its surface -- which ``_same_record`` then sees)."""
+    if getattr(model, 'n_edge', 0):
+        return False
+    return all(type(f).__name__ in KNOWN_NODE_SCORERS for f in list(model.pre_funcs) + list(model.post_funcs))
+
+
+def _record(model, w):
+    """(wid, mid, tid, mask, pre, f4, f5, f6, post) of node w, as pack stores it."""
+    wid, mid, tid, m, c4, c5, c6 = node_record(model, w)
+    p, q = model.node_terms(w)
+    return (wid, mid, tid, m, float(p), 0.0 if c4 is None else c4, 0.0 if c5 is None else c5,
+            0.0 if c6 is None else c6, [float(v) for v in q])
+
+
+def _bits(rec):
+    """A record with its floats as bit patterns (exact equality, -0.0 kept)."""
+    f = lambda v: struct.pack('<d', v)       # noqa: E731
+    return rec[:4] + tuple(f(v) for v in rec[4:8]) + tuple(f(v) for v in rec[8])
+
+
+def unknown_records(model, S):
+    """The canonical implicit-Unknown records of span lengths d = 1..S: the
+    record of Word(x, x, None, 'Unknown', None, d, ..., False) for a surface x
+    equal to nothing the model holds (id 0, no class-5 feature, no
+    preference-table value)."""
+    return [_record(model, Word(_NOSTR, _NOSTR, None, Unk, None, d, 0, d, False)) for d in range(1, S + 1)]
+
+
+def unknown_word(chars, code, S):
+    """The Word of the implicit Unknown with path code ``code`` (<= -2) in a
+    sentence of characters ``chars`` (beam.py:36-38)."""
+    x = -2 - int(code)
+    e = x // S + 1
+    d = S - x % S
+    b = e - d
+    sub = chars[b:e]
+    return Word(sub, sub, None, Unk, None, d, b, e, False)
+
+
+class SentNodes(list):
+    """Local node -> Word of one packed sentence (``pack``'s node_objects[s]);
+    a negative index is a path code of an implicit Unknown (``unknown_word``),
+    not Python's from-the-end indexing."""
+    __slots__ = ('chars', 'S')
+
+    def __getitem__(self, i):
+        if not isinstance(i, slice) and i < 0:
+            return unknown_word(self.chars, i, self.S)
+        return list.__getitem__(self, i)
+
+
+def pack(sentences, model, max_len=8, implicit_unk=True):
     """Pack ``sentences`` = iterable of ``(bindex, chars)``.
 
     Returns ``(PackedBatch, node_objects)`` where ``node_objects[s][i]`` is the
     Python node behind local node ``i`` of sentence ``s`` (the original
-    object for dictionary nodes).  Raises ``IndexError`` for a sentence whose
-    ``bindex`` is shorter than its character count, as the reference does
-    (`beam.py:32`).
+    object for dictionary nodes; ``node_objects[s][code]`` for the negative
+    path code of an implicit Unknown).  Raises ``IndexError`` for a sentence
+    whose ``bindex`` is shorter than its character count, as the reference
+    does (`beam.py:32`).  ``implicit_unk``: leave out the Unknowns whose
+    record is the canonical one of their length (module docstring).
     """
     sentences = list(sentences)
     max_len = effective_max_len(max_len, [len(chars) for _, chars in sentences])
@@ -215,6 +327,9 @@ def pack(sentences, model, max_len=8):
     n_edge = model.n_edge
     edge_vals = [[] for _ in range(n_edge)]
     edge_base, edge_off = [], [0]
+    implicit = bool(implicit_unk) and implicit_unk_ok(model)
+    canon = unknown_records(model, S) if implicit else []
+    canon_bits = [_bits(r) for r in canon]
 
     sent_n, node_off, span_off = [], [0], [0]
     span_start = []
@@ -223,27 +338,27 @@ def pack(sentences, model, max_len=8):
     post = [[] for _ in range(n_post)]
     node_objects = []
 
-    def add_node(w):
-        wid, mid, tid, m, c4, c5, c6 = node_record(model, w)
-        p, q = model.node_terms(w)
+    def add_record(rec):
+        wid, mid, tid, m, p, c4, c5, c6, q = rec
         words.append(wid)
         morphs.append(mid)
         tags.append(tid)
         masks.append(m)
-        pre.append(float(p))
-        f4.append(0.0 if c4 is None else c4)
-        f5.append(0.0 if c5 is None else c5)
-        f6.append(0.0 if c6 is None else c6)
+        pre.append(p)
+        f4.append(c4)
+        f5.append(c5)
+        f6.append(c6)
         for j in range(n_post):
-            post[j].append(float(q[j]))
+            post[j].append(q[j])
 
     for bindex, chars in sentences:
         n = len(chars)
         if len(bindex) < n:
             raise IndexError('list index out of range')
-        objs = [bos_word()]
+        objs = SentNodes([bos_word()])
+        objs.chars, objs.S = chars, S
         base = len(words)
-        add_node(objs[0])
+        add_record(_record(model, objs[0]))
         groups = [_span_candidates(bindex[b], b, n, max_len) for b in range(n)]
         for e in range(1, n + 1):
             for d in range(S, 0, -1):
@@ -253,10 +368,16 @@ def pack(sentences, model, max_len=8):
                     continue
                 cands = groups[b].get(e)
                 if not cands:
-                    cands = [Word(chars[b:e], chars[b:e], None, Unk, None, d, b, e, False)]
+                    w = Word(chars[b:e], chars[b:e], None, Unk, None, d, b, e, False)
+                    rec = _record(model, w)
+                    if implicit and _bits(rec) == canon_bits[d - 1]:
+                        continue                            # implicit: no node
+                    objs.append(w)
+                    add_record(rec)
+                    continue
                 for w in cands:
                     objs.append(w)
-                    add_node(w)
+                    add_record(_record(model, w))
         span_start.append(len(objs))
         if n_edge:
             _pack_edges(model, objs, span_start[len(span_start) - S * n - 1:], S, n,
@@ -279,7 +400,15 @@ def pack(sentences, model, max_len=8):
         node_f5=f64(f5), node_f6=f64(f6),
         node_post=f64(post).reshape(n_post, -1) if n_post else np.zeros((0, len(words))),
         edge_terms=n_edge, term_kinds=int(model.term_kinds), n_terms=len(model.plan),
+        unk_n=S if implicit else 0,
     )
+    if implicit:
+        col = lambda i: [r[i] for r in canon]      # noqa: E731
+        batch.unk_word, batch.unk_morph0, batch.unk_tag = i32(col(0)), i32(col(1)), i32(col(2))
+        batch.unk_mask = u32(col(3))
+        batch.unk_pre, batch.unk_f4, batch.unk_f5, batch.unk_f6 = f64(col(4)), f64(col(5)), f64(col(6)), f64(col(7))
+        batch.unk_post = (f64([[r[8][j] for r in canon] for j in range(n_post)]).reshape(n_post, S)
+                          if n_post else np.zeros((0, S)))
     if n_edge:
         batch.edge_val = f64(edge_vals).reshape(n_edge, -1)
         batch.node_edge_base = np.asarray(edge_base, dtype=np.int64)

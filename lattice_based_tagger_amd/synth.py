@@ -137,9 +137,11 @@ class FastLayout:
         self.__dict__.update(kw)
 
 
-def layout(raw):
+def layout(raw, implicit_unk=False):
     """Packed node order of ``raw`` (dictionary + Unknown nodes) without
-    model-dependent columns."""
+    model-dependent columns.  ``implicit_unk``: the Unknowns are implicit
+    (packer.py; every synthetic Unknown surface is in no key, so all of them
+    are) -- only dictionary nodes are nodes."""
     S, T = raw.S, int(raw.sent_n.sum())
     n = raw.sent_n.astype(np.int64)
     span_base = np.zeros(S + 1, dtype=np.int64)
@@ -152,7 +154,7 @@ def layout(raw):
     valid = d <= (n[cs] - b)[:, None]
     slot = span_base[cs][:, None] + (b[:, None] + d - 1) * 8 + (8 - d)
     span_count = np.zeros(n_span, dtype=np.int64)
-    span_count[slot[valid]] = np.maximum(raw.cnt, 1)[valid]
+    span_count[slot[valid]] = (raw.cnt if implicit_unk else np.maximum(raw.cnt, 1))[valid]
     # local start of every span = 1 (BOS) + exclusive prefix inside the sentence
     incl = np.cumsum(span_count)
     excl = incl - span_count
@@ -178,7 +180,7 @@ def layout(raw):
     dict_pos = node_off[nsent] + local[nslot] + ranks
 
     # Unknown nodes: valid spans without dictionary candidates
-    unk_mask = valid & (raw.cnt == 0)
+    unk_mask = valid & (raw.cnt == 0) & (not implicit_unk)
     uslot = slot[unk_mask]
     usent = np.broadcast_to(cs[:, None], valid.shape)[unk_mask]
     ub = np.broadcast_to(b[:, None], valid.shape)[unk_mask]
@@ -190,7 +192,7 @@ def layout(raw):
     return FastLayout(node_b=node_b, S=S, n=n, span_base=span_base, n_span=n_span,
                       span_start=local.astype(np.int32), node_off=node_off, NT=NT,
                       dict_pos=dict_pos, unk_pos=unk_pos, unk_sent=usent, unk_b=ub, unk_d=ud,
-                      bos_pos=node_off[:-1])
+                      bos_pos=node_off[:-1], implicit=bool(implicit_unk))
 
 
 def node_columns(raw, lay):
@@ -277,9 +279,11 @@ def _dec_rows(k):
 
 def make_model(raw, lay=None, cols=None, seed=0, n_features=1_000_000, samples_per_char=0.1,
                fill=True):
-    """Features of sampled real expansions + random fill up to n_features."""
-    if lay is None:
-        lay = layout(raw)
+    """Features of sampled real expansions + random fill up to n_features
+    (sampled over the explicit layout, so the model does not depend on how
+    the batch stores its Unknowns)."""
+    if lay is None or lay.implicit:
+        lay, cols = layout(raw), None
     if cols is None:
         cols = node_columns(raw, lay)
     rng = np.random.default_rng(seed + 7919)
@@ -358,12 +362,13 @@ def _reg_terms(length, unk, tag_is_noun, reg):
     return 0.0 + v          # BeamScoreFunctions: 0 + reg
 
 
-def pack_fast(raw, model, lay=None, cols=None):
+def pack_fast(raw, model, lay=None, cols=None, implicit_unk=True):
     """Device batch layout for ``raw`` under ``model`` (same arrays packer.pack
-    would build from the Word rendering, up to a renaming of ids)."""
+    would build from the Word rendering, up to a renaming of ids).
+    ``implicit_unk``: Unknowns implicit (packer.py), else every Unknown a node."""
     from .packer import PackedBatch
-    if lay is None:
-        lay = layout(raw)
+    if lay is None or lay.implicit != bool(implicit_unk):
+        lay, cols = layout(raw, implicit_unk), None
     if cols is None:
         cols = node_columns(raw, lay)
     word, morph, tag, length, is_l, unk = cols
@@ -414,7 +419,24 @@ def pack_fast(raw, model, lay=None, cols=None):
         max_len=8, n_post=0, has_trigram=1, sent_n=raw.sent_n.astype(np.int32),
         sent_node_off=lay.node_off, sent_span_off=lay.span_base, span_start=lay.span_start,
         node_word=word, node_morph0=morph, node_tag=tag, node_mask=mask, node_pre=pre,
-        node_f4=f4, node_f5=f5, node_f6=f6, node_post=np.zeros((0, lay.NT)))
+        node_f4=f4, node_f5=f5, node_f6=f6, node_post=np.zeros((0, lay.NT)), unk_n=0)
+    if implicit_unk:
+        # the canonical Unknown of each span length d (packer.unknown_records):
+        # ids 0, tag 'Unknown', classes 4 / 6 of d, Regularization of d
+        d = np.arange(1, MAX_SPAN + 1, dtype=np.int32)
+        um = np.uint32(Lw.node_mask_from_vocab(int(vmask[0]), int(vmask[0]), int(vmask[ids.unk])) | Lw.F_UNK)
+        u4 = i4[np.clip(d, 0, 15)]
+        u6 = i6[np.minimum(8, d)]
+        batch.unk_n = MAX_SPAN
+        batch.unk_word = np.zeros(MAX_SPAN, np.int32)
+        batch.unk_morph0 = np.zeros(MAX_SPAN, np.int32)
+        batch.unk_tag = np.full(MAX_SPAN, ids.unk, np.int32)
+        batch.unk_mask = (um | np.where(u4 >= 0, Lw.F_HAS4, 0) | np.where(u6 >= 0, Lw.F_HAS6, 0)).astype(np.uint32)
+        batch.unk_pre = _reg_terms(d, np.ones(MAX_SPAN, bool), np.zeros(MAX_SPAN, bool), model.reg)
+        batch.unk_f4 = np.where(u4 >= 0, coef[np.maximum(u4, 0)], 0.0)
+        batch.unk_f5 = np.zeros(MAX_SPAN)
+        batch.unk_f6 = np.where(u6 >= 0, coef[np.maximum(u6, 0)], 0.0)
+        batch.unk_post = np.zeros((0, MAX_SPAN))
     return batch, keys, coef[model.probed_idx].astype(np.float64)
 
 

@@ -18,7 +18,10 @@
  *   numpy pairwise sum     (score_funcs.py:144; numpy pairwise_sum order)
  * Independent of the product's data structures: key presence is a binary
  * search over the sorted key array (no hash table, no pre-filter masks) and
- * the beam is a full stable sort of every grown hypothesis.
+ * the beam is a full stable sort of every grown hypothesis.  Implicit Unknown
+ * candidates (lt_batch_desc.n_unk: an empty span in range holds the
+ * synthesised Unknown of beam.py:36-38) are enumerated in their span's place
+ * and reported by their negative path code.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -101,16 +104,43 @@ static double numpy_sum(const double* v, int m) {
   return s;
 }
 
+/* A candidate word of sentence `nb` by its path code (lattice_decode.h):
+ * x >= 0 local node x; x <= -2 the implicit Unknown of span entry -2 - x
+ * (n_unk: the synthesised Word of an empty span, beam.py:36-38), whose record
+ * is entry d - 1 of the unk_* arrays, d = SS - (entry mod SS). */
+typedef struct {
+  int32_t w, m, t;
+  uint32_t f;
+  double pre, f4, f5, f6;
+  int64_t at;     /* node index into node_post, or -(d) for unk_post */
+} onode;
+
+static void node_at(const lt_batch_desc* d, int64_t nb, int SS, int32_t x, onode* o) {
+  if (x >= 0) {
+    const int64_t i = nb + x;
+    o->w = d->node_word[i]; o->m = d->node_morph0[i]; o->t = d->node_tag[i]; o->f = d->node_mask[i];
+    o->pre = d->node_pre[i]; o->f4 = d->node_f4[i]; o->f5 = d->node_f5[i]; o->f6 = d->node_f6[i];
+    o->at = i;
+  } else {
+    const int dd = SS - ((-2 - x) % SS);
+    const int i = dd - 1;
+    o->w = d->unk_word[i]; o->m = d->unk_morph0[i]; o->t = d->unk_tag[i]; o->f = d->unk_mask[i];
+    o->pre = d->unk_pre[i]; o->f4 = d->unk_f4[i]; o->f5 = d->unk_f5[i]; o->f6 = d->unk_f6[i];
+    o->at = -(int64_t)dd;
+  }
+}
+
+static double post_term(const lt_batch_desc* d, const onode* o, int t) {
+  return o->at >= 0 ? d->node_post[(int64_t)t * d->n_nodes + o->at]
+                    : d->unk_post[(int64_t)t * d->n_unk + (-o->at - 1)];
+}
+
 static int decode_sentence(const omodel* m, const lt_batch_desc* d, int s, int k, int32_t* count,
                            int32_t* length, double* score, int32_t* codes, int64_t code_base,
                            int64_t* n_exp, int64_t* n_tup, int64_t* n_hit) {
   const int n = d->sent_n[s];
   const int64_t nb = d->sent_node_off[s];
   const int32_t* ss = d->span_start + d->sent_span_off[s];
-  const int32_t* W = d->node_word + nb;
-  const int32_t* M = d->node_morph0 + nb;
-  const int32_t* T = d->node_tag + nb;
-  const uint32_t* F = d->node_mask + nb;
   ohyp* H = (ohyp*)malloc(sizeof(ohyp) * (size_t)(n + 1) * (size_t)k);
   int32_t* cnt = (int32_t*)calloc((size_t)n + 1, sizeof(int32_t));
   size_t gcap = 1024;
@@ -128,47 +158,54 @@ static int decode_sentence(const omodel* m, const lt_batch_desc* d, int s, int k
       const int dd = e - b;
       const int j = SS - dd;
       const int32_t lo = ss[(int64_t)(e - 1) * SS + j], hi = ss[(int64_t)(e - 1) * SS + j + 1];
+      /* no node in the span: its implicit Unknown (beam.py:36-38), by code */
+      const int imp = lo == hi && d->n_unk > 0;
+      const int32_t xlo = imp ? -2 - ((e - 1) * SS + j) : lo, xhi = imp ? xlo + 1 : hi;
       for (int r = 0; r < cnt[b]; ++r) {
         const ohyp* h = &H[(size_t)b * k + r];
-        for (int32_t x = lo; x < hi; ++x) {
+        for (int32_t x = xlo; x < xhi; ++x) {
           const int64_t gi = gen++;
-          if (h->unk && (F[x] & F_UNK) && bmin < b) continue;
+          onode X, J, I;
+          node_at(d, nb, SS, x, &X);
+          if (h->unk && (X.f & F_UNK) && bmin < b) continue;
           double tri = 0.0;
           if (d->has_trigram) {
             const int jn = h->node, in = h->prev;
+            node_at(d, nb, SS, jn, &J);
+            if (in != -1) node_at(d, nb, SS, in, &I);
             double v[9];
             int mm = 0;
             double c;
             int tup = 6;
-            if (lookup(m, 0, W[jn], W[x], T[x], &c)) v[mm++] = c;
-            if (lookup(m, 1, W[jn], T[x], 0, &c)) v[mm++] = c;
-            if (lookup(m, 2, T[jn], W[x], T[x], &c)) v[mm++] = c;
-            if (lookup(m, 3, T[jn], T[x], 0, &c)) v[mm++] = c;
-            if (F[x] & F_HAS4) v[mm++] = d->node_f4[nb + x];
-            if (F[x] & F_HAS5) v[mm++] = d->node_f5[nb + x];
-            if (F[jn] & F_UNK) {
+            if (lookup(m, 0, J.w, X.w, X.t, &c)) v[mm++] = c;
+            if (lookup(m, 1, J.w, X.t, 0, &c)) v[mm++] = c;
+            if (lookup(m, 2, J.t, X.w, X.t, &c)) v[mm++] = c;
+            if (lookup(m, 3, J.t, X.t, 0, &c)) v[mm++] = c;
+            if (X.f & F_HAS4) v[mm++] = X.f4;
+            if (X.f & F_HAS5) v[mm++] = X.f5;
+            if (J.f & F_UNK) {
               ++tup;
-              if (F[jn] & F_HAS6) v[mm++] = d->node_f6[nb + jn];
+              if (J.f & F_HAS6) v[mm++] = J.f6;
             }
-            if (in >= 0) {
+            if (in != -1) {
               ++tup;
-              if (W[in] != 0 && lookup(m, 7, W[in], W[jn], W[x], &c)) v[mm++] = c;
+              if (I.w != 0 && lookup(m, 7, I.w, J.w, X.w, &c)) v[mm++] = c;
             }
-            if (F[x] & F_CTX) {
-              if (F[jn] & F_CTX) {
+            if (X.f & F_CTX) {
+              if (J.f & F_CTX) {
                 ++tup;
-                if (lookup(m, 8, M[jn], M[x], 0, &c)) v[mm++] = c;
-              } else if (in >= 0 && (F[in] & F_CTX)) {
+                if (lookup(m, 8, J.m, X.m, 0, &c)) v[mm++] = c;
+              } else if (in != -1 && (I.f & F_CTX)) {
                 ++tup;
-                if (lookup(m, 8, M[in], M[x], 0, &c)) v[mm++] = c;
+                if (lookup(m, 8, I.m, X.m, 0, &c)) v[mm++] = c;
               }
             }
             tri = numpy_sum(v, mm);
             *n_tup += tup;
             *n_hit += mm;
           }
-          double inc = d->node_pre[nb + x] + tri;
-          for (int t = 0; t < d->n_post; ++t) inc += d->node_post[(int64_t)t * d->n_nodes + nb + x];
+          double inc = X.pre + tri;
+          for (int t = 0; t < d->n_post; ++t) inc += post_term(d, &X, t);
           if (ng == gcap) {
             gcap *= 2;
             ogrown* G2 = (ogrown*)realloc(G, sizeof(ogrown) * gcap);
@@ -183,7 +220,7 @@ static int decode_sentence(const omodel* m, const lt_batch_desc* d, int s, int k
           g->depth = h->depth + 1;
           g->ppos = b;
           g->prank = r;
-          g->unk = (F[x] & F_UNK) ? 1 : 0;
+          g->unk = (X.f & F_UNK) ? 1 : 0;
           ++*n_exp;
         }
       }

@@ -22,11 +22,17 @@ class _ModelDesc(C.Structure):
 
 
 class _BatchDesc(C.Structure):
+    # include/lattice_decode.h lt_batch_desc (ABI 5); edge terms unused here
     _fields_ = [('n_sent', C.c_int32), ('max_len', C.c_int32), ('n_post', C.c_int32),
                 ('has_trigram', C.c_int32), ('n_nodes', C.c_int64), ('n_span', C.c_int64)] + [
         (f, C.c_void_p) for f in ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start',
                                   'node_word', 'node_morph0', 'node_tag', 'node_mask',
-                                  'node_pre', 'node_f4', 'node_f5', 'node_f6', 'node_post')]
+                                  'node_pre', 'node_f4', 'node_f5', 'node_f6', 'node_post')] + [
+        ('n_edge', C.c_int32), ('n_terms', C.c_int32), ('term_kinds', C.c_uint64),
+        ('n_edges', C.c_int64), ('sent_edge_off', C.c_void_p), ('node_edge_base', C.c_void_p),
+        ('edge_val', C.c_void_p), ('n_unk', C.c_int32)] + [
+        (f, C.c_void_p) for f in ('unk_word', 'unk_morph0', 'unk_tag', 'unk_mask', 'unk_pre',
+                                  'unk_f4', 'unk_f5', 'unk_f6', 'unk_post')]
 
 
 _lib = None
@@ -56,6 +62,8 @@ _DT = {'sent_n': np.int32, 'sent_node_off': np.int64, 'sent_span_off': np.int64,
        'span_start': np.int32, 'node_word': np.int32, 'node_morph0': np.int32,
        'node_tag': np.int32, 'node_mask': np.uint32, 'node_pre': np.float64,
        'node_f4': np.float64, 'node_f5': np.float64, 'node_f6': np.float64}
+_UNK_DT = {'unk_word': np.int32, 'unk_morph0': np.int32, 'unk_tag': np.int32, 'unk_mask': np.uint32,
+           'unk_pre': np.float64, 'unk_f4': np.float64, 'unk_f5': np.float64, 'unk_f6': np.float64}
 
 
 def decode(packed, keys, coefs, k, s0=0, s1=None, nthreads=1):
@@ -68,6 +76,13 @@ def decode(packed, keys, coefs, k, s0=0, s1=None, nthreads=1):
     bd = _BatchDesc(S, int(packed.max_len), n_post, int(packed.has_trigram),
                     arr['node_word'].shape[0], arr['span_start'].shape[0],
                     *[arr[f].ctypes.data for f in _DT], None if post is None else post.ctypes.data)
+    n_unk = int(getattr(packed, 'n_unk', 0))
+    if n_unk:                    # implicit Unknowns (lattice_decode.h n_unk)
+        unk = {f: np.ascontiguousarray(getattr(packed, f), dtype=dt) for f, dt in _UNK_DT.items()}
+        unk['unk_post'] = np.ascontiguousarray(packed.unk_post, dtype=np.float64).reshape(n_post, n_unk)
+        bd.n_unk = n_unk
+        for f, a in unk.items():
+            setattr(bd, f, a.ctypes.data if a.size else None)
     keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 4)
     coefs = np.ascontiguousarray(coefs, dtype=np.float64)
     md = _ModelDesc(keys.shape[0], keys.ctypes.data, coefs.ctypes.data)

@@ -33,14 +33,14 @@ def _case(name, idx):
 def test_debug_dump_equals_reference(gpu_decoder, dump):
     case = _case(dump['set'], dump['index'])
     buf = io.StringIO()
-    err = None
+    err = msg = None
     with contextlib.redirect_stdout(buf):
         try:
             got = beam_search(case.bindex, case.chars, case.funcs, beam_size=dump['beam'],
                               max_len=case.max_len, debug=True)
         except Exception as exc:
-            err = type(exc).__name__
-    assert err == dump['error']
+            err, msg = type(exc).__name__, str(exc)
+    assert err == dump['error'], msg
     assert buf.getvalue() == dump['stdout']
     if err is None:
         # the returned matures are the decoder's, unchanged by debug

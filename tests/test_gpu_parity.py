@@ -163,23 +163,29 @@ def test_full_size_properties(gpu_decoder):
     count, length, score, codes = r1
     assert np.all(count == k)
     assert np.all(np.diff(score, axis=1) <= 0)
-    # span chain check on a sample
-    node_b = lay.node_b
-    span_of = lambda g: (node_b[g], node_b[g] + 0)
+    # span chain check on a sample: every path word's span entry x (a node's:
+    # the entry whose node range holds it; an implicit Unknown's: from its
+    # code -2 - x, and its span holds no node), spans chained from 0 to n
     n = packed.sent_n.astype(np.int64)
     cum = np.r_[0, np.cumsum(n)]
     rng = np.random.default_rng(0)
+    n_imp = 0
     for s in rng.choice(len(n), size=200, replace=False):
+        ss = packed.span_start[packed.sent_span_off[s]:packed.sent_span_off[s + 1]].astype(np.int64)
         for t in range(k):
             L = length[s, t]
             off = k * cum[s] + t * n[s]
             local = codes[off:off + L].astype(np.int64)
-            g = packed.sent_node_off[s] + local
-            b = node_b[g]
-            # e of each node = b of the next one; first starts at 0
-            assert b[0] == 0
-            ends = np.r_[b[1:], n[s]]
-            assert np.all(ends > b) and np.all(ends - b <= 8)
+            imp = local <= -2
+            x = np.where(imp, -2 - local, np.searchsorted(ss, local, side='right') - 1)
+            assert np.all(ss[x[imp]] == ss[x[imp] + 1])            # implicit: an empty span
+            assert np.all(ss[x[~imp]] <= local[~imp]) and np.all(local[~imp] < ss[x[~imp] + 1])
+            e = x // 8 + 1
+            d = 8 - x % 8
+            b = e - d
+            assert b[0] == 0 and e[-1] == n[s] and np.all(b[1:] == e[:-1])
+            n_imp += int(imp.sum())
+    assert n_imp > 0                       # the sample crosses implicit Unknowns
     db.close()
     dm.close()
 
