@@ -9,6 +9,7 @@ separate IEEE operation, which bit-exact parity with the reference requires.
 import os
 import subprocess
 import sys
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
@@ -24,7 +25,10 @@ HEADERS = ['lt_common.h', 'lt_internal.h', 'lt_error.h', 'lt_handles.h', 'lt_hos
            os.path.join('..', '..', 'include', 'lattice_lookup.h')]
 
 PYOBJ_SRC = os.path.join(CSRC, 'lt_pyobj.c')
-PYOBJ = os.path.join(LIBDIR, '_ltpy.so')
+# named for the interpreter ABI it is built against (EXT_SUFFIX, e.g.
+# .cpython-310-x86_64-linux-gnu.so): another CPython finds no stale build of
+# the wrong ABI, it builds its own
+PYOBJ = os.path.join(LIBDIR, '_ltpy' + (sysconfig.get_config_var('EXT_SUFFIX') or '.so'))
 
 COMMON_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
                 '-Wall', '-Wno-unused-result', '-I' + os.path.join(HERE, '..', 'include')]
@@ -41,7 +45,6 @@ def build_pyobj(force=False, verbose=True):
     """The CPython extension `_ltpy` (csrc/lt_pyobj.c: bulk Word / path
     construction for the returned Sequences), compiled with the host C
     compiler against this interpreter's headers."""
-    import sysconfig
     os.makedirs(LIBDIR, exist_ok=True)
     if not force and not _stale(PYOBJ, [PYOBJ_SRC, __file__]):
         return PYOBJ

@@ -16,7 +16,7 @@ def load():
     if _mod is None:
         with _lock:
             if _mod is None:
-                path = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', '_ltpy.so')
+                from ._build import PYOBJ as path             # (per-interpreter name, EXT_SUFFIX)
                 if not os.path.exists(path):
                     raise ImportError('lattice_based_tagger_amd: %s is missing -- run '
                                       '__graft_entry__.build() (python -m lattice_based_tagger_amd._build)' % path)

@@ -74,22 +74,31 @@ _model_cache = weakref.WeakKeyDictionary()
 
 def _immutable(a):
     """True when no one can write into the array's memory: the array and
-    every array it views are read-only and the memory is owned by numpy or
-    by an immutable ``bytes`` object."""
+    every array it views are read-only and the memory itself is a read-only
+    buffer (``bytes``, a read-only ``mmap`` -- a model pack's arrays).  An
+    array that owns its memory is never immutable: numpy lets its owner set
+    ``flags.writeable`` back to True, edit it, and clear the flag again."""
     while isinstance(a, np.ndarray):
         if a.flags.writeable:
             return False
         a = a.base
-    return a is None or isinstance(a, bytes)
+    if a is None:
+        return False
+    try:
+        return memoryview(a).readonly
+    except TypeError:
+        return False
 
 
 def _digest_array(a):
-    """Content digest of a numpy array (in-place edits change it).  A
-    read-only array (``coef.flags.writeable = False``) cannot change, so its
-    identity stands in for the content and the per-call hash of the whole
-    array (about 1 ms for 1M coefficients) is skipped."""
+    """Content digest of a numpy array (in-place edits change it).  An array
+    over read-only memory (``_immutable``) cannot change, so its identity
+    stands in for the content and the per-call hash of the whole array
+    (about 1 ms for 1M coefficients) is skipped; the cached model holds a
+    reference to it, so its address cannot be reused while it is cached.
+    (``invalidate_model_cache`` drops every lowered model.)"""
     if isinstance(a, np.ndarray) and _immutable(a):
-        return ('ro', a.dtype.str, a.shape, a.__array_interface__['data'][0], a.strides)
+        return ('ro', a.dtype.str, a.shape, a.__array_interface__['data'][0], a.strides, id(a))
     a = np.ascontiguousarray(a)
     try:
         import xxhash

@@ -740,11 +740,13 @@ __device__ __forceinline__ bool bm_hit(const typename Tab<NARROW>::S& s, uint32_
   }
 }
 
+// The probed classes' coefficients cf[q] (-0.0 when absent) and presence
+// bits of one expansion (waits for its slot loads).
 template <bool NARROW>
-__device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntry& h, const Cand& c) {
+__device__ __forceinline__ void bm_classes(const BMProbe<NARROW>& P, const VEntry& h, const Cand& c, double (&cf)[6],
+                                           uint32_t& pres) {
   const V1Keys K = v1_keys(h, c);
-  double cf[6];
-  uint32_t pres = P.pres3;
+  pres = P.pres3;
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     const bool n = (P.gneed >> q) & 1u;
@@ -756,8 +758,42 @@ __device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntr
       pres |= (m1 | m2) ? 1u << q : 0u;
     }
   }
+}
+
+template <bool NARROW>
+__device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntry& h, const Cand& c) {
+  double cf[6];
+  uint32_t pres;
+  bm_classes<NARROW>(P, h, c, cf, pres);
   return v1_sum(cf, pres, c, h);
 }
+
+// ---------------------------------------------------------------------------
+// Probe dedup (beam kernels).  Hypotheses of one beam[b] often end in the same
+// word: at k = 5 two thirds of the expansions repeat an earlier hypothesis'
+// last word, at k = 16 nearly nine in ten.  Feature classes 0-3
+// (feature.py:95-103: (wj.word, wk.word, tk), (wj.word, tk), (tj, wk.word,
+// tk), (tj, tk)) and their pre-filter bits depend on the candidate and on wj's
+// word and tag only, so two expansions of one candidate from hypotheses whose
+// last words agree in (word, tag) find the same coefficients.  The first such
+// hypothesis of a beam (its "lead", computed when the beam is written) probes
+// them; an expansion from a later one (a "dup", within DD_WIN expansions of
+// its lead's) takes them from a small LDS cache keyed by expansion index and
+// probes only classes 7 and 8, which read wi / the morphs.  The sum is then
+// the same numpy-order sum over the same values (H7), so results are
+// bit-identical.
+// ---------------------------------------------------------------------------
+#ifndef BM_DEDUP
+#define BM_DEDUP 1
+#endif
+// The cache holds DD_Q entries, entry g mod DD_Q; a dup is within DD_WIN =
+// DD_Q expansions of its lead, so no expansion between them rewrites the
+// lead's entry.  A round writes its (up to 64) consecutive entries at once,
+// which can rewrite the entry of a lead of an earlier round that a dup of
+// this round needs: such dups read before the round's writes, dups of a lead
+// in the same round after them.
+constexpr int DD_Q = 64;
+constexpr int DD_WIN = DD_Q;
 
 // Sequence.add into a ring entry (beam.py:112-116): wi = wj, wj = wk
 template <bool COUNT>
@@ -819,6 +855,9 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #endif
 #ifndef HW_SPRE
 #define HW_SPRE 1
+#endif
+#ifndef HW_STAGE
+#define HW_STAGE 32                     // lt_beam_hw: records staged per wave and position
 #endif
 #ifndef PK_SPRE
 #define PK_SPRE 1
@@ -1249,8 +1288,19 @@ __device__ __forceinline__ void rank_into(const unsigned long long* LK, int q0, 
   if (ck != 0ull && r < k) { TK[r] = ck; TG[r] = cg; }
 }
 
+// records lt_beam_pk stages per position (the rest take a global load): the
+// dictionary candidates of one end position (implicit Unknowns take none), 2.5
+// on average in the bench lattices
+#ifndef PK_STAGE
+#define PK_STAGE 32
+#endif
+// occupancy floor of lt_beam_pk per beam template (the probe dedup's registers
+// would otherwise drop k = 9..16 to 3 waves per SIMD)
+#ifndef PK_WPE
+#define PK_WPE(kt) ((kt) == 16 ? 4 : 1)
+#endif
 template <int KT, int WPB, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(64 * WPB)
+__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PK_WPE(KT), 8)))
 lt_beam_pk(DecodeParams p) {
   constexpr int RPC = KT <= 16 ? 2 : 4;         // scoring rounds per chunk
   // beams above 64 (KT = 128, 256): more than one entry per lane in the
@@ -1261,10 +1311,11 @@ lt_beam_pk(DecodeParams p) {
   constexpr int KTP = KT < 4 ? 4 : KT;          // running-list room (multiple of 4)
   constexpr int LN = KTP + CH;                  // ranked list: running top-k + chunk
   static_assert(KTP % 4 == 0, "list alignment");
-  constexpr int STAGE = 64;                     // candidate records staged per position
+  constexpr int STAGE = PK_STAGE;               // candidate records staged per position
+  constexpr int PL = (3 * STAGE + 63) / 64;     // 16 B staging loads per lane
   __shared__ VEntry ring[WPB][RING][KT];
   __shared__ int32_t cntl[WPB][RING];
-  __shared__ uint4 stg[WPB][3 * 64];            // records of the current position
+  __shared__ uint4 stg[WPB][3 * STAGE];         // records of the current position
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][LN];
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][LN];
   __shared__ unsigned long long tkey[WPB][KT];
@@ -1276,6 +1327,11 @@ lt_beam_pk(DecodeParams p) {
   __shared__ __attribute__((aligned(16))) int sstp[WPB][PK_SPRE ? 12 : 1];
   __shared__ __attribute__((aligned(16))) int sprep[WPB][PK_SPRE ? 12 : 1];
   __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
+  // probe dedup (BM_DEDUP): each beam entry's lead rank, the classes 0-3 cache
+  constexpr bool DEDUP = BM_DEDUP && KT <= 16;
+  __shared__ uint8_t lead9[WPB][DEDUP ? RING : 1][DEDUP ? KT : 1];
+  __shared__ double ddc[WPB][DEDUP ? DD_Q : 1][4];
+  __shared__ uint8_t ddp[WPB][DEDUP ? DD_Q : 1];
   stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
@@ -1307,6 +1363,7 @@ lt_beam_pk(DecodeParams p) {
   if (lane == 0) {                              // beam[0] = [BOS] (beam.py:21-23)
     R[0][0] = v_bos(load_cand(B, nbase));
     cnt9[0] = 1;
+    if (DEDUP) lead9[wv][0][0] = 0;
   }
   // The next position's first 64 records (lane t holds 16 B chunks t,
   // 64 + t, 128 + t of the block: consecutive lanes read consecutive bytes)
@@ -1314,12 +1371,13 @@ lt_beam_pk(DecodeParams p) {
   // ahead and written to LDS at the top of the position: ordinary loads, so
   // the compiler's waits count them exactly (an LDS-DMA in flight would make
   // it drain every memory operation before each LDS access).
-  u32x4 pf[3];
+  u32x4 pf[PL];
   int pfs = 0;
   auto prefetch = [&](int e1, int first, bool valid) {
     const uint32_t base = (nbase + (uint32_t)first) * (uint32_t)sizeof(NodeRec);
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) pf[pl] = ld128(B.node, valid ? base + (uint32_t)(pl * 64 + lane) * 16u : OOB);
+    for (int pl = 0; pl < PL; ++pl)
+      pf[pl] = ld128(B.node, valid && pl * 64 + lane < 3 * STAGE ? base + (uint32_t)(pl * 64 + lane) * 16u : OOB);
     pfs = (valid && lane <= MAX_SPAN) ? ssp[(e1 - 1) * MAX_SPAN + lane] : 0;
   };
   int ss[MAX_SPAN + 1];
@@ -1336,7 +1394,8 @@ lt_beam_pk(DecodeParams p) {
     else __builtin_amdgcn_s_waitcnt(0x0F71);
     uint4* const cst = stg[wv];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
+    for (int pl = 0; pl < PL; ++pl)
+      if (pl * 64 + lane < 3 * STAGE) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
 #pragma unroll
     for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = __builtin_amdgcn_readlane(pfs, j);
     __builtin_amdgcn_wave_barrier();
@@ -1367,17 +1426,18 @@ lt_beam_pk(DecodeParams p) {
     // slot whose prefix is <= g (pre is nondecreasing), its prefix, size and
     // first node selected by the same compare -- PK_SPRE: j counted, the three
     // values read from LDS
-    auto decode = [&](int g, int& j, int& r, int& i, int& sj, bool& imp) {
+    auto decode = [&](int g, int& j, int& r, int& i, int& sj, bool& imp, int& m) {
 #if PK_SPRE
       j = 0;
 #pragma unroll
       for (int q = 1; q < MAX_SPAN; ++q) j += g >= pre[q] ? 1 : 0;
       const int pj = sprep[wv][j];
       sj = sstp[wv][j];
-      int m = sstp[wv][j + 1] - sj;
+      m = sstp[wv][j + 1] - sj;
 #else
       j = 0;
-      int pj = pre[0], m = ss[1] - ss[0];
+      int pj = pre[0];
+      m = ss[1] - ss[0];
       sj = ss[0];
 #pragma unroll
       for (int q = 1; q < MAX_SPAN; ++q) {
@@ -1409,9 +1469,9 @@ lt_beam_pk(DecodeParams p) {
         if (base + 64 * t >= M) continue;        // uniform
         const int g = base + 64 * t + lane;
         const bool act = g < M;
-        int j = 0, r = 0, i = 0, sj = 0;
+        int j = 0, r = 0, i = 0, sj = 0, m = 1;
         bool imp = false;
-        if (act) decode(g, j, r, i, sj, imp);
+        if (act) decode(g, j, r, i, sj, imp, m);
         const int d = MAX_SPAN - j;
         const int node = sj + i;
         const int so = node - A0;
@@ -1428,13 +1488,47 @@ lt_beam_pk(DecodeParams p) {
         const VEntry h0 = R[hb][hr];
         // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));
+        // a dup (BM_DEDUP): its lead's expansion of the same candidate is gl
+        const int ldr = DEDUP ? (int)lead9[wv][hb][hr] : hr;
+        const int gdist = (hr - ldr) * m;
+        const bool dup = DEDUP && !skip && has_tri && ldr != hr && gdist < DD_WIN;
         BMProbe<NARROW> P;
         const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
-        bm_issue<NARROW>(P, B, slots, seed, h0, c, need, aux);
+        bm_issue<NARROW>(P, B, slots, seed, h0, c, dup ? (need & 0x30u) : need, aux);
         asm volatile("" ::: "memory");
         const VEntry h1 = R[hb][hr];
+        double cf[6];
+        uint32_t pres = 0;
+        if (has_tri) bm_classes<NARROW>(P, h1, c, cf, pres);
+        if (DEDUP && has_tri) {
+          // leads (every lane that probed classes 0-3) publish them; dups read
+          // their lead's: one of an earlier round before this round's writes,
+          // one of this round after them
+          const int gl = g - gdist;
+          const int ql = gl & (DD_Q - 1);
+          const bool early = gl < base + 64 * t;
+          if (dup && early) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x) cf[x] = ddc[wv][ql][x];
+            pres = (pres & ~0xFu) | ddp[wv][ql];
+          }
+          __builtin_amdgcn_wave_barrier();
+          if (!skip && !dup) {
+            const int q = g & (DD_Q - 1);
+#pragma unroll
+            for (int x = 0; x < 4; ++x) ddc[wv][q][x] = cf[x];
+            ddp[wv][q] = (uint8_t)(pres & 0xFu);
+          }
+          __builtin_amdgcn_wave_barrier();
+          if (dup && !early) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x) cf[x] = ddc[wv][ql][x];
+            pres = (pres & ~0xFu) | ddp[wv][ql];
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
         if (!skip) {
-          const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
+          const double tri = has_tri ? v1_sum(cf, pres, c, h1) : 0.0;
           if (COUNT) v_count(cnt, h1, c, need, 2 * __builtin_popcount(P.gneed));
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
@@ -1571,9 +1665,9 @@ lt_beam_pk(DecodeParams p) {
     VEntry ne;
     uint32_t bpv = 0;
     const bool writer = wl < nrun;
-    int wj = 0, wr = 0, wi = 0, wsj = 0;
+    int wj = 0, wr = 0, wi = 0, wsj = 0, wm = 1;
     bool wimp = false;
-    if (writer) decode((int)LG[KTP - nrun + wl], wj, wr, wi, wsj, wimp);
+    if (writer) decode((int)LG[KTP - nrun + wl], wj, wr, wi, wsj, wimp, wm);
     const int wd = MAX_SPAN - wj;
     const uint32_t wnode = wimp ? UNK_LOCAL : (uint32_t)(wsj + wi);
     const bool far = writer && !wimp && (int)wnode - A0 >= STAGE;
@@ -1592,6 +1686,19 @@ lt_beam_pk(DecodeParams p) {
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][wl] = ne;
     __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + wl) * 4u : OOB, 0, 0);
+    if (DEDUP) {
+      // each entry's lead: the first rank of beam[e] whose last word has the
+      // same (word, tag) -- the same classes 0-3 for every candidate
+      __builtin_amdgcn_wave_barrier();
+      if (writer) {
+        int ld = wl;
+        for (int q = wl - 1; q >= 0; --q) {
+          const uint2 jw = *reinterpret_cast<const uint2*>(&R[em9][q].jword);
+          ld = (jw.x == ne.jword && jw.y == ne.jtag) ? q : ld;
+        }
+        lead9[wv][em9][wl] = (uint8_t)ld;
+      }
+    }
     }
     if (lane == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
@@ -1663,12 +1770,15 @@ lt_beam_hw(DecodeParams p) {
   constexpr int CH = G * RPC;                   // expansions per chunk per group
   constexpr int KTP = KT < 4 ? 4 : KT;
   constexpr int LN = KTP + CH;
-  constexpr int STAGE = 64 / S;                 // records staged per group and position
+  // records staged per group and position (the rest take a global load): a
+  // position's dictionary candidates, 2.5 on average in the bench lattices
+  constexpr int STAGE = HW_STAGE / S;
   constexpr int CPG = 3 * STAGE;                // staged 16 B chunks per group
+  constexpr int PL = (S * CPG + 63) / 64;       // 16 B staging loads per lane
   static_assert(KT <= G && G >= MAX_SPAN + 1, "one writer lane per rank in a group; span starts fit a group");
   __shared__ VEntry ring[WPB][S][RING][KT];
   __shared__ int32_t cntl[WPB][S][RING];
-  __shared__ uint4 stg[WPB][3 * 64];            // group h's record r: chunks CPG h + 3r .. +2
+  __shared__ uint4 stg[WPB][S * CPG];           // group h's record r: chunks CPG h + 3r .. +2
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][S][LN];
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][S][LN];
   __shared__ unsigned long long tkey[WPB][S][KT];
@@ -1678,6 +1788,16 @@ lt_beam_hw(DecodeParams p) {
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
+  // probe dedup (BM_DEDUP, lt_beam_pk): lead ranks, and per group a cache of
+  // 2G entries (a dup within G expansions of its lead reads it after its
+  // round's writes) holding classes 0-3 as the first four terms of the
+  // numpy-order sum, s4 = (((0 + c0) + c1) + c2) + c3: registers are what this
+  // kernel is short of, so a dup is one whose sum is sure to stay left to
+  // right (at most 7 features present) and takes s4 as it is
+  constexpr bool DEDUP = BM_DEDUP && G == 32;
+  constexpr int DQ = 2 * G;
+  __shared__ uint8_t lead9[WPB][S][DEDUP ? RING : 1][DEDUP ? KT : 1];
+  __shared__ double dds[WPB][S][DEDUP ? DQ : 1];
   stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
@@ -1727,24 +1847,25 @@ lt_beam_hw(DecodeParams p) {
   if (hv && hl == 0) {                          // beam[0] = [BOS] (beam.py:21-23)
     R[0][0] = v_bos(load_cand(B, nbase));
     cnt9[0] = 1;
+    if (DEDUP) lead9[wv][hf][0][0] = 0;
   }
   if (HW_SPRE && hl == 0) spre[wv][hf][0] = 0;
   // next position's first STAGE records of every group (chunk c = 64 pl +
   // lane of the wave's stream: group c / CPG, chunk c % CPG of that group's
   // block) and span starts (lane G h + j <= 8: span start j of group h), one
   // position ahead, issued after the position's last load wait (lt_beam_pk)
-  u32x4 pf[3];
+  u32x4 pf[PL];
   int pfs = 0;
   auto prefetch = [&](int e1, int first_own) {
     int fS[S];
 #pragma unroll
     for (int h = 0; h < S; ++h) fS[h] = __builtin_amdgcn_readlane(first_own, h * G);
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < PL; ++pl) {
       const int c = 64 * pl + lane;
       const int hc = c / CPG, cc = c - hc * CPG;
       uint32_t nb = nbS[0], f = (uint32_t)fS[0];
-      bool ok = e1 <= nS[0];
+      bool ok = e1 <= nS[0] && c < S * CPG;
 #pragma unroll
       for (int h = 1; h < S; ++h)
         if (hc == h) { nb = nbS[h]; f = (uint32_t)fS[h]; ok = e1 <= nS[h]; }
@@ -1761,7 +1882,8 @@ lt_beam_hw(DecodeParams p) {
     __builtin_amdgcn_s_waitcnt(0x0F71);         // vmcnt(1): the prefetch (older than the store)
     uint4* const cst = stg[wv];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
+    for (int pl = 0; pl < PL; ++pl)
+      if (pl * 64 + lane < S * CPG) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
     // the group's span starts through LDS: lanes j <= 8 of each group write
     // theirs, every lane reads its group's nine (three reads instead of a
     // readlane / select per value and group)
@@ -1817,7 +1939,7 @@ lt_beam_hw(DecodeParams p) {
     const int M = pre[MAX_SPAN];                // this half's expansions
     const int Mmax = gmax(M);
 
-    auto decode = [&](int g, int& j, int& r, int& i, int& sj, bool& imp) {     // (lt_beam_pk)
+    auto decode = [&](int g, int& j, int& r, int& i, int& sj, bool& imp, int& m) {     // (lt_beam_pk)
 #if HW_SPRE
       // pre is nondecreasing: the slot is the number of prefixes <= g; its
       // prefix, first node and size from LDS
@@ -1826,10 +1948,11 @@ lt_beam_hw(DecodeParams p) {
       for (int q = 1; q < MAX_SPAN; ++q) j += g >= pre[q] ? 1 : 0;
       const int pj = spre[wv][hf][j];
       sj = sst[wv][hf][j];
-      int m = sst[wv][hf][j + 1] - sj;
+      m = sst[wv][hf][j + 1] - sj;
 #else
       j = 0;
-      int pj = pre[0], m = ss[1] - ss[0];
+      int pj = pre[0];
+      m = ss[1] - ss[0];
       sj = ss[0];
 #pragma unroll
       for (int q = 1; q < MAX_SPAN; ++q) {
@@ -1860,9 +1983,9 @@ lt_beam_hw(DecodeParams p) {
         if (base + G * t >= Mmax) continue;      // uniform
         const int g = base + G * t + hl;
         const bool act = g < M;
-        int j = 0, r = 0, i = 0, sj = 0;
+        int j = 0, r = 0, i = 0, sj = 0, m = 1;
         bool imp = false;
-        if (act) decode(g, j, r, i, sj, imp);
+        if (act) decode(g, j, r, i, sj, imp, m);
         const int d = MAX_SPAN - j;
         const int node = sj + i;
         const int so = node - A0;
@@ -1878,12 +2001,45 @@ lt_beam_hw(DecodeParams p) {
         const int hr = act ? r : 0;
         const VEntry h0 = R[hb][hr];
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
+        // a dup (BM_DEDUP, lt_beam_pk): its lead's expansion of this candidate is g - gdist
+        const int ldr = DEDUP ? (int)lead9[wv][hf][hb][hr] : hr;
+        const int gdist = (hr - ldr) * m;
+        const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
+        // ... and at most 7 features can be present (classes 0-3, and of
+        // f4 / f5 / f6 / class 7 / class 8 at most three): numpy's sum is then
+        // left to right (H7), which s4 starts
+        const uint32_t xb = ((c.mask >> 18) & 1u) + ((c.mask >> 19) & 1u) + ((h0.meta >> 20) & 1u) +
+                            ((need >> 4) & 1u) + ((need >> 5) & 1u);
+        const bool dup = DEDUP && !skip && has_tri && ldr != hr && gdist < G && xb <= 3u;
         BMProbe<NARROW> P;
-        bm_issue<NARROW, true>(P, B, slots, seed, h0, c, (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u, aux);
+        bm_issue<NARROW, true>(P, B, slots, seed, h0, c, dup ? (need & 0x30u) : need, aux);
         asm volatile("" ::: "memory");
         const VEntry h1 = R[hb][hr];
+        // the trigram term: a lead's (or a lane without dedup) from all its
+        // classes; a dup's in v1_sum's left-to-right order continued from its
+        // lead's s4 with its own classes 7 and 8
+        double tri = 0.0, c78[2] = {-0.0, -0.0};
+        if (has_tri) {
+          double cf[6];
+          uint32_t pres;
+          bm_classes<NARROW>(P, h1, c, cf, pres);
+          c78[0] = cf[4];
+          c78[1] = cf[5];
+          if (!dup) tri = v1_sum(cf, pres, c, h1);
+          if (DEDUP && !skip && !dup) {
+            const int q = g & (DQ - 1);
+            dds[wv][hf][q] = (((0.0 + cf[0]) + cf[1]) + cf[2]) + cf[3];
+          }
+        }
+        if (DEDUP && has_tri) {
+          __builtin_amdgcn_wave_barrier();
+          if (dup) {
+            const double s4 = dds[wv][hf][(g - gdist) & (DQ - 1)];
+            tri = ((((s4 + c.f4) + c.f5) + h1.f6) + c78[0]) + c78[1];
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
         if (!skip) {
-          const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
@@ -1970,9 +2126,9 @@ lt_beam_hw(DecodeParams p) {
     VEntry ne;
     uint32_t bpv = 0;
     const bool writer = live && hl < nrun;
-    int wj = 0, wr = 0, wi = 0, wsj = 0;
+    int wj = 0, wr = 0, wi = 0, wsj = 0, wm = 1;
     bool wimp = false;
-    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi, wsj, wimp);
+    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi, wsj, wimp, wm);
     const int wd = MAX_SPAN - wj;
     const uint32_t wnode = wimp ? UNK_LOCAL : (uint32_t)(wsj + wi);
     const bool far = writer && !wimp && (int)wnode - A0 >= STAGE;
@@ -1992,6 +2148,18 @@ lt_beam_hw(DecodeParams p) {
     if (writer) R[em9][hl] = ne;
     __builtin_amdgcn_raw_buffer_store_b32(
         bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, 0);
+    if (DEDUP) {
+      // each entry's lead (lt_beam_pk): the first rank with the same (word, tag)
+      __builtin_amdgcn_wave_barrier();
+      if (writer) {
+        int ld = hl;
+        for (int q = hl - 1; q >= 0; --q) {
+          const uint2 jw = *reinterpret_cast<const uint2*>(&R[em9][q].jword);
+          ld = (jw.x == ne.jword && jw.y == ne.jtag) ? q : ld;
+        }
+        lead9[wv][hf][em9][hl] = (uint8_t)ld;
+      }
+    }
     if (live && hl == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
   }

@@ -78,7 +78,10 @@ def evaluate_batch(sequences, score_functions, device=0):
             cols['f5'].append(0.0 if c5 is None else c5)
             cols['f6'].append(0.0 if c6 is None else c6)
             for t, f in enumerate(local):
-                if getattr(f, 'edge_local', False) is True and type(f).__name__ not in NODE_LOCAL_SCORERS:
+                # (LoweredModel's precedence: a plugin declaring node_local as
+                # well is lowered -- and evaluated -- as node-local)
+                if (getattr(f, 'edge_local', False) is True and getattr(f, 'node_local', False) is not True
+                        and type(f).__name__ not in NODE_LOCAL_SCORERS):
                     # an edge plugin's own evaluate(seq) (user code, host), as one
                     # value of the path: ((0 + E) + -0.0) + ... == E
                     sq = seq if hasattr(seq, 'sequences') else EdgeSequence(None, words)

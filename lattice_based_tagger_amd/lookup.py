@@ -299,9 +299,10 @@ def _gather_strings(blob, off, idx):
 
 
 class SentChars:
-    """The sentences' decode characters as a sequence of str, decoded from the
-    lattices' UTF-32 buffer on access (``cps``, ``off``: the buffer and the
-    sentence offsets, for bulk consumers)."""
+    """The sentences' decode characters as a sequence of str, decoded from a
+    UTF-32 buffer on access (``cps``, ``off``: the buffer and the sentence
+    offsets, for bulk consumers; NativeLattices hands it copies of its own,
+    so it stays valid after the lattices are closed)."""
 
     def __init__(self, cps, off):
         self.cps, self.off = cps, off
@@ -347,9 +348,10 @@ class NativeLattices:
                       'e': arr(c.e, C.c_int32, N, np.int32), 'is_l': arr(c.is_l, C.c_uint8, N, np.uint8)}
         self._view = None
         self._cols = None
-        # each sentence's characters (sent.replace(' ', '')), decoded on access
-        self.chars = SentChars(arr(c.chars, C.c_uint32, int(self.char_off[-1]) if S else 0, np.uint32),
-                               self.char_off)
+        # each sentence's characters (sent.replace(' ', '')), decoded on access;
+        # copies (4 B per character), so the sequence outlives these lattices
+        self.chars = SentChars(arr(c.chars, C.c_uint32, int(self.char_off[-1]) if S else 0, np.uint32).copy(),
+                               self.char_off.copy())
 
     @property
     def desc(self):

@@ -123,6 +123,13 @@ class Tagger:
     def __init__(self, dictionary='base', lookup='subword_lookup', encoder=None,
                  score_funcs=None, device=0, lexicon=None, native_lookup=True, lookup_threads=0,
                  custom_lookup=None):
+        if callable(lookup):
+            # the reference ignores lookup (tagger.py:57-62) and so does this
+            # Tagger; a caller handing a callable most likely wants it used
+            import warnings
+            warnings.warn('Tagger ignores lookup= as the reference does (tagger.py:57-62); pass '
+                          'custom_lookup=<callable(eojeol, offset) -> [Word]> to build the lattices with it',
+                          stacklevel=2)
         self._lexicon = lexicon
         self._lexicon_given = lexicon is not None     # used as given, never rebuilt
         self._eojeol_lookup = None

@@ -61,16 +61,48 @@ def test_scalar_table_and_coefficient_edits_relower():
 
 
 def test_read_only_coefficients_skip_the_content_hash():
-    """A read-only coefficient array cannot change, so its identity is its
-    fingerprint (no per-call hash of the array); a read-only view of a
-    writeable array is still hashed (the owner can write through)."""
+    """Coefficients over read-only memory (bytes, a read-only mmap: a model
+    pack) cannot change, so their identity is their fingerprint (no per-call
+    hash of the array).  An array that owns its memory is hashed even when
+    read-only: its owner can set writeable back, edit it and clear the flag
+    again; a read-only view of a writeable array likewise."""
+    frozen = np.frombuffer(np.arange(1000, dtype=np.float64).tobytes(), dtype=np.float64)
+    assert not frozen.flags.writeable
+    assert beam._digest_array(frozen)[0] == 'ro'
     owned = np.arange(1000, dtype=np.float64)
     owned.flags.writeable = False
-    assert beam._digest_array(owned)[0] == 'ro'
+    d0 = beam._digest_array(owned)
+    assert d0[0] != 'ro'
+    owned.flags.writeable = True
+    owned[7] = 123.0
+    owned.flags.writeable = False
+    assert beam._digest_array(owned) != d0
     base = np.arange(1000, dtype=np.float64)
     view = base[:]
     view.flags.writeable = False
-    d0 = beam._digest_array(view)
-    assert d0[0] != 'ro'
+    d1 = beam._digest_array(view)
+    assert d1[0] != 'ro'
     base[3] = -1.0
-    assert beam._digest_array(view) != d0
+    assert beam._digest_array(view) != d1
+
+
+def test_flipped_writeable_flag_relowers_the_model():
+    """Flip a read-only owned coefficient array writeable, edit it, flip it
+    back: the next call lowers the model again (no stale scores)."""
+    from golden_io import load
+    case = load('synth')[0]
+    tri = [f for f in case.funcs.funcs if type(f).__name__ == 'SimpleTrigramFeatureScore'][0]
+    coef = tri.coefficients
+    coef.flags.writeable = False
+    try:
+        m1 = beam.lowered_model(case.funcs)
+        assert beam.lowered_model(case.funcs) is m1
+        coef.flags.writeable = True
+        coef[0] += 1.0
+        coef.flags.writeable = False
+        m2 = beam.lowered_model(case.funcs)
+        assert m2 is not m1
+        assert m2.coefs is not None
+    finally:
+        coef.flags.writeable = True
+        coef[0] -= 1.0
