@@ -181,7 +181,8 @@ def test_tagger_ignores_lookup_argument_like_the_reference(fix):
         calls.append(eojeol)
         return []
 
-    t = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lookup=f, lexicon=fixture_lexicon(entry))
+    with pytest.warns(UserWarning, match='custom_lookup'):   # (the caller is told which keyword uses it)
+        t = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lookup=f, lexicon=fixture_lexicon(entry))
     for sent, exp in list(zip(entry['sentences'], entry['lattices']))[:10]:
         bindex, _ = t.lattice(sent)
         assert [[list(w) for w in ws] for ws in bindex] == exp
