@@ -25,13 +25,20 @@ from .tagset import BOS, EOS, Noun, Unk
 class BeamScoreFunction:
     """Protocol for one additive term of the expansion score.
 
-    A subclass whose ``score(seq, word_k)`` depends on ``word_k`` only may set
-    ``node_local = True``: the decoder then evaluates ``score(None, w)`` once
-    per lattice node (host side) and adds it on the device in constructor
-    order, as it does for the built-in node-local scorers.  Any other user
-    subclass has no device lowering (``NotImplementedError``)."""
+    Two kinds of user subclass are lowered to the device, in constructor
+    order, like the built-in scorers:
+
+    * ``node_local = True`` -- ``score(seq, word_k)`` reads ``word_k`` only:
+      evaluated as ``score(None, w)`` once per lattice node (host side);
+    * ``edge_local = True`` -- it reads ``seq.sequences[-1]`` and ``word_k``
+      only: evaluated once per lattice edge (last word wj -> candidate w),
+      host side, with a ``seq`` whose ``sequences`` ends in wj.
+
+    A subclass that reads more of the path has no device lowering and is
+    refused (``NotImplementedError``), never evaluated on a CPU path."""
 
     node_local = False
+    edge_local = False
 
     def __call__(self, sequence, word_k):
         return self.score(sequence, word_k)
