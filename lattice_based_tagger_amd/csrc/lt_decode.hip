@@ -784,7 +784,7 @@ __device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntr
 // bit-identical.
 // ---------------------------------------------------------------------------
 #ifndef BM_DEDUP
-#define BM_DEDUP 1
+#define BM_DEDUP 0          // measured slower (round 4: k=5 4.96 vs 4.25 ms, k=16 17.0 vs 11.6 ms)
 #endif
 // The cache holds DD_Q entries, entry g mod DD_Q; a dup is within DD_WIN =
 // DD_Q expansions of its lead, so no expansion between them rewrites the
@@ -922,11 +922,14 @@ struct alignas(16) SentRec {
 // the slot's nodes in bindex order, or its implicit Unknown); macro-step r of
 // e covers list entries [64r, 64r + 64).  Entry of lane l: lt_internal.h K1_*.
 // ---------------------------------------------------------------------------
+constexpr int SCH_CHUNK = 32;                   // end positions whose span starts one LDS fill holds
 template <int W>
 __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
   static_assert(W < 8, "the sentence field holds W - 1");
+  constexpr int SPN = SCH_CHUNK * MAX_SPAN + 1;
   __shared__ int spre[W][MAX_SPAN + 1];         // sentence w at e: candidate prefix over its span slots
   __shared__ int sfirst[W][MAX_SPAN + 1];       // and each slot's first piece-global node
+  __shared__ int spl[W][SPN];                   // span starts of SCH_CHUNK end positions per sentence
   const int wave = blockIdx.x;
   const int lane = (int)threadIdx.x;
   const int slot0 = wave * W;
@@ -935,26 +938,49 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
   const int sid = own ? p.order[slot0 + lane] : 0;
   const int nw = own ? p.sent_n[sid] : 0;
   const uint32_t nbase = own ? (uint32_t)p.node_off[sid] : 0u;
-  const int32_t* const ssp = p.span_start + (own ? p.span_off[sid] : 0);
+  const int64_t soff = own ? p.span_off[sid] : 0;
   int nmax = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) nmax = max(nmax, __builtin_amdgcn_readlane(nw, w));
   int64_t step = 0;
   uint32_t* const out = sched + wave_off[wave] * 64 + lane;
   for (int e = 1; e <= nmax; ++e) {
+    if ((e - 1) % SCH_CHUNK == 0) {
+      // the span starts of end positions [e, e + SCH_CHUNK) of every sentence,
+      // loaded by all lanes at once (one memory round trip per chunk instead
+      // of one per position)
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const int n_w = __builtin_amdgcn_readlane(nw, w);
+        const int64_t so = ((int64_t)__builtin_amdgcn_readlane((int)(soff >> 32), w) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)soff, w);
+        const int lim = min(SPN, (n_w - e + 1) * MAX_SPAN + 1);      // entries up to 8 n_w
+        const int32_t* const src = p.span_start + so + (int64_t)(e - 1) * MAX_SPAN;
+        int v[(SPN + 63) / 64];
+#pragma unroll
+        for (int t = 0; t < (SPN + 63) / 64; ++t) v[t] = lane + 64 * t < lim ? src[lane + 64 * t] : 0;
+#pragma unroll
+        for (int t = 0; t < (SPN + 63) / 64; ++t)
+          if (lane + 64 * t < SPN) spl[w][lane + 64 * t] = v[t];
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    }
     // the owner lane of each sentence: its slots' candidates and first nodes
     int X = 0;
     if (lane < W) {
       const bool live = own && e <= nw;
       const int dmax = min(e, p.max_len);
+      const int eb = ((e - 1) % SCH_CHUNK) * MAX_SPAN;
       int run = 0;
 #pragma unroll
       for (int j = 0; j <= MAX_SPAN; ++j) {
-        const int a = live ? ssp[(e - 1) * MAX_SPAN + j] : 0;
+        const int a = live ? spl[lane][eb + j] : 0;
         sfirst[lane][j] = (int)nbase + a;
         spre[lane][j] = run;
         if (j < MAX_SPAN) {
-          const int c = live ? ssp[(e - 1) * MAX_SPAN + j + 1] - a : 0;
+          const int c = live ? spl[lane][eb + j + 1] - a : 0;
           run += (live && c == 0 && MAX_SPAN - j <= dmax) ? 1 : c;     // empty in-range slot: implicit Unknown
         }
       }

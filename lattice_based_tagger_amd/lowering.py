@@ -36,6 +36,9 @@ is no CPU fallback decoder.
 import numpy as np
 
 from .feature import FEATURE_ARITY, EXPANSION_CLASSES
+from .tagset import POS_TAGS, Unk, BOS, EOS
+
+TAG_IDS_FIRST = POS_TAGS + (Unk, BOS, EOS)
 
 # ---------------------------------------------------------------------------
 # Node mask bits (shared with csrc/lt_decode.hip and oracle/lt_oracle.c).
@@ -206,6 +209,10 @@ class LoweredModel:
         self.feature_dic = dic
         self.coefficients = coef
         vocab = self.vocab
+        # the tag set first: ids 1..13, distinct in their low four bits -- the
+        # slot inside a key's line group (lt_common.h, HASH_VERSION 5)
+        for t in TAG_IDS_FIRST:
+            vocab[t] = len(vocab) + 1
         keys, coefs, slot_pairs = [], [], []
         cls_of = _ClassIndex.table
         n_coef = coef.shape[0]

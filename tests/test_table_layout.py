@@ -37,14 +37,24 @@ def mul24(x, k):
 
 
 def slot(h, a, b, c, cls, slots, which):
-    """HASH_VERSION 4: one mix x, i1 = x >> s, i2 = ((x ^ x >> 16) * K2) >> s on
-    2^n slots (s = 32 - n)."""
+    """HASH_VERSION 5: one mix x over the key without its sub component (the
+    tag of classes 0 / 1 / 2 / 3: c, b, a, b), i1 = (x >> s) & ~15 | sub & 15
+    (x >> s for classes 7 / 8), i2 = ((x ^ x >> 16 ^ sub) * K2) >> s on 2^n
+    slots (s = 32 - n)."""
     assert slots & (slots - 1) == 0
     shift = np.uint64(32 - (int(slots).bit_length() - 1))
-    x = mul24(a, h[0]) ^ mul24(b, h[1]) ^ mul24(c, h[2]) ^ _u32(cls.astype(np.uint64) * np.uint64(h[3]))
+    cls = np.asarray(cls)
+    sp = np.select([cls == 0, cls == 1, cls == 2, cls == 3], [2, 1, 0, 1], -1)
+    comps = [np.asarray(a, np.uint64), np.asarray(b, np.uint64), np.asarray(c, np.uint64)]
+    zero = np.uint64(0)
+    ma, mb, mc = (np.where(sp == i, zero, mul24(comps[i], h[i])) for i in range(3))
+    sub = np.select([sp == 0, sp == 1, sp == 2], comps, zero).astype(np.uint64)
+    x = ma ^ mb ^ mc ^ _u32(cls.astype(np.uint64) * np.uint64(h[3]))
     if which == 2:
-        x = _u32((x ^ (x >> np.uint64(16))) * np.uint64(h[4]))
-    return (x >> shift).astype(np.int64)
+        return (_u32((x ^ (x >> np.uint64(16)) ^ sub) * np.uint64(h[4])) >> shift).astype(np.int64)
+    i = x >> shift
+    g = np.uint64(15)
+    return np.where(sp >= 0, (i & ~g) | (sub & g), i).astype(np.int64)
 
 
 def narrow_key(a, b, c, cls):
@@ -82,7 +92,7 @@ def model():
 
 def test_every_key_found_with_primary_first_lookup(model):
     keys, coefs, arr = model
-    assert arr['narrow'] == 1 and arr['hash_version'] == 4
+    assert arr['narrow'] == 1 and arr['hash_version'] == 5
     table = arr['table'].view(np.uint64).reshape(-1, 2)
     h = narrow_hash(arr['seed'])
     a, b, c, cls = keys.T

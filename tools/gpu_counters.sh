@@ -5,7 +5,7 @@
 # microkernels (tools/fetch_calib).  Output under gpurun_out/counters/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/counters
+O=$R/gpurun_out/${OUT:-counters}      # OUT: output dir; LT_LIBRARY: the library; NPASS: first N passes only
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python3 $R/tools/prof_decode.py --k 1 --steps 1 --cache /tmp/ltw > $O/gen.log 2>&1 || { echo GEN_FAIL; tail -5 $O/gen.log; exit 1; }
@@ -21,6 +21,7 @@ for K in ${KS:-1 2 5 16}; do
   i=0
   for G in "${PASSES[@]}"; do
     i=$((i+1))
+    [ $i -gt ${NPASS:-99} ] && break
     timeout -s KILL 150 rocprofv3 --pmc $G -T --output-format csv -d $O/k$K/p$i -o run -- python3 $R/tools/prof_decode.py --k $K --steps 3 --cache /tmp/ltw > $O/k${K}_p$i.log 2>&1 || { echo PASS_FAIL k=$K p=$i; tail -5 $O/k${K}_p$i.log; exit 1; }
   done
   python3 $R/tools/pmc_table.py $O/k$K lt_ > $O/k$K.txt
