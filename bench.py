@@ -42,13 +42,13 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 # Load the HIP library before anything that could pull another HIP runtime in.
-from lattice_based_tagger_amd import _capi, synth  # noqa: E402
+from lattice_based_tagger_amd import _capi, synth, lowering as Lw  # noqa: E402
 
 METRIC = 'sentences/sec Viterbi decode, 64K-sentence batch; achieved HBM GB/s vs 8 TB/s'
 HBM_PEAK_GBS = 8000.0
 # batch layout of this revision (implicit Unknowns, lattice_decode.h ABI 5): PMC
 # traffic summaries are only matched to a run of the same layout
-LAYOUT = 'abi5-implicit-unk'
+LAYOUT = 'abi5-rec32'
 
 
 BASE_SENTENCES = 65536         # lattices generated per seed (config 3); larger batches permute them
@@ -186,10 +186,11 @@ def algorithmic_bytes(piece, n_dict, tuples, length, count, k):
 PK_BPL = 87                    # k=1: end positions whose backpointers stay in LDS (lt_decode.hip)
 
 
-def kernel_bytes(piece, table_loads, k, prep_bytes, blocks, d3):
+def kernel_bytes(piece, table_loads, k, prep_bytes, blocks, d3, n_pairs=1):
     """The bytes the decode kernel must move per launch -- the roofline's
-    byte model (no kernel reads less): every node record once (48 B; the
-    implicit Unknowns' records are staged from one 384 B block per workgroup),
+    byte model (no kernel reads less): every node record once (32 B; the
+    implicit Unknowns' records are staged from one 256 B block per workgroup,
+    and at k=1 the class-4/6 pair table, ``n_pairs`` x 16 B, per workgroup),
     the k=1 lane schedule (``prep_bytes``) or, for beams, the span starts; the
     per-sentence offsets; 16 B per feature-table slot load actually issued
     (counted by the counting launch past the node pre-filter); the dense
@@ -207,8 +208,23 @@ def kernel_bytes(piece, table_loads, k, prep_bytes, blocks, d3):
         meta = 40 * S + 4 * int(len(piece.span_start))
         bp = 4 * int(((n + 1) * k).sum()) + 4 * chars * k      # written per (position, rank), read on paths
     results = 16 * S * k + 4 * chars * k                        # count, length, score; padded codes
-    stage = blocks * (384 + (8192 if d3 and k <= 4 else 0))
-    return 48 * piece.n_nodes + meta + 16 * table_loads + stage + bp + results
+    stage = blocks * (256 + (16 * n_pairs if k == 1 else 0) + (8192 if d3 and k <= 4 else 0))
+    return 32 * piece.n_nodes + meta + 16 * table_loads + stage + bp + results
+
+
+def pair_count(batch):
+    """Entries of the batch's class-4/6 pair table (lt_capi.cpp PairTable):
+    the distinct (f4, f6) pairs of the nodes and implicit Unknowns, absent
+    coefficients -0.0, plus the both-absent entry."""
+    def pairs(mask, f4, f6):
+        mask = np.asarray(mask, dtype=np.uint32)
+        a = np.where(mask & Lw.F_HAS4, np.asarray(f4, dtype=np.float64), -0.0).view(np.uint64)
+        b = np.where(mask & Lw.F_HAS6, np.asarray(f6, dtype=np.float64), -0.0).view(np.uint64)
+        return np.stack([a, b], 1)
+    x = [pairs(batch.node_mask, batch.node_f4, batch.node_f6), np.array([[1 << 63, 1 << 63]], dtype=np.uint64)]
+    if getattr(batch, 'unk_n', 0):
+        x.append(pairs(batch.unk_mask, batch.unk_f4, batch.unk_f6))
+    return min(len(np.unique(np.concatenate(x), axis=0)), 127)
 
 
 def has_dense3(keys):
@@ -503,7 +519,7 @@ def main():
     nd = dict_nodes(raw, order, lo, hi)
     B = algorithmic_bytes(piece, nd, tuples, length, count, k)
     KB = kernel_bytes(piece, table_loads, k, db.prep_bytes() if k == 1 else 0, workgroups(k, piece.n_sent),
-                      has_dense3(keys))
+                      has_dense3(keys), pair_count(piece))
     achieved = KB / avg_kernel_s / 1e9
     # the roofline's byte model is what the kernel must move: it cannot run
     # faster than HBM moves it

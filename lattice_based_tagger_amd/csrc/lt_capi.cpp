@@ -97,6 +97,77 @@ struct KeyRec {
   double coef;
 };
 
+// The class-4/6 pair table of a set of records (NodeRec): distinct (f4, f6)
+// bit patterns -> index, at most MAX_PAIRS entries (entry 0 = both absent);
+// a record whose pair does not fit takes PX_ESC and the escape array.
+struct PairTable {
+  static constexpr int CAP = 256;                  // open addressing, > 2 x MAX_PAIRS
+  std::vector<F46> vals;
+  uint64_t ka[CAP], kb[CAP];
+  int16_t idx[CAP];
+  bool full = false;                               // some pair did not fit
+  PairTable() { std::fill(idx, idx + CAP, (int16_t)-1); }
+  static uint64_t bits(double v) {
+    uint64_t u;
+    std::memcpy(&u, &v, 8);
+    return u;
+  }
+  static uint32_t home(uint64_t a, uint64_t b) {
+    return (uint32_t)(((a * 0x9E3779B97F4A7C15ull) ^ (b * 0xC2B2AE3D27D4EB4Full)) >> 56);
+  }
+  int find(double f4, double f6) const {
+    const uint64_t a = bits(f4), b = bits(f6);
+    for (uint32_t i = home(a, b);; i = (i + 1) & (CAP - 1)) {
+      if (idx[i] < 0) return -1;
+      if (ka[i] == a && kb[i] == b) return idx[i];
+    }
+  }
+  int add(double f4, double f6) {
+    const uint64_t a = bits(f4), b = bits(f6);
+    uint32_t i = home(a, b);
+    for (;; i = (i + 1) & (CAP - 1)) {
+      if (idx[i] < 0) break;
+      if (ka[i] == a && kb[i] == b) return idx[i];
+    }
+    if ((int)vals.size() >= MAX_PAIRS) {
+      full = true;
+      return -1;
+    }
+    ka[i] = a; kb[i] = b;
+    idx[i] = (int16_t)vals.size();
+    vals.push_back(F46{f4, f6});
+    return idx[i];
+  }
+};
+// The pair of a record from the API columns (absent: -0.0)
+static inline F46 api_pair(uint32_t am, const double* f4, const double* f6, int64_t i) {
+  return F46{(am & F_HAS4) ? f4[i] : -0.0, (am & F_HAS6) ? f6[i] : -0.0};
+}
+// The table of records [0, n) (masks / f4 / f6 columns), the `first` pairs
+// entered before them: per thread, then merged in thread order.
+static PairTable pair_table(int64_t n, const uint32_t* mask, const double* f4, const double* f6,
+                            const std::vector<F46>& first) {
+  PairTable tab;
+  tab.add(-0.0, -0.0);
+  for (const F46& f : first) tab.add(f.f4, f.f6);
+  std::vector<PairTable> local(32);
+  parallel_ranges(n, [&](int t, int64_t lo, int64_t hi) {
+    PairTable& lt = local[(size_t)t];
+    F46 last{-0.0, -0.0};
+    for (int64_t i = lo; i < hi && !lt.full; ++i) {
+      const F46 f = api_pair(mask[i], f4, f6, i);
+      if (std::memcmp(&f, &last, sizeof f) == 0) continue;
+      last = f;
+      lt.add(f.f4, f.f6);
+    }
+  }, 1 << 16);
+  for (const PairTable& lt : local) {
+    for (const F46& f : lt.vals) tab.add(f.f4, f.f6);
+    tab.full |= lt.full;
+  }
+  return tab;
+}
+
 }  // namespace
 
 // Infinite score terms: +inf and -inf may each occur, but not both in one
@@ -948,6 +1019,20 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     }
   }
 
+  // the class-4/6 pair table of the records (NodeRec): the implicit
+  // Unknowns' pairs first (their records are read without an escape)
+  std::vector<F46> unk_pairs;
+  for (int32_t i = 0; i < d->n_unk; ++i) unk_pairs.push_back(api_pair(d->unk_mask[i], d->unk_f4, d->unk_f6, i));
+  const PairTable ptab = pair_table(d->n_nodes, d->node_mask, d->node_f4, d->node_f6, unk_pairs);
+  for (const F46& f : unk_pairs)
+    if (ptab.find(f.f4, f.f6) < 0) {
+      delete b;
+      return fail(LT_EUNSUPPORTED, "lt_batch_create: more than %d distinct class-4/6 coefficient pairs among "
+                                   "the implicit Unknowns", MAX_PAIRS - 1);
+    }
+  const bool has_esc = ptab.full && d->n_nodes > 0;
+  b->n_pairs = (int32_t)ptab.vals.size();
+
   hipStream_t stm = c->ustream;     // complete when this returns (synchronised below)
   const size_t nres = (size_t)S * max_k;
   const size_t ncodes = (size_t)b->total_chars * max_k;
@@ -974,6 +1059,8 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   const size_t o_sent_n = cv.dev((size_t)S * 4), o_cum_n = cv.dev(((size_t)S + 1) * 8);
   const size_t o_unk = cv.dev((size_t)d->n_unk * sizeof(NodeRec)),
                o_unk_post = cv.dev((size_t)d->n_post * (size_t)d->n_unk * 8);
+  const size_t o_pairs = cv.dev(ptab.vals.size() * sizeof(F46)),
+               o_esc = cv.dev(has_esc ? (size_t)d->n_nodes * sizeof(F46) : 0);
   b->slab_cap = slab_layout(S, max_k, b->total_chars).capacity;
   const uint64_t slab_alloc = slab_alloc_bytes(S, max_k, b->total_chars);
   size_t o_count[2], o_len[2], o_score[2], o_codes[2], o_slab[2];
@@ -1023,6 +1110,9 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   b->d_cum_n = at<int64_t>(D, o_cum_n);
   b->d_unk = at<NodeRec>(D, o_unk);
   b->d_unk_post = at<double>(D, o_unk_post);
+  b->d_pairs = at<F46>(D, o_pairs);
+  for (size_t q = 0; q < P; ++q)
+    b->pieces[q].d_esc = has_esc ? at<F46>(D, o_esc) + b->pieces[q].node0 : nullptr;
   for (int i = 0; i < 2; ++i) {
     b->res[i].count = at<int32_t>(D, o_count[i]);
     b->res[i].len = at<int32_t>(D, o_len[i]);
@@ -1050,11 +1140,19 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     batch_free(b);
     return fail(LT_ENOMEM, "lt_batch_create: out of host memory");
   }
+  // the escape array of nodes whose pair is not in the table (host copy)
+  std::unique_ptr<F46[]> esc_h(has_esc ? new (std::nothrow) F46[(size_t)d->n_nodes] : nullptr);
+  if (has_esc && !esc_h) {
+    batch_free(b);
+    return fail(LT_ENOMEM, "lt_batch_create: out of host memory");
+  }
   // sentence by sentence on threads: the records, then each node's span
-  // length d-1 (bits 24-26) from the span table
+  // length d-1 (bits 21-23) from the span table
   parallel_ranges(S, [&](int, int64_t lo, int64_t hi) {
     for (int64_t s = lo; s < hi; ++s) {
       const int64_t base = d->sent_node_off[s];
+      F46 last{-0.0, -0.0};
+      uint32_t last_px = 0;
       for (int64_t i = base; i < d->sent_node_off[s + 1]; ++i) {
         NodeRec& r = recs[(size_t)i];
         r.word = (uint32_t)d->node_word[i];
@@ -1062,13 +1160,19 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
         r.tag = (uint32_t)d->node_tag[i];
         // device mask layout (lt_common.h device_mask); an absent class 4/5/6
         // coefficient is stored as -0.0, the identity of a float64 sum, so a
-        // decoder may add it unconditionally
-        const uint32_t am = (uint32_t)d->node_mask[i];
-        r.mask = device_mask(am);
+        // decoder may add it unconditionally; classes 4 / 6 as the index of
+        // their pair
+        const uint32_t am = d->node_mask[i];
+        const F46 f = api_pair(am, d->node_f4, d->node_f6, i);
+        if (std::memcmp(&f, &last, sizeof f) != 0) {
+          const int x = ptab.find(f.f4, f.f6);
+          last = f;
+          last_px = x < 0 ? PX_ESC : (uint32_t)x;
+        }
+        if (last_px == PX_ESC) esc_h[(size_t)i] = f;
+        r.mask = device_mask(am) | (last_px << PX_SHIFT);
         r.pre = d->node_pre[i];
-        r.f4 = (am & F_HAS4) ? d->node_f4[i] : -0.0;
         r.f5 = (am & F_HAS5) ? d->node_f5[i] : -0.0;
-        r.f6 = (am & F_HAS6) ? d->node_f6[i] : -0.0;
       }
       // (the general kernel of max_len > 8 takes the span from the table)
       const int32_t* ss = d->span_start + d->sent_span_off[s];
@@ -1089,13 +1193,15 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     r.word = (uint32_t)d->unk_word[i];
     r.morph = (uint32_t)d->unk_morph0[i];
     r.tag = (uint32_t)d->unk_tag[i];
-    r.mask = device_mask(am) | ((uint32_t)(std::min(MAX_SPAN, i + 1) - 1) << D_SHIFT);
+    const F46 f = unk_pairs[(size_t)i];
+    r.mask = device_mask(am) | ((uint32_t)(std::min(MAX_SPAN, i + 1) - 1) << D_SHIFT) |
+             ((uint32_t)ptab.find(f.f4, f.f6) << PX_SHIFT);
     r.pre = d->unk_pre[i];
-    r.f4 = (am & F_HAS4) ? d->unk_f4[i] : -0.0;
     r.f5 = (am & F_HAS5) ? d->unk_f5[i] : -0.0;
-    r.f6 = (am & F_HAS6) ? d->unk_f6[i] : -0.0;
   }
   up(b->d_unk, unk_recs.data(), unk_recs.size());
+  up(b->d_pairs, ptab.vals.data(), ptab.vals.size());
+  if (has_esc) up(at<F46>(D, o_esc), esc_h.get(), (size_t)d->n_nodes);
   if (d->n_post > 0) up(b->d_unk_post, d->unk_post, (size_t)d->n_post * (size_t)d->n_unk);
   std::vector<std::vector<int64_t>> edge_base_tmp(P);
   for (size_t q = 0; q < P; ++q) {
@@ -1222,6 +1328,8 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.n_unk = b->n_unk;
   p.unk = b->d_unk;
   p.unk_post = b->d_unk_post;
+  p.pairs = b->d_pairs;
+  p.n_pairs = b->n_pairs;
   return LT_OK;
 }
 
@@ -1237,6 +1345,7 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
   p.span_off = pc.d_span_off;
   p.span_start = pc.d_span_start;
   p.nodes = pc.d_nodes;
+  p.esc = pc.d_esc;
   p.npost = pc.d_post;
   p.sched = pc.d_sched;
   p.wave_off = pc.d_wave_off;
@@ -1362,24 +1471,30 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
     if (std::isnan(d->terms[x])) return fail(LT_EUNSUPPORTED, "lt_evaluate: NaN term");
   HIP_TRY(hipSetDevice(c->device));
   std::vector<NodeRec> recs((size_t)d->n_words);
+  std::vector<F46> esc((size_t)d->n_words);
   for (int64_t w = 0; w < d->n_words; ++w) {
     NodeRec& r = recs[(size_t)w];
     r.word = (uint32_t)d->word[w];
     r.morph = (uint32_t)d->morph0[w];
     r.tag = (uint32_t)d->tag[w];
-    r.mask = device_mask((uint32_t)d->mask[w]);          // lt_common.h device layout
+    // lt_common.h device layout; every word's class-4/6 pair from the escape
+    // array (evaluate is no hot path)
+    r.mask = device_mask((uint32_t)d->mask[w]) | (PX_ESC << PX_SHIFT);
     r.pre = 0.0;
-    r.f4 = d->f4[w];
     r.f5 = d->f5[w];
-    r.f6 = d->f6[w];
+    esc[(size_t)w] = F46{d->f4[w], d->f6[w]};
   }
+  const F46 absent{-0.0, -0.0};
   hipStream_t st = c->stream;
   hipError_t e = hipSuccess;
   NodeRec* d_words = nullptr;
+  F46 *d_pairs = nullptr, *d_esc = nullptr;
   int64_t *d_p1 = nullptr, *d_p2 = nullptr, *d_off = nullptr;
   double *d_terms = nullptr, *d_inc = nullptr, *d_out = nullptr;
   const size_t nw = (size_t)d->n_words, np = (size_t)d->n_paths;
   e = dalloc_copy(&d_words, recs.data(), nw, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_pairs, &absent, 1, st);
+  if (e == hipSuccess) e = dalloc_copy(&d_esc, esc.data(), nw, st);
   if (e == hipSuccess) e = dalloc_copy(&d_p1, d->prev1, nw, st);
   if (e == hipSuccess) e = dalloc_copy(&d_p2, d->prev2, nw, st);
   if (e == hipSuccess) e = dalloc_copy(&d_off, d->path_off, np + 1, st);
@@ -1399,6 +1514,8 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
     p.n_paths = d->n_paths;
     p.n_words = d->n_words;
     p.words = d_words;
+    p.pairs = d_pairs;
+    p.esc = d_esc;
     p.prev1 = d_p1;
     p.prev2 = d_p2;
     p.path_off = d_off;
@@ -1411,7 +1528,7 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
   }
   if (e == hipSuccess && np) e = hipMemcpyAsync(scores, d_out, np * sizeof(double), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  void* bufs[] = {d_words, d_p1, d_p2, d_off, d_terms, d_inc, d_out};
+  void* bufs[] = {d_words, d_pairs, d_esc, d_p1, d_p2, d_off, d_terms, d_inc, d_out};
   for (void* b : bufs) dfree(b);
   if (e != hipSuccess) return fail(LT_EHIP, "lt_evaluate: %s", hipGetErrorString(e));
   return LT_OK;

@@ -30,8 +30,9 @@ constexpr uint32_t F_HAS5 = 1u << 19;
 constexpr uint32_t F_HAS6 = 1u << 20;
 constexpr uint32_t FLAG_BITS = 0x1F0000u;
 // set by the library on its device copy of the mask: span length d-1 of the
-// node (bits 24-26); bit 31 marks "wi exists" in hypothesis entries.
-constexpr int D_SHIFT = 24;
+// node (bits 21-23), the pair index (bits 24-30, PX_SHIFT below); bit 31
+// marks "wi exists" in hypothesis entries.
+constexpr int D_SHIFT = 21;
 constexpr uint32_t D_MASK = 7u << D_SHIFT;
 constexpr uint32_t F_WI = 1u << 31;
 
@@ -46,7 +47,8 @@ constexpr uint32_t F_WI = 1u << 31;
 //   bit 12     DJ_NCTX: tag0 not in C (class 8 then comes from (wi, wk))
 //   bit 13     DI_7: as wi of class 7 (I7A); bit 14 DI_8: as wi of class 8 (I8A&ctx)
 //   bits 16-20 the API flags (F_UNK, F_CTX, F_HAS4, F_HAS5, F_HAS6)
-//   bits 24-26 span length d-1 (D_SHIFT); bit 31 F_WI (hypothesis entries)
+//   bits 21-23 span length d-1 (D_SHIFT); bits 24-30 the class-4/6 pair
+//   index (PX_SHIFT, NodeRec); bit 31 F_WI (hypothesis entries)
 constexpr int DJ_SHIFT = 6;
 constexpr uint32_t DQ_ALL = 0x3Fu;
 constexpr uint32_t DJ_NCTX = 1u << 12, DI_7 = 1u << 13, DI_8 = 1u << 14;
@@ -252,12 +254,27 @@ constexpr int D3_DIM = 1 << D3_BITS;
 constexpr uint64_t D3_ABSENT = 0x7FF5A5A55A5A0001ull;     // a NaN payload
 LT_HD uint32_t d3_index(uint32_t v, uint32_t mul) { return (v * mul) >> (32 - D3_BITS); }
 
-// Device node record (AoS, 48 B = 3 x 16 B loads), built by the library from
-// the SoA arrays of lt_batch_desc.
+// Device node record (AoS, 32 B = 2 x 16 B loads), built by the library from
+// the SoA arrays of lt_batch_desc.  The node's class-4 and class-6
+// coefficients (feature.py:100-104: (4, len) and (6, min(8, len)), functions
+// of the length alone, so few distinct values per batch) are a pair in the
+// batch's pair table: mask bits 24-30 (PX_SHIFT) hold its index; PX_ESC
+// (a batch with more distinct pairs than the table holds) sends the node to
+// its own entry of the batch's escape array (piece-global node index).
+// Absent coefficients are -0.0 (the identity of a float64 sum).
 struct alignas(16) NodeRec {
   uint32_t word, morph, tag, mask;
-  double pre, f4, f5, f6;
+  double pre, f5;
 };
+constexpr int REC_CHUNKS = (int)(sizeof(NodeRec) / 16);   // 16 B chunks per record
+struct alignas(16) F46 {
+  double f4, f6;
+};
+constexpr int PX_SHIFT = 24;
+constexpr uint32_t PX_MASK = 0x7Fu << PX_SHIFT;
+constexpr uint32_t PX_ESC = 0x7Fu;                   // the node's pair is in the escape array
+constexpr int MAX_PAIRS = (int)PX_ESC;               // table entries 0..126 (0: both absent)
+LT_HD uint32_t rec_px(uint32_t mask) { return (mask & PX_MASK) >> PX_SHIFT; }
 
 // Backpointer word: local node index (21 b) | span d-1 (3 b) | parent rank (8 b)
 LT_HD uint32_t bp_pack(uint32_t node, uint32_t d, uint32_t r) {

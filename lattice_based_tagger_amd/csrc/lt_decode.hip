@@ -69,6 +69,8 @@ __device__ __forceinline__ u32x4 ld128(rsrc_t r, uint32_t off) {
 
 struct Bufs {
   rsrc_t node, tab;
+  rsrc_t esc;             // class-4/6 pairs of PX_ESC records, by record index
+  const F46* pairs;       // class-4/6 pair table of the records (NodeRec)
 };
 
 __device__ __forceinline__ Bufs make_bufs(const DecodeParams& p) {
@@ -76,6 +78,8 @@ __device__ __forceinline__ Bufs make_bufs(const DecodeParams& p) {
   B.node = make_rsrc(p.nodes, (uint64_t)p.n_nodes * sizeof(NodeRec));
   const uint64_t slot_bytes = p.narrow ? sizeof(SlotN) : sizeof(SlotW);
   B.tab = make_rsrc(p.table, (uint64_t)p.slots * slot_bytes);
+  B.pairs = p.pairs;
+  B.esc = make_rsrc(p.esc, p.esc ? (uint64_t)p.n_nodes * sizeof(F46) : 0u);
   return B;
 }
 
@@ -88,23 +92,45 @@ struct Cand {
 __device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+// The fields of a 32 B record (two 16 B chunks); f4 / f6 -0.0 until
+// set_pair.
+__device__ __forceinline__ Cand rec_cand(uint4 q0, uint4 q1) {
+  Cand c;
+  c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
+  c.pre = dbl(q1.x, q1.y); c.f5 = dbl(q1.z, q1.w);
+  c.f4 = -0.0; c.f6 = -0.0;
+  return c;
+}
+// The record's class-4/6 pair: entry rec_px(mask) of the table `tab` (the
+// batch's pair table, or a block's LDS copy of it), or the escape array's
+// entry of record gn.
+__device__ __forceinline__ void set_pair(Cand& c, const F46* tab, const Bufs& B, uint32_t gn) {
+  const uint32_t px = rec_px(c.mask);
+  const F46 f = tab[px == PX_ESC ? 0u : px];
+  c.f4 = f.f4; c.f6 = f.f6;
+  if (px == PX_ESC && gn != INV) {                 // rare: a batch whose table overflowed
+    // (a buffer load: a plain one would be merged with the table read above
+    // into one flat load of a selected address)
+    const u32x4 e = ld128(B.esc, gn * (uint32_t)sizeof(F46));
+    c.f4 = dbl(e.x, e.y); c.f6 = dbl(e.z, e.w);
+  }
+}
 __device__ __forceinline__ Cand load_cand(const Bufs& B, uint32_t gn) {
   const uint32_t o = gn == INV ? OOB : gn * (uint32_t)sizeof(NodeRec);
   const u32x4 a = ld128(B.node, o);
   const u32x4 b = ld128(B.node, o == OOB ? OOB : o + 16u);
-  const u32x4 c4 = ld128(B.node, o == OOB ? OOB : o + 32u);
-  Cand c;
-  c.word = a.x; c.morph = a.y; c.tag = a.z; c.mask = a.w;
-  c.pre = dbl(b.x, b.y); c.f4 = dbl(b.z, b.w);
-  c.f5 = dbl(c4.x, c4.y); c.f6 = dbl(c4.z, c4.w);
+  Cand c = rec_cand(make_uint4(a.x, a.y, a.z, a.w), make_uint4(b.x, b.y, b.z, b.w));
+  set_pair(c, B.pairs, B, gn);
   return c;
 }
 
 // The implicit Unknown of span length d (lattice_decode.h n_unk; beam.py:36-38:
-// the synthesised Word of a span with no dictionary candidate).
+// the synthesised Word of a span with no dictionary candidate).  Its pair is
+// always in the table (the library enters the Unknowns' pairs first).
 __device__ __forceinline__ Cand unk_cand(const DecodeParams& p, int d) {
   const NodeRec r = p.unk[d - 1];
-  return Cand{r.word, r.morph, r.tag, r.mask, r.pre, r.f4, r.f5, r.f6};
+  const F46 f = p.pairs[rec_px(r.mask)];
+  return Cand{r.word, r.morph, r.tag, r.mask, r.pre, f.f4, r.f5, f.f6};
 }
 // Local node `node` of the sentence whose first node is nbase, or (UNK_LOCAL)
 // the implicit Unknown of span length d.
@@ -112,55 +138,22 @@ __device__ __forceinline__ Cand cand_at(const Bufs& B, const DecodeParams& p, ui
   return node == UNK_LOCAL ? unk_cand(p, d) : load_cand(B, nbase + node);
 }
 // The tuned kernels' copy of the 8 implicit-Unknown records in LDS (record
-// d - 1 at chunks 3(d - 1) .. 3(d - 1) + 2; zeros without implicit Unknowns).
-// Every thread of the block calls it before any early exit.
+// d - 1 at chunks 2(d - 1), 2(d - 1) + 1, as a staged record; zeros without
+// implicit Unknowns).  Every thread of the block calls it before any early
+// exit.
 __device__ __forceinline__ void stage_unk(const DecodeParams& p, uint4* ul) {
-  if (threadIdx.x < 3 * MAX_SPAN)
+  if (threadIdx.x < REC_CHUNKS * MAX_SPAN)
     ul[threadIdx.x] = p.n_unk ? reinterpret_cast<const uint4*>(p.unk)[threadIdx.x] : make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
 }
-__device__ __forceinline__ Cand cand_lds(const uint4* q) {
-  const uint4 q0 = q[0], q1 = q[1], q2 = q[2];
-  Cand c;
-  c.word = q0.x; c.morph = q0.y; c.tag = q0.z; c.mask = q0.w;
-  c.pre = dbl(q1.x, q1.y); c.f4 = dbl(q1.z, q1.w);
-  c.f5 = dbl(q2.x, q2.y); c.f6 = dbl(q2.z, q2.w);
+// A 32 B record staged in LDS (two chunks at q[0], q[step]) with its pair
+__device__ __forceinline__ Cand cand_lds32(const uint4* q, int step, const F46* tab, const Bufs& B, uint32_t gn) {
+  Cand c = rec_cand(q[0], q[step]);
+  set_pair(c, tab, B, gn);
   return c;
 }
 
-// Buffer -> LDS DMA of a block of consecutive node records.  A group of G
-// lanes stages the records [first, first + G) of its sentence: instruction p
-// (p = 0..2) has lane l fetch the contiguous 16 B chunk p*G + l of the block,
-// so each instruction touches 16*G contiguous bytes (4 cache lines per 16
-// lanes) instead of one line per lane.  The DMA writes lane l's 16 B at
-// wave_planes + p*1024 + 16*lane; `gbase` is the group's first lane in its
-// wave.  No VGPR holds the data.
 typedef __attribute__((address_space(3))) void lds_void;
-template <int G>
-__device__ __forceinline__ void dma_block(const Bufs& B, uint32_t first, bool valid, uint4* wave_planes,
-                                          int gl) {
-  const uint32_t base = first * (uint32_t)sizeof(NodeRec);
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {
-    const uint32_t o = valid ? base + (uint32_t)(pl * G + gl) * 16u : OOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wave_planes + pl * 64), 16, o, 0, 0, 0);
-  }
-}
-// record r (0 <= r < G) of the staged block
-template <int G>
-__device__ __forceinline__ Cand read_block(const uint4* wave_planes, int gbase, int r) {
-  uint4 q[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int c = 3 * r + t;
-    q[t] = wave_planes[(c / G) * 64 + gbase + (c % G)];
-  }
-  Cand c;
-  c.word = q[0].x; c.morph = q[0].y; c.tag = q[0].z; c.mask = q[0].w;
-  c.pre = dbl(q[1].x, q[1].y); c.f4 = dbl(q[1].z, q[1].w);
-  c.f5 = dbl(q[2].x, q[2].y); c.f6 = dbl(q[2].z, q[2].w);
-  return c;
-}
 
 // Hypothesis fields the scorer needs (from the LDS frontier).
 struct Hyp {
@@ -866,23 +859,20 @@ constexpr int P_WPB = PK_WPB;           // waves per block
 // (k=1 lane-schedule entries: K1_* in lt_internal.h)
 
 // Stage the records of the wave's packed candidates (lane l's node gn, INV =
-// none) into wave_planes: the 3 x 64 chunks of 16 B form one stream in lane
-// order, and DMA instruction pl has lane t fetch chunk 64*pl + t -- the part
-// (c mod 3) of lane (c / 3)'s record -- so consecutive lanes read consecutive
-// bytes of a sentence's node block.  Lane l's record ends up at chunks
-// 3l .. 3l+2.
+// none) into wave_planes: the 2 x 64 chunks of 16 B form one stream in lane
+// order, and DMA instruction pl has lane t fetch chunk 64*pl + t -- part
+// (c mod 2) of lane (c / 2)'s record -- so consecutive lanes read consecutive
+// bytes of a sentence's node block.  Lane l's record ends up at chunks 2l,
+// 2l+1.
 __device__ __forceinline__ void dma_packed(const Bufs& B, uint32_t gn, uint4* wave_planes, int lane) {
-  uint32_t nj[3], part[3];
+  static_assert(REC_CHUNKS == 2, "two 16 B chunks per record");
+  uint32_t nj[2];
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {               // all three permutes first: one LDS round trip
-    const uint32_t c = (uint32_t)(64 * pl + lane);
-    const uint32_t j = (c * 171u) >> 9;           // c / 3 for c < 192
-    part[pl] = c - 3u * j;
-    nj[pl] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)gn);
-  }
+  for (int pl = 0; pl < 2; ++pl)                 // both permutes first: one LDS round trip
+    nj[pl] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((uint32_t)(64 * pl + lane) >> 1) << 2), (int)gn);
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {
-    const uint32_t o = nj[pl] != INV ? nj[pl] * (uint32_t)sizeof(NodeRec) + part[pl] * 16u : OOB;
+  for (int pl = 0; pl < 2; ++pl) {
+    const uint32_t o = nj[pl] != INV ? nj[pl] * (uint32_t)sizeof(NodeRec) + (uint32_t)(lane & 1) * 16u : OOB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wave_planes + pl * 64), 16, o, 0, 0, PK_DMA_AUX);
   }
 }
@@ -1029,20 +1019,22 @@ lt_viterbi_pk(DecodeParams p) {
   constexpr int BPL = PK_BPL;                   // end positions whose backpointer stays in LDS
   __shared__ VEntry ring[P_WPB][W][RING];
   __shared__ uint32_t bpl[P_WPB][W][BPL];
-  __shared__ uint4 stg[P_WPB][3 * 64];
+  __shared__ uint4 stg[P_WPB][REC_CHUNKS * 64];
   __shared__ SentRec srec[P_WPB][W];
   __shared__ unsigned long long amax[P_WPB][2][W];
   __shared__ uint32_t amin[P_WPB][2][W];
   __shared__ double d3l[D3_DIM * D3_DIM];
-  __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
+  __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records (as staged ones)
+  __shared__ F46 pxl[MAX_PAIRS];                // the batch's class-4/6 pair table
   // the occupancy the launch bounds ask for must fit a CU's 160 KiB of LDS
   // (4 SIMDs x PK_WAVES waves in blocks of P_WPB waves); the LDS window PK_BPL
   // is sized to the last byte of it
   static_assert(!(NARROW && W <= 8) ||
                     (sizeof(ring) + sizeof(bpl) + sizeof(stg) + sizeof(srec) + sizeof(amax) + sizeof(amin) +
-                     sizeof(d3l) + sizeof(ucan)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
+                     sizeof(d3l) + sizeof(ucan) + sizeof(pxl)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
                 "lt_viterbi_pk LDS exceeds the CU's share for PK_WAVES waves per SIMD");
-  stage_unk(p, ucan);
+  for (int i = (int)threadIdx.x; i < p.n_pairs; i += 64 * P_WPB) pxl[i] = p.pairs[i];
+  stage_unk(p, ucan);                           // (its barrier publishes pxl too)
   const Aux aux = stage_aux<NARROW>(p, d3l);
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1111,7 +1103,7 @@ lt_viterbi_pk(DecodeParams p) {
     const bool act = gn0 != INV || imp;
     const int msr = act ? (int)((ent >> 26) & 7u) : 0;
     // this lane's candidate: its staged record, or the implicit Unknown's
-    const Cand cur = cand_lds(imp ? ucan + 3u * (ent & 7u) : wst + 3 * lane);
+    const Cand cur = cand_lds32(imp ? ucan + 2u * (ent & 7u) : wst + 2 * lane, 1, pxl, B, imp ? INV : gn0);
     const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
     int bm0 = em9 - d0;
     bm0 += bm0 < 0 ? RING : 0;
@@ -1338,10 +1330,10 @@ lt_beam_pk(DecodeParams p) {
   constexpr int LN = KTP + CH;                  // ranked list: running top-k + chunk
   static_assert(KTP % 4 == 0, "list alignment");
   constexpr int STAGE = PK_STAGE;               // candidate records staged per position
-  constexpr int PL = (3 * STAGE + 63) / 64;     // 16 B staging loads per lane
+  constexpr int PL = (REC_CHUNKS * STAGE + 63) / 64;   // 16 B staging loads per lane
   __shared__ VEntry ring[WPB][RING][KT];
   __shared__ int32_t cntl[WPB][RING];
-  __shared__ uint4 stg[WPB][3 * STAGE];         // records of the current position
+  __shared__ uint4 stg[WPB][REC_CHUNKS * STAGE];   // records of the current position
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][LN];
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][LN];
   __shared__ unsigned long long tkey[WPB][KT];
@@ -1352,7 +1344,7 @@ lt_beam_pk(DecodeParams p) {
   // expansion index (a lane-variable index into wave-uniform values)
   __shared__ __attribute__((aligned(16))) int sstp[WPB][PK_SPRE ? 12 : 1];
   __shared__ __attribute__((aligned(16))) int sprep[WPB][PK_SPRE ? 12 : 1];
-  __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
+  __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records
   // probe dedup (BM_DEDUP): each beam entry's lead rank, the classes 0-3 cache
   constexpr bool DEDUP = BM_DEDUP && KT <= 16;
   __shared__ uint8_t lead9[WPB][DEDUP ? RING : 1][DEDUP ? KT : 1];
@@ -1403,7 +1395,7 @@ lt_beam_pk(DecodeParams p) {
     const uint32_t base = (nbase + (uint32_t)first) * (uint32_t)sizeof(NodeRec);
 #pragma unroll
     for (int pl = 0; pl < PL; ++pl)
-      pf[pl] = ld128(B.node, valid && pl * 64 + lane < 3 * STAGE ? base + (uint32_t)(pl * 64 + lane) * 16u : OOB);
+      pf[pl] = ld128(B.node, valid && pl * 64 + lane < REC_CHUNKS * STAGE ? base + (uint32_t)(pl * 64 + lane) * 16u : OOB);
     pfs = (valid && lane <= MAX_SPAN) ? ssp[(e1 - 1) * MAX_SPAN + lane] : 0;
   };
   int ss[MAX_SPAN + 1];
@@ -1421,7 +1413,7 @@ lt_beam_pk(DecodeParams p) {
     uint4* const cst = stg[wv];
 #pragma unroll
     for (int pl = 0; pl < PL; ++pl)
-      if (pl * 64 + lane < 3 * STAGE) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
+      if (pl * 64 + lane < REC_CHUNKS * STAGE) cst[pl * 64 + lane] = make_uint4(pf[pl].x, pf[pl].y, pf[pl].z, pf[pl].w);
 #pragma unroll
     for (int j = 0; j <= MAX_SPAN; ++j) ss[j] = __builtin_amdgcn_readlane(pfs, j);
     __builtin_amdgcn_wave_barrier();
@@ -1505,7 +1497,7 @@ lt_beam_pk(DecodeParams p) {
         if (!act) {
           c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
         } else if (imp || so < STAGE) {
-          c = imp ? cand_lds(ucan + 3 * (d - 1)) : read_block<64>(cst, 0, so);
+          c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + 2 * so, 1, B.pairs, B, imp ? INV : nbase + (uint32_t)node);
         } else {
           c = load_cand(B, nbase + (uint32_t)node);
         }
@@ -1702,7 +1694,8 @@ lt_beam_pk(DecodeParams p) {
       bpv = bp_pack(wnode, (uint32_t)wd, (uint32_t)wr);
     };
     auto near = [&]() {                          // staged record or implicit Unknown
-      return cand_lds(wimp ? ucan + 3 * (wd - 1) : cst + 3 * min((int)wnode - A0, STAGE - 1));
+      const int so = min((int)wnode - A0, STAGE - 1);
+      return cand_lds32(wimp ? ucan + 2 * (wd - 1) : cst + 2 * so, 1, B.pairs, B, wimp ? INV : nbase + wnode);
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
       if (writer) build(near());
@@ -1799,12 +1792,12 @@ lt_beam_hw(DecodeParams p) {
   // records staged per group and position (the rest take a global load): a
   // position's dictionary candidates, 2.5 on average in the bench lattices
   constexpr int STAGE = HW_STAGE / S;
-  constexpr int CPG = 3 * STAGE;                // staged 16 B chunks per group
+  constexpr int CPG = REC_CHUNKS * STAGE;       // staged 16 B chunks per group
   constexpr int PL = (S * CPG + 63) / 64;       // 16 B staging loads per lane
   static_assert(KT <= G && G >= MAX_SPAN + 1, "one writer lane per rank in a group; span starts fit a group");
   __shared__ VEntry ring[WPB][S][RING][KT];
   __shared__ int32_t cntl[WPB][S][RING];
-  __shared__ uint4 stg[WPB][S * CPG];           // group h's record r: chunks CPG h + 3r .. +2
+  __shared__ uint4 stg[WPB][S * CPG];           // group h's record r: chunks CPG h + 2r, +1
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][S][LN];
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][S][LN];
   __shared__ unsigned long long tkey[WPB][S][KT];
@@ -1813,7 +1806,7 @@ lt_beam_hw(DecodeParams p) {
   __shared__ __attribute__((aligned(16))) int spre[WPB][S][HW_SPRE ? 12 : 1];   // and expansion prefixes
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
-  __shared__ uint4 ucan[3 * MAX_SPAN];          // the implicit Unknowns' records
+  __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records
   // probe dedup (BM_DEDUP, lt_beam_pk): lead ranks, and per group a cache of
   // 2G entries (a dup within G expansions of its lead reads it after its
   // round's writes) holding classes 0-3 as the first four terms of the
@@ -2019,7 +2012,8 @@ lt_beam_hw(DecodeParams p) {
         if (!act) {
           c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
         } else if (imp || so < STAGE) {
-          c = cand_lds(imp ? ucan + 3 * (d - 1) : cst + CPG * hf + 3 * so);
+          c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + CPG * hf + 2 * so, 1, B.pairs, B,
+                         imp ? INV : nbase + (uint32_t)node);
         } else {
           c = load_cand(B, nbase + (uint32_t)node);
         }
@@ -2163,7 +2157,9 @@ lt_beam_hw(DecodeParams p) {
       bpv = bp_pack(wnode, (uint32_t)wd, (uint32_t)wr);
     };
     auto near = [&]() {                          // staged record or implicit Unknown
-      return cand_lds(wimp ? ucan + 3 * (wd - 1) : cst + CPG * hf + 3 * min((int)wnode - A0, STAGE - 1));
+      const int so = min((int)wnode - A0, STAGE - 1);
+      return cand_lds32(wimp ? ucan + 2 * (wd - 1) : cst + CPG * hf + 2 * so, 1, B.pairs, B,
+                        wimp ? INV : nbase + wnode);
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
       if (writer) build(near());
@@ -2258,6 +2254,8 @@ __global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
   Bufs B;
   B.node = make_rsrc(p.words, (uint64_t)p.n_words * sizeof(NodeRec));
   B.tab = make_rsrc(p.table, (uint64_t)p.slots * (NARROW ? sizeof(SlotN) : sizeof(SlotW)));
+  B.pairs = p.pairs;
+  B.esc = make_rsrc(p.esc, p.esc ? (uint64_t)p.n_words * sizeof(F46) : 0u);
   const Cand c = load_cand(B, (uint32_t)w);
   const Cand cj = load_cand(B, (uint32_t)j);
   const int64_t i = p.prev2[w];

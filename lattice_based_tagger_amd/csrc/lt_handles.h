@@ -60,6 +60,7 @@ struct lt_piece {
   int64_t sched_steps = 0;
   int64_t* d_edge_base = nullptr;                // [n_nodes], rebased to the piece
   double* d_edge_val = nullptr;                  // [n_edge][n_edges]
+  lt::F46* d_esc = nullptr;                      // [n_nodes] class-4/6 pairs of PX_ESC nodes (or none)
 };
 
 struct lt_batch {
@@ -75,6 +76,9 @@ struct lt_batch {
   int32_t n_unk = 0;
   lt::NodeRec* d_unk = nullptr;
   double* d_unk_post = nullptr;
+  // the class-4/6 pair table of the records (NodeRec, PX_SHIFT): [n_pairs]
+  int32_t n_pairs = 0;
+  lt::F46* d_pairs = nullptr;
   // device preparation (the k=1 lane schedules of the pieces): has_sched = the
   // batch has them (max_len <= 8); prep_done = the fill kernels are queued
   bool has_sched = false, prep_done = false;

@@ -29,6 +29,9 @@ struct DecodeParams {
   const int64_t* span_off;
   const int32_t* span_start;
   const NodeRec* nodes;         // AoS node records; mask + span length bits (D_SHIFT)
+  const F46* pairs;             // the batch's class-4/6 pair table (NodeRec, PX_SHIFT)
+  int32_t n_pairs;
+  const F46* esc;               // [n_nodes] pairs of PX_ESC nodes (nullptr: none)
   const double* npost;
   // implicit Unknown candidates (lattice_decode.h n_unk): an in-range span with
   // no node holds one, whose record is unk[d-1] (d = span length) and whose
@@ -78,6 +81,8 @@ struct EvalParams {
   int32_t n_paths;
   int64_t n_words;
   const NodeRec* words;         // AoS word records
+  const F46* pairs;             // their class-4/6 pair table (NodeRec, PX_SHIFT)
+  const F46* esc;               // [n_words] pairs of PX_ESC words (nullptr: none)
   const int64_t* prev1;
   const int64_t* prev2;
   const int64_t* path_off;

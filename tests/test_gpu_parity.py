@@ -132,6 +132,28 @@ def test_config3_full_batch_matches_c_oracle(gpu_decoder, config3_batch, k):
     assert (ex, tu) == (o_ex, o_tu)
 
 
+@pytest.mark.parametrize('k', [1, 2, 5, 16, 300])
+def test_class46_pair_escape_matches_c_oracle(gpu_decoder, k):
+    """The node records hold their class-4/6 coefficients as an index into the
+    batch's pair table (at most 126 distinct pairs, lt_common.h NodeRec); a
+    batch with more sends the rest to the per-node escape array.  Here every
+    node gets its own class-4 coefficient (and the implicit Unknowns keep
+    theirs): the table fills, most nodes escape, and every kernel (k=1, the
+    lane-group and one-wave beams, the general kernel at 300) still decodes
+    byte-equal to the C restatement."""
+    packed, keys, coefs = _synthetic(1024 if k <= 16 else 64, seed=4600 + k, n_features=200_000)
+    rng = np.random.default_rng(k)
+    packed.node_f4 = rng.standard_normal(len(packed.node_f4))
+    packed.node_mask = (np.asarray(packed.node_mask, dtype=np.uint32) | np.uint32(1 << 18)).astype(np.uint32)
+    (count, length, score, codes), (ex, tu, _, _) = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
+    o_count, o_len, o_score, o_codes, o_ex, o_tu = lt_oracle.decode(packed, keys, coefs, k, nthreads=16)
+    assert np.array_equal(count, o_count)
+    assert np.array_equal(length, o_len)
+    assert np.array_equal(score.view(np.uint64), o_score.view(np.uint64))
+    assert np.array_equal(codes, o_codes)
+    assert (ex, tu) == (o_ex, o_tu)
+
+
 def test_long_sentences_cross_the_lds_backpointer_window(gpu_decoder):
     """k=1 keeps the backpointers of end positions < PK_BPL (87) in LDS and
     the rest in HBM: 40-eojeol sentences (about 140 characters) put most
