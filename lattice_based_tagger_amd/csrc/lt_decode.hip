@@ -1817,6 +1817,9 @@ lt_beam_hw(DecodeParams p) {
   constexpr int DQ = 2 * G;
   __shared__ uint8_t lead9[WPB][S][DEDUP ? RING : 1][DEDUP ? KT : 1];
   __shared__ double dds[WPB][S][DEDUP ? DQ : 1];
+  // the batch's class-4/6 pair table (read per expansion: LDS, not the caches)
+  __shared__ F46 pxl[MAX_PAIRS];
+  for (int i = (int)threadIdx.x; i < p.n_pairs; i += (int)blockDim.x) pxl[i] = p.pairs[i];
   stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
@@ -2012,7 +2015,7 @@ lt_beam_hw(DecodeParams p) {
         if (!act) {
           c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
         } else if (imp || so < STAGE) {
-          c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + CPG * hf + 2 * so, 1, B.pairs, B,
+          c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + CPG * hf + 2 * so, 1, pxl, B,
                          imp ? INV : nbase + (uint32_t)node);
         } else {
           c = load_cand(B, nbase + (uint32_t)node);
@@ -2158,7 +2161,7 @@ lt_beam_hw(DecodeParams p) {
     };
     auto near = [&]() {                          // staged record or implicit Unknown
       const int so = min((int)wnode - A0, STAGE - 1);
-      return cand_lds32(wimp ? ucan + 2 * (wd - 1) : cst + CPG * hf + 2 * so, 1, B.pairs, B,
+      return cand_lds32(wimp ? ucan + 2 * (wd - 1) : cst + CPG * hf + 2 * so, 1, pxl, B,
                         wimp ? INV : nbase + wnode);
     };
     if (__builtin_amdgcn_ballot_w64(far) == 0ull) {
