@@ -299,7 +299,8 @@ lt_status lt_decode(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k, 
  * feature tuples generated by trigram_encoder (feature.py:76-121); and the
  * kernel's own work: feature probes past the node pre-filter (LDS + table)
  * and the table slot loads they issued (primary, plus secondary at flagged
- * slots).  Any output pointer may be NULL. */
+ * slots).  Every kernel has a counting variant, the general one included.
+ * Any output pointer may be NULL. */
 lt_status lt_count_ops(lt_ctx* ctx, const lt_model* model, lt_batch* batch, int k,
                        int64_t* expansions, int64_t* feature_tuples, int64_t* probes,
                        int64_t* table_loads);

@@ -1429,7 +1429,7 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
     hipEvent_t e0 = q == 0 ? c->kev0[r] : nullptr, e1 = q + 1 == P ? c->kev1[r] : nullptr;
     if (wide) {
       p.wide_threads = std::max(1, std::min(wide_threads, p.n_sent));
-      HIP_TRY(launch_wide(p, c->stream, e0, e1));
+      HIP_TRY(launch_wide(p, c->stream, false, e0, e1));
     } else {
       HIP_TRY(launch_decode(p, c->stream, false, e0, e1));
     }
@@ -1767,16 +1767,15 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
-  if (decode_is_wide(b->max_len, k))
-    return fail(LT_EUNSUPPORTED, "lt_count_ops: not collected by the general kernel (max_len > %d or beam > %d)",
-                MAX_SPAN, LT_MAX_BEAM_COMPILED);
+  const bool wide = decode_is_wide(b->max_len, k);
   HIP_TRY(hipSetDevice(c->device));
-  if (beam_template_for(k) == 1) HIP_TRY(prep_fill(b, c->stream));
+  if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
+  if (!wide && beam_template_for(k) == 1) HIP_TRY(prep_fill(b, c->stream));
   if ((st = next_slot(c, b)) != LT_OK) return st;
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
 #ifdef PK_PHASES
   // diagnostic build: the shipping (non-counting) kernel, its phase stamps
-  for (size_t q = 0; q < b->pieces.size(); ++q) {
+  for (size_t q = 0; q < (wide ? 0 : b->pieces.size()); ++q) {
     piece_params(b, q, k, p);
     HIP_TRY(launch_decode(p, c->stream, false));
   }
@@ -1790,9 +1789,15 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   }
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
 #endif
+  const int32_t wide_threads = p.wide_threads;
   for (size_t q = 0; q < b->pieces.size(); ++q) {
     piece_params(b, q, k, p);
-    HIP_TRY(launch_decode(p, c->stream, true));
+    if (wide) {
+      p.wide_threads = std::max(1, std::min(wide_threads, p.n_sent));
+      HIP_TRY(launch_wide(p, c->stream, true));
+    } else {
+      HIP_TRY(launch_decode(p, c->stream, true));
+    }
   }
   b->launch_serial = c->n_serial++;
   b->last_end = nullptr;             // complete below

@@ -761,32 +761,6 @@ __device__ __forceinline__ double bm_score(const BMProbe<NARROW>& P, const VEntr
   return v1_sum(cf, pres, c, h);
 }
 
-// ---------------------------------------------------------------------------
-// Probe dedup (beam kernels).  Hypotheses of one beam[b] often end in the same
-// word: at k = 5 two thirds of the expansions repeat an earlier hypothesis'
-// last word, at k = 16 nearly nine in ten.  Feature classes 0-3
-// (feature.py:95-103: (wj.word, wk.word, tk), (wj.word, tk), (tj, wk.word,
-// tk), (tj, tk)) and their pre-filter bits depend on the candidate and on wj's
-// word and tag only, so two expansions of one candidate from hypotheses whose
-// last words agree in (word, tag) find the same coefficients.  The first such
-// hypothesis of a beam (its "lead", computed when the beam is written) probes
-// them; an expansion from a later one (a "dup", within DD_WIN expansions of
-// its lead's) takes them from a small LDS cache keyed by expansion index and
-// probes only classes 7 and 8, which read wi / the morphs.  The sum is then
-// the same numpy-order sum over the same values (H7), so results are
-// bit-identical.
-// ---------------------------------------------------------------------------
-#ifndef BM_DEDUP
-#define BM_DEDUP 0          // measured slower (round 4: k=5 4.96 vs 4.25 ms, k=16 17.0 vs 11.6 ms)
-#endif
-// The cache holds DD_Q entries, entry g mod DD_Q; a dup is within DD_WIN =
-// DD_Q expansions of its lead, so no expansion between them rewrites the
-// lead's entry.  A round writes its (up to 64) consecutive entries at once,
-// which can rewrite the entry of a lead of an earlier round that a dup of
-// this round needs: such dups read before the round's writes, dups of a lead
-// in the same round after them.
-constexpr int DD_Q = 64;
-constexpr int DD_WIN = DD_Q;
 
 // Sequence.add into a ring entry (beam.py:112-116): wi = wj, wj = wk
 template <bool COUNT>
@@ -933,13 +907,19 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
 #pragma unroll
   for (int w = 0; w < W; ++w) nmax = max(nmax, __builtin_amdgcn_readlane(nw, w));
   int64_t step = 0;
-  uint32_t* const out = sched + wave_off[wave] * 64 + lane;
+  // the wave's schedule rows as a buffer: row offset in the scalar offset,
+  // the lane's 4 B in a loop-invariant address register
+  const int64_t w0 = wave_off[wave];
+  const rsrc_t out = make_rsrc(sched + w0 * 64, (uint64_t)(wave_off[wave + 1] - w0) * 256u);
   for (int e = 1; e <= nmax; ++e) {
     if ((e - 1) % SCH_CHUNK == 0) {
       // the span starts of end positions [e, e + SCH_CHUNK) of every sentence,
       // loaded by all lanes at once (one memory round trip per chunk instead
       // of one per position)
       __builtin_amdgcn_wave_barrier();
+      // every sentence's loads issued before the first wait (one round trip)
+      constexpr int TPL = (SPN + 63) / 64;
+      int v[W][TPL];
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         const int n_w = __builtin_amdgcn_readlane(nw, w);
@@ -947,15 +927,24 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
                            (uint32_t)__builtin_amdgcn_readlane((int)soff, w);
         const int lim = min(SPN, (n_w - e + 1) * MAX_SPAN + 1);      // entries up to 8 n_w
         const int32_t* const src = p.span_start + so + (int64_t)(e - 1) * MAX_SPAN;
-        int v[(SPN + 63) / 64];
 #pragma unroll
-        for (int t = 0; t < (SPN + 63) / 64; ++t) v[t] = lane + 64 * t < lim ? src[lane + 64 * t] : 0;
-#pragma unroll
-        for (int t = 0; t < (SPN + 63) / 64; ++t)
-          if (lane + 64 * t < SPN) spl[w][lane + 64 * t] = v[t];
+        for (int t = 0; t < TPL; ++t) v[w][t] = lane + 64 * t < lim ? src[lane + 64 * t] : 0;
       }
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+#pragma unroll
+        for (int t = 0; t < TPL; ++t)
+          if (lane + 64 * t < SPN) spl[w][lane + 64 * t] = v[w][t];
+      // (a one-wave workgroup: its LDS operations complete in issue order, so
+      // a compiler barrier orders the writes before the reads below; a
+      // workgroup fence would also wait for every schedule store in flight.
+      // The explicit vmcnt(0) here, once per chunk, retires the chunk's
+      // exec-masked loads: without it their registers stay "maybe pending" to
+      // the compiler at every later position, whose writes to them then wait
+      // for vmcnt(0) -- the schedule stores in flight included)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      asm volatile("" ::: "memory");
     }
     // the owner lane of each sentence: its slots' candidates and first nodes
     int X = 0;
@@ -977,7 +966,7 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
       X = run;
     }
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("" ::: "memory");
     int st[W], run = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -1006,7 +995,8 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
                        : (uint32_t)(a + (ix - spre[w][j]));
         ent |= (uint32_t)w << 26;
       }
-      out[(step + r) * 64] = r == 0 ? (ent | K1_FIRST) : ent;
+      __builtin_amdgcn_raw_buffer_store_b32(r == 0 ? (ent | K1_FIRST) : ent, out, (uint32_t)lane * 4u,
+                                            (int)((step + r) * 256), 0);
     }
     step += rounds;
     __builtin_amdgcn_wave_barrier();             // the LDS tables are rewritten at the next position
@@ -1312,13 +1302,15 @@ __device__ __forceinline__ void rank_into(const unsigned long long* LK, int q0, 
 #ifndef PK_STAGE
 #define PK_STAGE 32
 #endif
-// occupancy floor of lt_beam_pk per beam template (the probe dedup's registers
-// would otherwise drop k = 9..16 to 3 waves per SIMD)
+// occupancy floor of lt_beam_pk per beam template: 4 waves per SIMD for the
+// narrow-key k = 9..16 kernel (it fits 128 VGPRs without spilling); the
+// wide-key (32 B slot) kernels need more registers than that floor leaves --
+// under it they spilled 53 (decode) and 101 (COUNT) VGPRs -- and take none
 #ifndef PK_WPE
-#define PK_WPE(kt) ((kt) == 16 ? 4 : 1)
+#define PK_WPE(kt, narrow) ((kt) == 16 && (narrow) ? 4 : 1)
 #endif
 template <int KT, int WPB, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PK_WPE(KT), 8)))
+__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PK_WPE(KT, NARROW), 8)))
 lt_beam_pk(DecodeParams p) {
   constexpr int RPC = KT <= 16 ? 2 : 4;         // scoring rounds per chunk
   // beams above 64 (KT = 128, 256): more than one entry per lane in the
@@ -1345,11 +1337,6 @@ lt_beam_pk(DecodeParams p) {
   __shared__ __attribute__((aligned(16))) int sstp[WPB][PK_SPRE ? 12 : 1];
   __shared__ __attribute__((aligned(16))) int sprep[WPB][PK_SPRE ? 12 : 1];
   __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records
-  // probe dedup (BM_DEDUP): each beam entry's lead rank, the classes 0-3 cache
-  constexpr bool DEDUP = BM_DEDUP && KT <= 16;
-  __shared__ uint8_t lead9[WPB][DEDUP ? RING : 1][DEDUP ? KT : 1];
-  __shared__ double ddc[WPB][DEDUP ? DD_Q : 1][4];
-  __shared__ uint8_t ddp[WPB][DEDUP ? DD_Q : 1];
   stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
   if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
@@ -1381,7 +1368,6 @@ lt_beam_pk(DecodeParams p) {
   if (lane == 0) {                              // beam[0] = [BOS] (beam.py:21-23)
     R[0][0] = v_bos(load_cand(B, nbase));
     cnt9[0] = 1;
-    if (DEDUP) lead9[wv][0][0] = 0;
   }
   // The next position's first 64 records (lane t holds 16 B chunks t,
   // 64 + t, 128 + t of the block: consecutive lanes read consecutive bytes)
@@ -1506,45 +1492,14 @@ lt_beam_pk(DecodeParams p) {
         const VEntry h0 = R[hb][hr];
         // skip successive unknown words (beam.py:43-45): num_unk > 0 <=> wj is Unk
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));
-        // a dup (BM_DEDUP): its lead's expansion of the same candidate is gl
-        const int ldr = DEDUP ? (int)lead9[wv][hb][hr] : hr;
-        const int gdist = (hr - ldr) * m;
-        const bool dup = DEDUP && !skip && has_tri && ldr != hr && gdist < DD_WIN;
         BMProbe<NARROW> P;
         const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
-        bm_issue<NARROW>(P, B, slots, seed, h0, c, dup ? (need & 0x30u) : need, aux);
+        bm_issue<NARROW>(P, B, slots, seed, h0, c, need, aux);
         asm volatile("" ::: "memory");
         const VEntry h1 = R[hb][hr];
         double cf[6];
         uint32_t pres = 0;
         if (has_tri) bm_classes<NARROW>(P, h1, c, cf, pres);
-        if (DEDUP && has_tri) {
-          // leads (every lane that probed classes 0-3) publish them; dups read
-          // their lead's: one of an earlier round before this round's writes,
-          // one of this round after them
-          const int gl = g - gdist;
-          const int ql = gl & (DD_Q - 1);
-          const bool early = gl < base + 64 * t;
-          if (dup && early) {
-#pragma unroll
-            for (int x = 0; x < 4; ++x) cf[x] = ddc[wv][ql][x];
-            pres = (pres & ~0xFu) | ddp[wv][ql];
-          }
-          __builtin_amdgcn_wave_barrier();
-          if (!skip && !dup) {
-            const int q = g & (DD_Q - 1);
-#pragma unroll
-            for (int x = 0; x < 4; ++x) ddc[wv][q][x] = cf[x];
-            ddp[wv][q] = (uint8_t)(pres & 0xFu);
-          }
-          __builtin_amdgcn_wave_barrier();
-          if (dup && !early) {
-#pragma unroll
-            for (int x = 0; x < 4; ++x) cf[x] = ddc[wv][ql][x];
-            pres = (pres & ~0xFu) | ddp[wv][ql];
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
         if (!skip) {
           const double tri = has_tri ? v1_sum(cf, pres, c, h1) : 0.0;
           if (COUNT) v_count(cnt, h1, c, need, 2 * __builtin_popcount(P.gneed));
@@ -1705,19 +1660,6 @@ lt_beam_pk(DecodeParams p) {
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][wl] = ne;
     __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + wl) * 4u : OOB, 0, 0);
-    if (DEDUP) {
-      // each entry's lead: the first rank of beam[e] whose last word has the
-      // same (word, tag) -- the same classes 0-3 for every candidate
-      __builtin_amdgcn_wave_barrier();
-      if (writer) {
-        int ld = wl;
-        for (int q = wl - 1; q >= 0; --q) {
-          const uint2 jw = *reinterpret_cast<const uint2*>(&R[em9][q].jword);
-          ld = (jw.x == ne.jword && jw.y == ne.jtag) ? q : ld;
-        }
-        lead9[wv][em9][wl] = (uint8_t)ld;
-      }
-    }
     }
     if (lane == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
@@ -1807,16 +1749,6 @@ lt_beam_hw(DecodeParams p) {
   constexpr bool USE_D3 = KT <= 4;
   __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records
-  // probe dedup (BM_DEDUP, lt_beam_pk): lead ranks, and per group a cache of
-  // 2G entries (a dup within G expansions of its lead reads it after its
-  // round's writes) holding classes 0-3 as the first four terms of the
-  // numpy-order sum, s4 = (((0 + c0) + c1) + c2) + c3: registers are what this
-  // kernel is short of, so a dup is one whose sum is sure to stay left to
-  // right (at most 7 features present) and takes s4 as it is
-  constexpr bool DEDUP = BM_DEDUP && G == 32;
-  constexpr int DQ = 2 * G;
-  __shared__ uint8_t lead9[WPB][S][DEDUP ? RING : 1][DEDUP ? KT : 1];
-  __shared__ double dds[WPB][S][DEDUP ? DQ : 1];
   // the batch's class-4/6 pair table (read per expansion: LDS, not the caches)
   __shared__ F46 pxl[MAX_PAIRS];
   for (int i = (int)threadIdx.x; i < p.n_pairs; i += (int)blockDim.x) pxl[i] = p.pairs[i];
@@ -1869,7 +1801,6 @@ lt_beam_hw(DecodeParams p) {
   if (hv && hl == 0) {                          // beam[0] = [BOS] (beam.py:21-23)
     R[0][0] = v_bos(load_cand(B, nbase));
     cnt9[0] = 1;
-    if (DEDUP) lead9[wv][hf][0][0] = 0;
   }
   if (HW_SPRE && hl == 0) spre[wv][hf][0] = 0;
   // next position's first STAGE records of every group (chunk c = 64 pl +
@@ -2024,44 +1955,12 @@ lt_beam_hw(DecodeParams p) {
         const int hr = act ? r : 0;
         const VEntry h0 = R[hb][hr];
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
-        // a dup (BM_DEDUP, lt_beam_pk): its lead's expansion of this candidate is g - gdist
-        const int ldr = DEDUP ? (int)lead9[wv][hf][hb][hr] : hr;
-        const int gdist = (hr - ldr) * m;
         const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
-        // ... and at most 7 features can be present (classes 0-3, and of
-        // f4 / f5 / f6 / class 7 / class 8 at most three): numpy's sum is then
-        // left to right (H7), which s4 starts
-        const uint32_t xb = ((c.mask >> 18) & 1u) + ((c.mask >> 19) & 1u) + ((h0.meta >> 20) & 1u) +
-                            ((need >> 4) & 1u) + ((need >> 5) & 1u);
-        const bool dup = DEDUP && !skip && has_tri && ldr != hr && gdist < G && xb <= 3u;
         BMProbe<NARROW> P;
-        bm_issue<NARROW, true>(P, B, slots, seed, h0, c, dup ? (need & 0x30u) : need, aux);
+        bm_issue<NARROW, true>(P, B, slots, seed, h0, c, need, aux);
         asm volatile("" ::: "memory");
         const VEntry h1 = R[hb][hr];
-        // the trigram term: a lead's (or a lane without dedup) from all its
-        // classes; a dup's in v1_sum's left-to-right order continued from its
-        // lead's s4 with its own classes 7 and 8
-        double tri = 0.0, c78[2] = {-0.0, -0.0};
-        if (has_tri) {
-          double cf[6];
-          uint32_t pres;
-          bm_classes<NARROW>(P, h1, c, cf, pres);
-          c78[0] = cf[4];
-          c78[1] = cf[5];
-          if (!dup) tri = v1_sum(cf, pres, c, h1);
-          if (DEDUP && !skip && !dup) {
-            const int q = g & (DQ - 1);
-            dds[wv][hf][q] = (((0.0 + cf[0]) + cf[1]) + cf[2]) + cf[3];
-          }
-        }
-        if (DEDUP && has_tri) {
-          __builtin_amdgcn_wave_barrier();
-          if (dup) {
-            const double s4 = dds[wv][hf][(g - gdist) & (DQ - 1)];
-            tri = ((((s4 + c.f4) + c.f5) + h1.f6) + c78[0]) + c78[1];
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
+        const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
         if (!skip) {
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
@@ -2173,18 +2072,6 @@ lt_beam_hw(DecodeParams p) {
     if (writer) R[em9][hl] = ne;
     __builtin_amdgcn_raw_buffer_store_b32(
         bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, 0);
-    if (DEDUP) {
-      // each entry's lead (lt_beam_pk): the first rank with the same (word, tag)
-      __builtin_amdgcn_wave_barrier();
-      if (writer) {
-        int ld = hl;
-        for (int q = hl - 1; q >= 0; --q) {
-          const uint2 jw = *reinterpret_cast<const uint2*>(&R[em9][q].jword);
-          ld = (jw.x == ne.jword && jw.y == ne.jtag) ? q : ld;
-        }
-        lead9[wv][hf][em9][hl] = (uint8_t)ld;
-      }
-    }
     if (live && hl == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
   }
@@ -2574,7 +2461,7 @@ __device__ void wheap_up(WItem* H, int i) {
   H[i] = x;
 }
 
-template <bool NARROW>
+template <bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
   const int tid = (int)(blockIdx.x * 64 + threadIdx.x);
   if (tid >= p.wide_threads) return;
@@ -2620,7 +2507,8 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
             const uint32_t nd = imp ? UNK_LOCAL : (uint32_t)node;
             const Cand c = cand_at(B, p, nbase, nd, d);
             if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;    // beam.py:43-45
-            const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cn, aux) : 0.0;
+            if (COUNT) ++cn.exp;
+            const double tri = p.has_tri ? trigram<NARROW, COUNT>(B, p.slots, p.seed, h, c, cn, aux) : 0.0;
             const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode, imp ? d : 0);   // beam.py:115
             const WItem it{ord_key(sc), g, nd, (uint32_t)d, (uint32_t)r};
             if (hn < k) {
@@ -2682,21 +2570,30 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
       for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;      // padded layout
     }
   }
+  if (COUNT) {                                  // lt_count_ops: one thread's sentences
+    atomicAdd(p.counters + 0, cn.exp);
+    atomicAdd(p.counters + 1, cn.tup);
+    atomicAdd(p.counters + 2, cn.probe);
+    atomicAdd(p.counters + 3, cn.load);
+  }
 }
 }  // namespace
 
 namespace lt {
-hipError_t launch_wide(const DecodeParams& p, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+hipError_t launch_wide(const DecodeParams& p, hipStream_t st, bool count, hipEvent_t e0, hipEvent_t e1) {
   const int blocks = (p.wide_threads + 63) / 64;
   if (p.n_sent == 0 || blocks == 0) {
     hipError_t e = e0 ? hipEventRecord(e0, st) : hipSuccess;
     if (e == hipSuccess && e1) e = hipEventRecord(e1, st);
     return e;
   }
-  if (p.narrow)
-    hipExtLaunchKernelGGL(lt_beam_wide<true>, dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
-  else
-    hipExtLaunchKernelGGL(lt_beam_wide<false>, dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
+  if (p.narrow) {
+    if (count) hipExtLaunchKernelGGL((lt_beam_wide<true, true>), dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
+    else hipExtLaunchKernelGGL((lt_beam_wide<true, false>), dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
+  } else {
+    if (count) hipExtLaunchKernelGGL((lt_beam_wide<false, true>), dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
+    else hipExtLaunchKernelGGL((lt_beam_wide<false, false>), dim3(blocks), dim3(64), 0, st, e0, e1, 0, p);
+  }
   return hipGetLastError();
 }
 }  // namespace lt

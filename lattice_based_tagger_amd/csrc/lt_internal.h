@@ -182,7 +182,8 @@ inline int64_t wide_scratch_bytes(int span_slots, int k) {
   const int64_t heap = ((int64_t)k * WIDE_ITEM_BYTES + 15) & ~(int64_t)15;
   return ring + cnt + heap;
 }
-hipError_t launch_wide(const DecodeParams& p, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t launch_wide(const DecodeParams& p, hipStream_t st, bool count = false, hipEvent_t e0 = nullptr,
+                       hipEvent_t e1 = nullptr);
 int beam_template_for(int k);
 const char* kernel_name_for(int k);
 // e0 / e1 (may be NULL): events recorded at the start / end of the kernel.

@@ -48,9 +48,12 @@ def _device_vs_oracle(dec, packed, model, k):
     db = _capi.DeviceBatch(dec.ctx, packed, max_k=k)
     try:
         count, length, score, codes = db.decode(dm, k)
+        ex, tu, _, _ = db.count_ops(dm, k)           # the general kernel's COUNT variant
     finally:
         db.close()
-    o_count, o_len, o_score, o_codes, _, _ = lt_oracle.decode(packed, model.keys, model.coefs, k, nthreads=16)
+    o_count, o_len, o_score, o_codes, o_ex, o_tu = lt_oracle.decode(packed, model.keys, model.coefs, k,
+                                                                    nthreads=16)
+    assert (ex, tu) == (o_ex, o_tu)                    # reference-algorithm operation counts
     assert np.array_equal(count, o_count)
     assert np.array_equal(length, o_len)
     assert np.array_equal(score.view(np.uint64), o_score.view(np.uint64))    # 0 ULP
