@@ -807,6 +807,11 @@ static void batch_free(lt_batch* b) {
       if (ev) (void)hipEventDestroy(ev);
   if (b->prep_ev0) (void)hipEventDestroy(b->prep_ev0);
   if (b->prep_ev1) (void)hipEventDestroy(b->prep_ev1);
+  if (b->lazy_sched)
+    for (lt_piece& pc : b->pieces) {
+      dfree(pc.d_sched);
+      dfree(pc.d_wave_off);
+    }
   arena_give(b->ctx, b->arena);
   delete b;
 }
@@ -894,6 +899,52 @@ static hipError_t prep_fill(lt_batch* b, hipStream_t st) {
   return e;
 }
 
+// The k=1 lane schedule of a batch created for larger beams, at its first
+// beam-1 decode: each wave's macro-steps counted on the device
+// (lt_k1_sched_count), the offsets summed on the host (one synchronisation),
+// the schedule in buffers of its own; prep_fill then fills it as for a beam-1
+// batch.
+static lt_status lazy_sched(lt_ctx* c, lt_batch* b) {
+  if (b->has_sched || b->max_len > MAX_SPAN) return LT_OK;
+  std::vector<std::vector<int64_t>> offs(b->pieces.size());
+  for (size_t q = 0; q < b->pieces.size(); ++q) {
+    lt_piece& pc = b->pieces[q];
+    if (pc.n_nodes >= (int64_t)K1_NODE)
+      return fail(LT_EUNSUPPORTED, "decode: %lld nodes in one launch piece for the beam-1 schedule",
+                  (long long)pc.n_nodes);
+    const int waves = k1_waves(pc.n_sent);
+    int64_t* d_off = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_off, ((size_t)waves + 1) * 8));
+    pc.d_wave_off = d_off;                     // (freed with the batch from here on)
+    b->lazy_sched = true;
+    DecodeParams p{};
+    piece_params(b, q, 1, p);
+    p.max_len = b->max_len;
+    HIP_TRY(launch_k1_sched_count(p, d_off, c->stream));
+    offs[q].assign((size_t)waves + 1, 0);
+    HIP_TRY(hipMemcpyAsync(offs[q].data(), d_off, (size_t)waves * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (size_t q = 0; q < b->pieces.size(); ++q) {
+    lt_piece& pc = b->pieces[q];
+    std::vector<int64_t>& wo = offs[q];
+    int64_t run = 0;
+    for (size_t w = 0; w + 1 < wo.size(); ++w) {   // exclusive prefix sum
+      const int64_t x = wo[w];
+      wo[w] = run;
+      run += x;
+    }
+    wo.back() = run;
+    pc.sched_steps = run;
+    HIP_TRY(hipMalloc((void**)&pc.d_sched, (size_t)std::max<int64_t>(run, 1) * 64 * 4));
+    HIP_TRY(hipMemcpyAsync(pc.d_wave_off, wo.data(), wo.size() * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));        // (the host offsets go out of scope)
+  b->has_sched = true;
+  b->prep_done = false;
+  return LT_OK;
+}
+
 // LT_TIMING=1: per-phase wall times of lt_batch_create on stderr (diagnostic)
 static bool timing_on() {
   static const bool on = [] {
@@ -977,11 +1028,13 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     pc.bp_entries = bp_off[q][n];
     b->bp_entries += pc.bp_entries;
   }
-  // the k=1 lane schedule of every piece (the tuned kernels' layout, max_len
-  // <= 8): each wave's macro-steps counted here from the span tables (threads
-  // over waves), so that the schedule is part of the arena; its entries are
-  // filled on the device (prep_fill)
-  b->has_sched = d->max_len <= MAX_SPAN;
+  // the k=1 lane schedule of every piece of a beam-1 batch (the tuned
+  // kernels' layout, max_len <= 8): each wave's macro-steps counted here from
+  // the span tables (threads over waves), so that the schedule is part of the
+  // arena; its entries are filled on the device (prep_fill).  A batch created
+  // for larger beams carries none (no host counting, no arena bytes); a k=1
+  // decode of it runs on the lane-group beam kernel (launch_decode)
+  b->has_sched = d->max_len <= MAX_SPAN && max_k == 1;
   b->n_unk = d->n_unk;
   std::vector<std::vector<int64_t>> wave_off(P);
   if (b->has_sched) {
@@ -1347,8 +1400,8 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
   p.nodes = pc.d_nodes;
   p.esc = pc.d_esc;
   p.npost = pc.d_post;
-  p.sched = pc.d_sched;
-  p.wave_off = pc.d_wave_off;
+  p.sched = b->has_sched ? pc.d_sched : nullptr;
+  p.wave_off = b->has_sched ? pc.d_wave_off : nullptr;
   p.n_edges = pc.n_edges;
   p.edge_base = pc.d_edge_base;
   p.edge_val = pc.d_edge_val;
@@ -1418,8 +1471,12 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   const bool wide = decode_is_wide(b->max_len, k);
   if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
   // the k=1 lane schedule, if the batch has not got it yet: queued in front
-  // of the decode on its stream (lt_batch_create builds it for max_k = 1)
-  if (!wide && beam_template_for(k) == 1) HIP_TRY(prep_fill(b, c->stream));
+  // of the decode on its stream (lt_batch_create builds it for max_k = 1; a
+  // batch for larger beams gets it here, at its first beam-1 decode)
+  if (!wide && beam_template_for(k) == 1) {
+    if ((st = lazy_sched(c, b)) != LT_OK) return st;
+    HIP_TRY(prep_fill(b, c->stream));
+  }
   if ((st = next_slot(c, b)) != LT_OK) return st;
   const int r = (int)(c->n_launch % lt_ctx::KRING);
   const size_t P = b->pieces.size();
@@ -1770,7 +1827,10 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   const bool wide = decode_is_wide(b->max_len, k);
   HIP_TRY(hipSetDevice(c->device));
   if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
-  if (!wide && beam_template_for(k) == 1) HIP_TRY(prep_fill(b, c->stream));
+  if (!wide && beam_template_for(k) == 1) {
+    if ((st = lazy_sched(c, b)) != LT_OK) return st;
+    HIP_TRY(prep_fill(b, c->stream));
+  }
   if ((st = next_slot(c, b)) != LT_OK) return st;
   HIP_TRY(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
 #ifdef PK_PHASES

@@ -886,120 +886,169 @@ struct alignas(16) SentRec {
 // the slot's nodes in bindex order, or its implicit Unknown); macro-step r of
 // e covers list entries [64r, 64r + 64).  Entry of lane l: lt_internal.h K1_*.
 // ---------------------------------------------------------------------------
-constexpr int SCH_CHUNK = 32;                   // end positions whose span starts one LDS fill holds
+// One wave per wave schedule, one lane per end position (64 positions per
+// chunk): every lane loads its position's span starts of the W sentences and
+// counts its candidates (run) at once, a wave prefix sum of the macro-steps
+// (max(1, ceil(run / 64))) places each position's rows, and each lane writes
+// its entries in generation order into its row of an LDS tile (64 rows,
+// stride 65 words: conflict-free for a common entry index), copied out by one
+// coalesced 256 B store per row.  A position with more than 64 entries (dense
+// lattices) writes its rows directly.
+constexpr int SCH_ROW = 65;                     // LDS row stride (words)
+// The W sentences of wave schedule `wave` (wave-uniform): lengths, first
+// nodes, span-table offsets, the longest length.
 template <int W>
-__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
-  static_assert(W < 8, "the sentence field holds W - 1");
-  constexpr int SPN = SCH_CHUNK * MAX_SPAN + 1;
-  __shared__ int spre[W][MAX_SPAN + 1];         // sentence w at e: candidate prefix over its span slots
-  __shared__ int sfirst[W][MAX_SPAN + 1];       // and each slot's first piece-global node
-  __shared__ int spl[W][SPN];                   // span starts of SCH_CHUNK end positions per sentence
+__device__ __forceinline__ int k1_wave_sents(const DecodeParams& p, int slot0, int (&nS)[W], uint32_t (&nbS)[W],
+                                             int64_t (&soS)[W]) {
+  int nmax = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const bool v = slot0 + w < p.n_sent;
+    const int sid = v ? p.order[slot0 + w] : 0;
+    nS[w] = v ? p.sent_n[sid] : 0;
+    nbS[w] = v ? (uint32_t)p.node_off[sid] : 0u;
+    soS[w] = v ? p.span_off[sid] : 0;
+    nmax = max(nmax, nS[w]);
+  }
+  return nmax;
+}
+// End position e (pos: e <= the wave's longest sentence) of the W sentences:
+// their span starts, and the number of candidates -- a slot's nodes, or its
+// implicit Unknown when it is empty and in range (beam.py:31-38).
+template <int W>
+__device__ __forceinline__ int k1_position(const DecodeParams& p, int e, bool pos, const int (&nS)[W],
+                                           const int64_t (&soS)[W], int (&ss)[W][MAX_SPAN + 1]) {
+  const int dmax = min(e, p.max_len);
+#pragma unroll
+  for (int w = 0; w < W; ++w) {                 // every sentence's loads before any use
+    const bool live = pos && e <= nS[w];
+    const int32_t* const src = p.span_start + soS[w] + (int64_t)(max(e, 1) - 1) * MAX_SPAN;
+#pragma unroll
+    for (int j = 0; j <= MAX_SPAN; ++j) ss[w][j] = live ? src[j] : 0;
+  }
+  int run = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const bool live = pos && e <= nS[w];
+#pragma unroll
+    for (int j = 0; j < MAX_SPAN; ++j) {
+      const int c = ss[w][j + 1] - ss[w][j];
+      run += (live && c == 0 && MAX_SPAN - j <= dmax) ? 1 : c;
+    }
+  }
+  return run;
+}
+
+// Macro-steps of every wave schedule of a piece (the count lt_batch_create
+// makes on the host), for a batch that gets its schedule at its first beam-1
+// decode: steps[wave] = sum over its end positions of max(1, ceil(run / 64)).
+template <int W>
+__global__ void __launch_bounds__(64) lt_k1_sched_count(DecodeParams p, int64_t* steps) {
   const int wave = blockIdx.x;
   const int lane = (int)threadIdx.x;
   const int slot0 = wave * W;
   if (slot0 >= p.n_sent) return;
-  const bool own = lane < W && slot0 + lane < p.n_sent;
-  const int sid = own ? p.order[slot0 + lane] : 0;
-  const int nw = own ? p.sent_n[sid] : 0;
-  const uint32_t nbase = own ? (uint32_t)p.node_off[sid] : 0u;
-  const int64_t soff = own ? p.span_off[sid] : 0;
-  int nmax = 0;
+  int nS[W];
+  uint32_t nbS[W];
+  int64_t soS[W];
+  const int nmax = k1_wave_sents<W>(p, slot0, nS, nbS, soS);
+  int64_t total = 0;
+  for (int e0 = 1; e0 <= nmax; e0 += 64) {
+    const int e = e0 + lane;
+    const bool pos = e <= nmax;
+    int ss[W][MAX_SPAN + 1];
+    const int run = k1_position<W>(p, e, pos, nS, soS, ss);
+    int rounds = pos ? max(1, (run + 63) >> 6) : 0;
 #pragma unroll
-  for (int w = 0; w < W; ++w) nmax = max(nmax, __builtin_amdgcn_readlane(nw, w));
-  int64_t step = 0;
-  // the wave's schedule rows as a buffer: row offset in the scalar offset,
-  // the lane's 4 B in a loop-invariant address register
+    for (int o = 32; o >= 1; o >>= 1) rounds += __shfl_xor(rounds, o);
+    total += rounds;
+  }
+  if (lane == 0) steps[wave] = total;
+}
+
+// One wave per wave schedule, one lane per end position (64 positions per
+// chunk): every lane loads its position's span starts of the W sentences and
+// counts its candidates (run) at once, a wave prefix sum of the macro-steps
+// (max(1, ceil(run / 64))) places each position's rows, and each lane writes
+// its entries in generation order into its row of an LDS tile (64 rows,
+// stride 65 words: conflict-free for a common entry index), copied out by one
+// coalesced 256 B store per row.  A position with more than 64 entries (dense
+// lattices) writes its further rows directly.
+template <int W>
+__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
+  static_assert(W < 8, "the sentence field holds W - 1");
+  __shared__ uint32_t rows[64 * SCH_ROW];
+  const int wave = blockIdx.x;
+  const int lane = (int)threadIdx.x;
+  const int slot0 = wave * W;
+  if (slot0 >= p.n_sent) return;
+  int nS[W];
+  uint32_t nbS[W];
+  int64_t soS[W];
+  const int nmax = k1_wave_sents<W>(p, slot0, nS, nbS, soS);
+  // the wave's schedule rows as a buffer (stores past its rows are dropped)
   const int64_t w0 = wave_off[wave];
   const rsrc_t out = make_rsrc(sched + w0 * 64, (uint64_t)(wave_off[wave + 1] - w0) * 256u);
-  for (int e = 1; e <= nmax; ++e) {
-    if ((e - 1) % SCH_CHUNK == 0) {
-      // the span starts of end positions [e, e + SCH_CHUNK) of every sentence,
-      // loaded by all lanes at once (one memory round trip per chunk instead
-      // of one per position)
-      __builtin_amdgcn_wave_barrier();
-      // every sentence's loads issued before the first wait (one round trip)
-      constexpr int TPL = (SPN + 63) / 64;
-      int v[W][TPL];
+  uint32_t* const myrow = rows + lane * SCH_ROW;
+  int base = 0;                                 // rows of the chunks before
+  for (int e0 = 1; e0 <= nmax; e0 += 64) {
+    const int e = e0 + lane;
+    const bool pos = e <= nmax;
+    const int dmax = min(e, p.max_len);
+    int ss[W][MAX_SPAN + 1];
+    const int run = k1_position<W>(p, e, pos, nS, soS, ss);
+    const int rounds = pos ? max(1, (run + 63) >> 6) : 0;
+    int incl = rounds;                          // inclusive prefix over the lanes
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const int n_w = __builtin_amdgcn_readlane(nw, w);
-        const int64_t so = ((int64_t)__builtin_amdgcn_readlane((int)(soff >> 32), w) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)soff, w);
-        const int lim = min(SPN, (n_w - e + 1) * MAX_SPAN + 1);      // entries up to 8 n_w
-        const int32_t* const src = p.span_start + so + (int64_t)(e - 1) * MAX_SPAN;
-#pragma unroll
-        for (int t = 0; t < TPL; ++t) v[w][t] = lane + 64 * t < lim ? src[lane + 64 * t] : 0;
-      }
-#pragma unroll
-      for (int w = 0; w < W; ++w)
-#pragma unroll
-        for (int t = 0; t < TPL; ++t)
-          if (lane + 64 * t < SPN) spl[w][lane + 64 * t] = v[w][t];
-      // (a one-wave workgroup: its LDS operations complete in issue order, so
-      // a compiler barrier orders the writes before the reads below; a
-      // workgroup fence would also wait for every schedule store in flight.
-      // The explicit vmcnt(0) here, once per chunk, retires the chunk's
-      // exec-masked loads: without it their registers stay "maybe pending" to
-      // the compiler at every later position, whose writes to them then wait
-      // for vmcnt(0) -- the schedule stores in flight included)
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, (unsigned)o);
+      incl += lane >= o ? t : 0;
     }
-    // the owner lane of each sentence: its slots' candidates and first nodes
-    int X = 0;
-    if (lane < W) {
-      const bool live = own && e <= nw;
-      const int dmax = min(e, p.max_len);
-      const int eb = ((e - 1) % SCH_CHUNK) * MAX_SPAN;
-      int run = 0;
+    const int off = base + incl - rounds;       // the position's first row
+    const int total = __shfl(incl, 63);
+    // entries in generation order (sentence, span slot = begin ascending,
+    // the slot's nodes): the first 64 into the lane's LDS row (row 0 of the
+    // position, K1_FIRST on every entry), the rest (dense lattices) straight
+    // to the position's later rows
+#pragma unroll 4
+    for (int q = 0; q < 64; ++q) myrow[q] = K1_IDLE | K1_FIRST;
+    int q = 0;
 #pragma unroll
-      for (int j = 0; j <= MAX_SPAN; ++j) {
-        const int a = live ? spl[lane][eb + j] : 0;
-        sfirst[lane][j] = (int)nbase + a;
-        spre[lane][j] = run;
-        if (j < MAX_SPAN) {
-          const int c = live ? spl[lane][eb + j + 1] - a : 0;
-          run += (live && c == 0 && MAX_SPAN - j <= dmax) ? 1 : c;     // empty in-range slot: implicit Unknown
-        }
+    for (int w = 0; w < W; ++w) {
+      const bool live = pos && e <= nS[w];
+      const uint32_t wb = (uint32_t)w << 26;
+#pragma unroll
+      for (int j = 0; j < MAX_SPAN; ++j) {
+        const int a = ss[w][j];
+        const bool unk = live && a == ss[w][j + 1] && MAX_SPAN - j <= dmax;
+        const int c = live ? (unk ? 1 : ss[w][j + 1] - a) : 0;
+        // entry i: node nbS[w] + a + i, or the slot's implicit Unknown (d - 1 = 7 - j)
+        const uint32_t e0v = (unk ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - j)) : nbS[w] + (uint32_t)a) | wb;
+        const int n1 = min(c, max(64 - q, 0));
+        int i = 0;
+#pragma unroll 1
+        for (; i < n1; ++i) myrow[q + i] = (e0v + (uint32_t)i) | K1_FIRST;
+#pragma unroll 1
+        for (; i < c; ++i) __builtin_amdgcn_raw_buffer_store_b32(e0v + (uint32_t)i, out, (uint32_t)(off * 256 + (q + i) * 4), 0, 0);
+        q += c;
       }
-      X = run;
+    }
+#pragma unroll 1
+    for (int r = max(q, 64); r < rounds * 64; ++r)     // the rest of a dense position's last row
+      __builtin_amdgcn_raw_buffer_store_b32(K1_IDLE, out, (uint32_t)(off * 256 + r * 4), 0, 0);
+    // (one wave: its LDS operations complete in issue order)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    unsigned long long live_rows = __ballot(pos);
+    while (live_rows) {                         // row 0 of every position, coalesced
+      const int pp = __builtin_ctzll(live_rows);
+      live_rows &= live_rows - 1ull;
+      const int offp = __builtin_amdgcn_readlane(off, pp);
+      __builtin_amdgcn_raw_buffer_store_b32(rows[pp * SCH_ROW + lane], out, (uint32_t)lane * 4u, offp * 256, 0);
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    int st[W], run = 0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      st[w] = run;
-      run += __builtin_amdgcn_readlane(X, w);
-    }
-    const int rounds = max(1, (run + 63) >> 6);
-    for (int r = 0; r < rounds; ++r) {
-      const int f = 64 * r + lane;
-      uint32_t ent = K1_IDLE;
-      if (f < run) {
-        // sentence w: the last with st[w] <= f (empty sentences share their
-        // successor's start); its slot j: the last with spre[w][j] <= i
-        int w = 0;
-#pragma unroll
-        for (int q = 1; q < W; ++q) w += st[q] <= f ? 1 : 0;
-        int sw = st[0];
-#pragma unroll
-        for (int q = 1; q < W; ++q) sw = q == w ? st[q] : sw;
-        const int ix = f - sw;
-        int j = 0;
-#pragma unroll
-        for (int q = 1; q < MAX_SPAN; ++q) j += spre[w][q] <= ix ? 1 : 0;
-        const int a = sfirst[w][j], cnt = sfirst[w][j + 1] - a;
-        ent = cnt == 0 ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - j))                 // d - 1 = 7 - j
-                       : (uint32_t)(a + (ix - spre[w][j]));
-        ent |= (uint32_t)w << 26;
-      }
-      __builtin_amdgcn_raw_buffer_store_b32(r == 0 ? (ent | K1_FIRST) : ent, out, (uint32_t)lane * 4u,
-                                            (int)((step + r) * 256), 0);
-    }
-    step += rounds;
-    __builtin_amdgcn_wave_barrier();             // the LDS tables are rewritten at the next position
+    base += total;
   }
 }
 
@@ -1830,6 +1879,15 @@ lt_beam_hw(DecodeParams p) {
   prefetch(1, n >= 1 ? ssp[0] : 0);
   __builtin_amdgcn_raw_buffer_store_b32(0u, bpr, OOB, 0, 0);
   __builtin_amdgcn_wave_barrier();
+#ifdef PK_PHASES
+  // diagnostic build: per-wave cycles of [0] position setup, [1] expansion
+  // decode + record + probe issue, [2] probe wait + score, [3] top-k, [4]
+  // prefetch + beam write (tools/gpu_phases.sh)
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long tstart = pk_stamp();
+  unsigned long long tprev = tstart;
+  unsigned long long nsteps_done = 0;
+#endif
 
   for (int e = 1; e <= nmax; ++e) {
     __builtin_amdgcn_s_waitcnt(0x0F71);         // vmcnt(1): the prefetch (older than the store)
@@ -1891,6 +1949,7 @@ lt_beam_hw(DecodeParams p) {
 #endif
     const int M = pre[MAX_SPAN];                // this half's expansions
     const int Mmax = gmax(M);
+    PK_STAMP(0);
 
     auto decode = [&](int g, int& j, int& r, int& i, int& sj, bool& imp, int& m) {     // (lt_beam_pk)
 #if HW_SPRE
@@ -1959,6 +2018,7 @@ lt_beam_hw(DecodeParams p) {
         BMProbe<NARROW> P;
         bm_issue<NARROW, true>(P, B, slots, seed, h0, c, need, aux);
         asm volatile("" ::: "memory");
+        PK_STAMP(1);
         const VEntry h1 = R[hb][hr];
         const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
         if (!skip) {
@@ -1969,6 +2029,7 @@ lt_beam_hw(DecodeParams p) {
         LK[KTP + G * t + hl] = myk[t];
         LG[KTP + G * t + hl] = myg[t];
       }
+      PK_STAMP(2);
       // top-k of this half's chunk entries and its running top-k
       const int R0 = max(0, min(RPC, (M - base + G - 1) / G));      // this group's rounds
       const unsigned long long rk = hl < nrun ? LK[KTP - nrun + hl] : 0ull;
@@ -2042,6 +2103,7 @@ lt_beam_hw(DecodeParams p) {
       }
     }
 
+    PK_STAMP(3);
     prefetch(e + 1, ss[MAX_SPAN]);              // after the position's last load wait
 
     // beam[e] of each half (Sequence.add, beam.py:112-116)
@@ -2074,8 +2136,23 @@ lt_beam_hw(DecodeParams p) {
         bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, 0);
     if (live && hl == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
+    PK_STAMP(4);
+#ifdef PK_PHASES
+    ++nsteps_done;
+#endif
   }
 
+#ifdef PK_PHASES
+  {
+    const unsigned long long tend = pk_stamp();
+    if (lane == 0) {
+      for (int i = 0; i < 8; ++i) atomicAdd(p.counters + 4 + i, ph[i]);
+      atomicAdd(p.counters + 12, nsteps_done);
+      atomicAdd(p.counters + 13, tend - tstart);
+      atomicAdd(p.counters + 14, 1ull);
+    }
+  }
+#endif
   // matures = beam[n] + EOS (beam.py:59-61); backtrace per (half, rank)
   __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): the backpointer stores are done
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -2266,6 +2343,13 @@ int beam_template_for(int k) {
   return -1;
 }
 
+hipError_t launch_k1_sched_count(const DecodeParams& p, int64_t* steps, hipStream_t st) {
+  const int waves = k1_waves(p.n_sent);
+  if (waves == 0) return hipSuccess;
+  hipLaunchKernelGGL((lt_k1_sched_count<P_W>), dim3(waves), dim3(64), 0, st, p, steps);
+  return hipGetLastError();
+}
+
 hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st,
                                 hipEvent_t e0, hipEvent_t e1) {
   const int waves = k1_waves(p.n_sent);
@@ -2280,6 +2364,7 @@ hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, 
 
 hipError_t launch_decode(const DecodeParams& p, hipStream_t st, bool count, hipEvent_t e0, hipEvent_t e1) {
   const int kt = beam_template_for(p.k);
+  if (kt == 1 && (!p.sched || !p.wave_off)) return hipErrorInvalidValue;   // (the library builds it first)
   // the timing events ride on the kernel's dispatch (no extra stream
   // commands between back-to-back decodes); an empty batch launches nothing
   if (p.n_sent == 0) {

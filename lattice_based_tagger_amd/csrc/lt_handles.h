@@ -80,8 +80,10 @@ struct lt_batch {
   int32_t n_pairs = 0;
   lt::F46* d_pairs = nullptr;
   // device preparation (the k=1 lane schedules of the pieces): has_sched = the
-  // batch has them (max_len <= 8); prep_done = the fill kernels are queued
-  bool has_sched = false, prep_done = false;
+  // batch has them (max_len <= 8; at create for max_k = 1, else at the first
+  // beam-1 decode -- lazy_sched: then in buffers of their own, not the
+  // arena); prep_done = the fill kernels are queued
+  bool has_sched = false, prep_done = false, lazy_sched = false;
   hipEvent_t prep_ev0 = nullptr, prep_ev1 = nullptr;   // around the last fill
   // device inputs, per launch piece (lt_batch_create: node records and
   // backpointers of a piece stay below 2^31 B)

@@ -217,6 +217,7 @@ __host__ __device__ inline int k1_candidates(const int32_t* ss, int e, int max_l
   }
   return x;
 }
+hipError_t launch_k1_sched_count(const DecodeParams& p, int64_t* steps, hipStream_t st);
 hipError_t launch_k1_sched_fill(const DecodeParams& p, const int64_t* wave_off, uint32_t* sched, hipStream_t st,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 

@@ -70,9 +70,12 @@ def main():
         sents = unique_text(entry['sentences'], a.sentences, a.seed)
     lex = fixture_lexicon(entry)
     tagger = Tagger(dictionary=fixture_dictionary(entry['lexicon']), lexicon=lex, score_funcs=funcs)
-    tagger.tag_batch(sents[:256], beam_size=a.k)                   # warm: model lowering, device model
     if a.chunk:
         Tagger.CHUNK = a.chunk
+    # warm-up, as a service does once at start: model lowering, device model,
+    # and the pipeline's batch arenas at chunk size (three chunks in flight;
+    # the context recycles them for every later call)
+    tagger.tag_batch(sents[:3 * Tagger.CHUNK], beam_size=a.k)
     model = lowered_model(funcs)
     npk = packer_for(model)
     best = {}
