@@ -1008,10 +1008,8 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
     const int total = __shfl(incl, 63);
     // entries in generation order (sentence, span slot = begin ascending,
     // the slot's nodes): the first 64 into the lane's LDS row (row 0 of the
-    // position, K1_FIRST on every entry), the rest (dense lattices) straight
-    // to the position's later rows
-#pragma unroll 4
-    for (int q = 0; q < 64; ++q) myrow[q] = K1_IDLE | K1_FIRST;
+    // position; the copy below adds K1_FIRST and the idle entries past run),
+    // the rest (dense lattices) straight to the position's later rows
     int q = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -1027,7 +1025,7 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
         const int n1 = min(c, max(64 - q, 0));
         int i = 0;
 #pragma unroll 1
-        for (; i < n1; ++i) myrow[q + i] = (e0v + (uint32_t)i) | K1_FIRST;
+        for (; i < n1; ++i) myrow[q + i] = e0v + (uint32_t)i;
 #pragma unroll 1
         for (; i < c; ++i) __builtin_amdgcn_raw_buffer_store_b32(e0v + (uint32_t)i, out, (uint32_t)(off * 256 + (q + i) * 4), 0, 0);
         q += c;
@@ -1043,8 +1041,9 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
     while (live_rows) {                         // row 0 of every position, coalesced
       const int pp = __builtin_ctzll(live_rows);
       live_rows &= live_rows - 1ull;
-      const int offp = __builtin_amdgcn_readlane(off, pp);
-      __builtin_amdgcn_raw_buffer_store_b32(rows[pp * SCH_ROW + lane], out, (uint32_t)lane * 4u, offp * 256, 0);
+      const int offp = __builtin_amdgcn_readlane(off, pp), runp = __builtin_amdgcn_readlane(run, pp);
+      const uint32_t v = lane < runp ? rows[pp * SCH_ROW + lane] : K1_IDLE;
+      __builtin_amdgcn_raw_buffer_store_b32(v | K1_FIRST, out, (uint32_t)lane * 4u, offp * 256, 0);
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
@@ -1235,14 +1234,26 @@ lt_viterbi_pk(DecodeParams p) {
     const uint32_t* bpg = p.bp + p.bp_off[sid];
     int pos = nw;
     // (pos > 0 and the depth bound hold on a consistent beam; they keep a
-    // corrupted one from chasing backpointers out of the sentence's rows)
-    for (int step = min((int)f.depth, nw) - 1; step >= 0 && pos > 0; --step) {
-      const uint32_t v = pos < BPL ? bpl[wv][lane][pos] : bpg[(int64_t)pos * bstride];
+    // corrupted one from chasing backpointers out of the sentence's rows).
+    // Positions past the LDS window first, from HBM; then the window: a loop
+    // of LDS reads only, so its stores are never waited for (one loop reading
+    // either memory compiles to a flat load, whose wait covers the stores of
+    // the step before -- a store round trip per path word)
+    int step = min((int)f.depth, nw) - 1;
+    for (; step >= 0 && pos >= BPL; --step) {
+      const uint32_t v = bpg[(int64_t)pos * bstride];
+      codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
+      pos -= (int)bp_d(v);
+    }
+    const uint32_t* const bw = bpl[wv][lane];
+    for (; step >= 0 && pos > 0; --step) {
+      const uint32_t v = bw[pos];
       codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
       pos -= (int)bp_d(v);
     }
     for (int j = (int)f.depth; j < nw; ++j) codes[j] = -1;      // padded layout
   }
+
   if (COUNT) {
     const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
                              pb = group_sum<64>(cnt.probe), ld = group_sum<64>(cnt.load);
@@ -2143,15 +2154,7 @@ lt_beam_hw(DecodeParams p) {
   }
 
 #ifdef PK_PHASES
-  {
-    const unsigned long long tend = pk_stamp();
-    if (lane == 0) {
-      for (int i = 0; i < 8; ++i) atomicAdd(p.counters + 4 + i, ph[i]);
-      atomicAdd(p.counters + 12, nsteps_done);
-      atomicAdd(p.counters + 13, tend - tstart);
-      atomicAdd(p.counters + 14, 1ull);
-    }
-  }
+  const unsigned long long tloop = pk_stamp();
 #endif
   // matures = beam[n] + EOS (beam.py:59-61); backtrace per (half, rank)
   __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): the backpointer stores are done
@@ -2181,6 +2184,19 @@ lt_beam_hw(DecodeParams p) {
       for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;     // padded layout
     }
   }
+#ifdef PK_PHASES
+  {
+    // [5] the matures and backtraces
+    const unsigned long long tend = pk_stamp();
+    ph[5] += tend - tloop;
+    if (lane == 0) {
+      for (int i = 0; i < 8; ++i) atomicAdd(p.counters + 4 + i, ph[i]);
+      atomicAdd(p.counters + 12, nsteps_done);
+      atomicAdd(p.counters + 13, tend - tstart);
+      atomicAdd(p.counters + 14, 1ull);
+    }
+  }
+#endif
 }
 
 template <int KT, int G, int WPB, bool NARROW>
