@@ -886,14 +886,6 @@ struct alignas(16) SentRec {
 // the slot's nodes in bindex order, or its implicit Unknown); macro-step r of
 // e covers list entries [64r, 64r + 64).  Entry of lane l: lt_internal.h K1_*.
 // ---------------------------------------------------------------------------
-// One wave per wave schedule, one lane per end position (64 positions per
-// chunk): every lane loads its position's span starts of the W sentences and
-// counts its candidates (run) at once, a wave prefix sum of the macro-steps
-// (max(1, ceil(run / 64))) places each position's rows, and each lane writes
-// its entries in generation order into its row of an LDS tile (64 rows,
-// stride 65 words: conflict-free for a common entry index), copied out by one
-// coalesced 256 B store per row.  A position with more than 64 entries (dense
-// lattices) writes its rows directly.
 constexpr int SCH_ROW = 65;                     // LDS row stride (words)
 // The W sentences of wave schedule `wave` (wave-uniform): lengths, first
 // nodes, span-table offsets, the longest length.
@@ -966,18 +958,20 @@ __global__ void __launch_bounds__(64) lt_k1_sched_count(DecodeParams p, int64_t*
   if (lane == 0) steps[wave] = total;
 }
 
-// One wave per wave schedule, one lane per end position (64 positions per
-// chunk): every lane loads its position's span starts of the W sentences and
-// counts its candidates (run) at once, a wave prefix sum of the macro-steps
-// (max(1, ceil(run / 64))) places each position's rows, and each lane writes
-// its entries in generation order into its row of an LDS tile (64 rows,
-// stride 65 words: conflict-free for a common entry index), copied out by one
-// coalesced 256 B store per row.  A position with more than 64 entries (dense
-// lattices) writes its further rows directly.
+// One wave per wave schedule, a lane pair per end position (32 positions per
+// chunk; the even lane takes sentences 0 .. H-1, the odd one H .. W-1): every
+// lane loads its position's span starts of its sentences and counts their
+// candidates at once, the pair adds its counts (run), a wave prefix sum of the
+// macro-steps (max(1, ceil(run / 64))) places each position's rows, and each
+// lane writes its entries in generation order into the position's row of an
+// LDS tile (32 rows, stride 65 words), the odd lane behind the even one's;
+// each row is copied out by one coalesced 256 B store.  A position with more
+// than 64 entries (dense lattices) writes its further rows directly.
 template <int W>
 __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
   static_assert(W < 8, "the sentence field holds W - 1");
-  __shared__ uint32_t rows[64 * SCH_ROW];
+  constexpr int H = (W + 1) / 2;                // sentences per lane of a pair
+  __shared__ uint32_t rows[32 * SCH_ROW];
   const int wave = blockIdx.x;
   const int lane = (int)threadIdx.x;
   const int slot0 = wave * W;
@@ -986,42 +980,56 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
   uint32_t nbS[W];
   int64_t soS[W];
   const int nmax = k1_wave_sents<W>(p, slot0, nS, nbS, soS);
+  const int part = lane & 1, pl = lane >> 1;
+  // this lane's sentences w = part * H + u
+  int nU[H];
+  uint32_t nbU[H];
+  int64_t soU[H];
+#pragma unroll
+  for (int u = 0; u < H; ++u) {
+    const bool hi = part && H + u < W;
+    nU[u] = part ? (hi ? nS[(H + u) % W] : 0) : nS[u];
+    nbU[u] = hi ? nbS[(H + u) % W] : nbS[u];
+    soU[u] = hi ? soS[(H + u) % W] : soS[u];
+  }
   // the wave's schedule rows as a buffer (stores past its rows are dropped)
   const int64_t w0 = wave_off[wave];
   const rsrc_t out = make_rsrc(sched + w0 * 64, (uint64_t)(wave_off[wave + 1] - w0) * 256u);
-  uint32_t* const myrow = rows + lane * SCH_ROW;
+  uint32_t* const myrow = rows + pl * SCH_ROW;
   int base = 0;                                 // rows of the chunks before
-  for (int e0 = 1; e0 <= nmax; e0 += 64) {
-    const int e = e0 + lane;
+  for (int e0 = 1; e0 <= nmax; e0 += 32) {
+    const int e = e0 + pl;
     const bool pos = e <= nmax;
     const int dmax = min(e, p.max_len);
-    int ss[W][MAX_SPAN + 1];
-    const int run = k1_position<W>(p, e, pos, nS, soS, ss);
+    int ss[H][MAX_SPAN + 1];
+    const int own = k1_position<H>(p, e, pos, nU, soU, ss);
+    const int other = __shfl_xor(own, 1);
+    const int run = own + other;                // the position's candidates
     const int rounds = pos ? max(1, (run + 63) >> 6) : 0;
-    int incl = rounds;                          // inclusive prefix over the lanes
+    int incl = part ? 0 : rounds;               // inclusive prefix over the positions (even lanes)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int t = __shfl_up(incl, (unsigned)o);
       incl += lane >= o ? t : 0;
     }
-    const int off = base + incl - rounds;       // the position's first row
+    const int off = base + incl - rounds;       // the position's first row (both lanes of the pair)
     const int total = __shfl(incl, 63);
     // entries in generation order (sentence, span slot = begin ascending,
-    // the slot's nodes): the first 64 into the lane's LDS row (row 0 of the
-    // position; the copy below adds K1_FIRST and the idle entries past run),
-    // the rest (dense lattices) straight to the position's later rows
-    int q = 0;
+    // the slot's nodes): the first 64 into the position's LDS row (row 0;
+    // the copy below adds K1_FIRST and the idle entries past run), the rest
+    // (dense lattices) straight to the position's later rows
+    int q = part ? other : 0;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const bool live = pos && e <= nS[w];
-      const uint32_t wb = (uint32_t)w << 26;
+    for (int u = 0; u < H; ++u) {
+      const bool live = pos && e <= nU[u];
+      const uint32_t wb = (uint32_t)(part * H + u) << 26;
 #pragma unroll
       for (int j = 0; j < MAX_SPAN; ++j) {
-        const int a = ss[w][j];
-        const bool unk = live && a == ss[w][j + 1] && MAX_SPAN - j <= dmax;
-        const int c = live ? (unk ? 1 : ss[w][j + 1] - a) : 0;
-        // entry i: node nbS[w] + a + i, or the slot's implicit Unknown (d - 1 = 7 - j)
-        const uint32_t e0v = (unk ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - j)) : nbS[w] + (uint32_t)a) | wb;
+        const int a = ss[u][j];
+        const bool unk = live && a == ss[u][j + 1] && MAX_SPAN - j <= dmax;
+        const int c = live ? (unk ? 1 : ss[u][j + 1] - a) : 0;
+        // entry i: node nbU[u] + a + i, or the slot's implicit Unknown (d - 1 = 7 - j)
+        const uint32_t e0v = (unk ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - j)) : nbU[u] + (uint32_t)a) | wb;
         const int n1 = min(c, max(64 - q, 0));
         int i = 0;
 #pragma unroll 1
@@ -1031,18 +1039,20 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
         q += c;
       }
     }
+    if (part) {
 #pragma unroll 1
-    for (int r = max(q, 64); r < rounds * 64; ++r)     // the rest of a dense position's last row
-      __builtin_amdgcn_raw_buffer_store_b32(K1_IDLE, out, (uint32_t)(off * 256 + r * 4), 0, 0);
+      for (int r = max(q, 64); r < rounds * 64; ++r)   // the rest of a dense position's last row
+        __builtin_amdgcn_raw_buffer_store_b32(K1_IDLE, out, (uint32_t)(off * 256 + r * 4), 0, 0);
+    }
     // (one wave: its LDS operations complete in issue order)
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    unsigned long long live_rows = __ballot(pos);
+    unsigned long long live_rows = __ballot(pos && !part);
     while (live_rows) {                         // row 0 of every position, coalesced
       const int pp = __builtin_ctzll(live_rows);
       live_rows &= live_rows - 1ull;
       const int offp = __builtin_amdgcn_readlane(off, pp), runp = __builtin_amdgcn_readlane(run, pp);
-      const uint32_t v = lane < runp ? rows[pp * SCH_ROW + lane] : K1_IDLE;
+      const uint32_t v = lane < runp ? rows[(pp >> 1) * SCH_ROW + lane] : K1_IDLE;
       __builtin_amdgcn_raw_buffer_store_b32(v | K1_FIRST, out, (uint32_t)lane * 4u, offp * 256, 0);
     }
     __builtin_amdgcn_wave_barrier();
@@ -1369,6 +1379,43 @@ __device__ __forceinline__ void rank_into(const unsigned long long* LK, int q0, 
 #ifndef PK_WPE
 #define PK_WPE(kt, narrow) ((kt) == 16 && (narrow) ? 4 : 1)
 #endif
+// The beam kernels' backtraces (beam.py:59-61 matures, Sequence.sequences):
+// a sentence's backpointer rows -- (n + 1) x bp_stride words in HBM -- are
+// first copied into LDS over its ring (dead once the final entries are read)
+// by its NL lanes, all loads in flight at once, when they fit CAP words; the
+// chain walks are then LDS reads only.  Walking HBM instead costs one memory
+// round trip per path word, the code stores of the word before waited for
+// behind it.
+constexpr int BP_STAGE_PER_LANE = 27;
+template <int NL, int CAP>
+__device__ __forceinline__ void stage_bp_rows(const uint32_t* __restrict__ bpg, int words, uint32_t* lbp, int li) {
+  constexpr int PER = (CAP + NL - 1) / NL;
+  uint32_t v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = li + u * NL;
+    v[u] = q < words ? bpg[q] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = li + u * NL;
+    if (q < words) lbp[q] = v[u];
+  }
+}
+// Mature rank t's path codes (padded with -1 to n) from backpointer rows
+// `bps` (LDS or HBM) of row stride `bstride`.
+template <typename P>
+__device__ __forceinline__ void walk_path(P bps, int bstride, int n, int depth, int t, int k, int32_t* codes) {
+  int pos = n, rank = t;
+  for (int step = min(depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
+    const uint32_t v = bps[pos * bstride + rank];
+    codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
+    pos -= (int)bp_d(v);
+    rank = min((int)bp_rank(v), k - 1);
+  }
+  for (int j = depth; j < n; ++j) codes[j] = -1;                        // padded layout
+}
+
 template <int KT, int WPB, bool NARROW, bool COUNT>
 __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PK_WPE(KT, NARROW), 8)))
 lt_beam_pk(DecodeParams p) {
@@ -1730,27 +1777,55 @@ lt_beam_pk(DecodeParams p) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const int nm = cnt9[n % RING];
   if (lane == 0) p.out_count[s] = nm;
-  for (int t = lane; t < k; t += 64) {          // mature rank t (one pass unless the beam exceeds 64)
-    if (t >= nm) {                              // unused mature slots read as empty
-      p.out_score[(int64_t)s * k + t] = 0.0;
-      p.out_len[(int64_t)s * k + t] = 0;
+  if constexpr (!BIG) {
+    // (one mature per lane) the final entries, then the backpointer rows
+    // into LDS over the ring (stage_bp_rows) when they fit
+    constexpr int RW = (int)(RING * KT * sizeof(VEntry) / 4);
+    constexpr int CAP = RW < BP_STAGE_PER_LANE * 64 ? RW : BP_STAGE_PER_LANE * 64;
+    const int t = lane;
+    double fs = 0.0;
+    int fd = 0;
+    if (t < k && t < nm) {
+      fs = R[n % RING][t].score;
+      fd = (int)R[n % RING][t].depth;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const int words = (n + 1) * bstride;
+    uint32_t* const lbp = reinterpret_cast<uint32_t*>(&R[0][0]);
+    const bool inl = words <= CAP;              // (wave-uniform)
+    if (inl) stage_bp_rows<64, CAP>(bp, words, lbp, lane);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (t < k) {
+      const int64_t o = (int64_t)s * k + t;
       int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
-      for (int j = 0; j < n; ++j) codes[j] = -1;
-      continue;
+      p.out_score[o] = t < nm ? fs + 0.0 : 0.0;
+      p.out_len[o] = t < nm ? fd : 0;
+      if (t >= nm) {                            // unused mature slots read as empty
+        for (int j = 0; j < n; ++j) codes[j] = -1;
+      } else if (inl) {
+        walk_path(static_cast<const uint32_t*>(lbp), bstride, n, fd, t, k, codes);
+      } else {
+        walk_path(static_cast<const uint32_t*>(bp), bstride, n, fd, t, k, codes);
+      }
     }
-    const VEntry& f = R[n % RING][t];
-    const int64_t o = (int64_t)s * k + t;
-    p.out_score[o] = f.score + 0.0;
-    p.out_len[o] = (int32_t)f.depth;
-    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
-    int pos = n, rank = t;
-    for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
-      const uint32_t v = bp[(int64_t)pos * bstride + rank];
-      codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
-      pos -= (int)bp_d(v);
-      rank = min((int)bp_rank(v), k - 1);
+  } else {
+    for (int t = lane; t < k; t += 64) {        // mature rank t (beams above 64: several passes)
+      if (t >= nm) {                            // unused mature slots read as empty
+        p.out_score[(int64_t)s * k + t] = 0.0;
+        p.out_len[(int64_t)s * k + t] = 0;
+        int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
+        for (int j = 0; j < n; ++j) codes[j] = -1;
+        continue;
+      }
+      const VEntry& f = R[n % RING][t];
+      const int64_t o = (int64_t)s * k + t;
+      p.out_score[o] = f.score + 0.0;
+      p.out_len[o] = (int32_t)f.depth;
+      walk_path(static_cast<const uint32_t*>(bp), bstride, n, (int)f.depth, t, k,
+                p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n);
     }
-    for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;       // padded layout
   }
   if (COUNT) {
     const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
@@ -2159,29 +2234,38 @@ lt_beam_hw(DecodeParams p) {
   // matures = beam[n] + EOS (beam.py:59-61); backtrace per (half, rank)
   __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): the backpointer stores are done
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  // the final entries, then each group's backpointer rows into LDS over its
+  // ring (stage_bp_rows) when they fit
+  constexpr int RW = (int)(RING * KT * sizeof(VEntry) / 4);
+  constexpr int CAP = RW < BP_STAGE_PER_LANE * G ? RW : BP_STAGE_PER_LANE * G;
+  const int nm = hv ? cnt9[n % RING] : 0;
+  double fs = 0.0;
+  int fd = 0;
+  if (hv && hl < k && hl < nm) {
+    fs = R[n % RING][hl].score;
+    fd = (int)R[n % RING][hl].depth;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const int words = (n + 1) * bstride;
+  uint32_t* const lbp = reinterpret_cast<uint32_t*>(&R[0][0]);
+  const uint32_t* const bpg = p.bp + bpo;
+  const bool inl = hv && words <= CAP;          // (group-uniform)
+  if (inl) stage_bp_rows<G, CAP>(bpg, words, lbp, hl);
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
   if (hv && hl < k) {
-    const int nm = cnt9[n % RING];
     if (hl == 0) p.out_count[s] = nm;
     const int64_t o = (int64_t)s * k + hl;
+    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
+    p.out_score[o] = hl < nm ? fs + 0.0 : 0.0;
+    p.out_len[o] = hl < nm ? fd : 0;
     if (hl >= nm) {
-      p.out_score[o] = 0.0;
-      p.out_len[o] = 0;
-      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
       for (int j = 0; j < n; ++j) codes[j] = -1;
+    } else if (inl) {
+      walk_path(static_cast<const uint32_t*>(lbp), bstride, n, fd, hl, k, codes);
     } else {
-      const VEntry& f = R[n % RING][hl];
-      p.out_score[o] = f.score + 0.0;
-      p.out_len[o] = (int32_t)f.depth;
-      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
-      const uint32_t* bpg = p.bp + bpo;
-      int pos = n, rank = hl;
-      for (int step = min((int)f.depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
-        const uint32_t v = bpg[(int64_t)pos * bstride + rank];
-        codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
-        pos -= (int)bp_d(v);
-        rank = min((int)bp_rank(v), k - 1);
-      }
-      for (int j = (int)f.depth; j < n; ++j) codes[j] = -1;     // padded layout
+      walk_path(bpg, bstride, n, fd, hl, k, codes);
     }
   }
 #ifdef PK_PHASES
