@@ -73,6 +73,8 @@ def parse():
                     help='1: gather every rank\'s results to rank 0 with RCCL inside each step '
                          '(default: on when WORLD_SIZE > 1; a failed RCCL setup then fails the run); '
                          '0: no result exchange (labelled in the JSON line)')
+    ap.add_argument('--no-wide-keys', dest='wide_keys', action='store_false',
+                    help='skip the wide-key (ids >= 2^20) model entry under "extra"')
     ap.add_argument('--extra-k', default='5,16',
                     help='beams timed after the headline on the same batch (single GPU), reported under '
                          '"extra": BASELINE config 3 secondary (k=5) and config 5 (k=16); "" for none')
@@ -367,6 +369,47 @@ def traffic_from_profiles(kernel, k, sentences, features, seed):
     return best
 
 
+def gather_ceiling(table_bytes):
+    """Random 16 B gather ceiling of the MI355X for a table of table_bytes:
+    the newest committed tools/gather_ceiling run (profiles/*/gather_ceiling.jsonl:
+    uniformly random 16 B loads, 4-16 in flight per lane, every CU busy), the
+    row of the smallest measured table at least this large, best over the
+    loads in flight.  (loads/s, source) or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'gather_ceiling*.jsonl')))
+    if not files:
+        return None
+    rows = []
+    for line in open(files[-1]):
+        try:
+            rows.append(json.loads(line))
+        except ValueError:
+            pass
+    fit = [r for r in rows if r.get('table_bytes', 0) >= table_bytes]
+    if not fit:
+        return None
+    tb = min(r['table_bytes'] for r in fit)
+    return max(r['loads_per_s'] for r in fit if r['table_bytes'] == tb), os.path.relpath(files[-1], ROOT), tb
+
+
+def probe_rate(table_loads, kernel_s, keys, slots):
+    """The feature-table slot loads the kernel issued per second against the
+    measured random-gather ceiling for the model's table size: the probes are
+    uniformly spread 16 B loads, so this is the roofline that binds them (the
+    byte roofline credits 16 B per load; the hardware moves a 128 B line per
+    miss).  Above 1.0 means cache reuse beyond uniform random (the beams'
+    hypotheses of one beam probe the same lines)."""
+    keys = np.asarray(keys).reshape(-1, 4)
+    narrow = keys.size == 0 or int(keys[:, :3].max()) < (1 << 20)
+    table_bytes = int(slots) * (16 if narrow else 32)
+    rate = table_loads / kernel_s
+    ceil = gather_ceiling(table_bytes)
+    return {'loads_per_s': rate, 'table_bytes': table_bytes,
+            'ceiling_loads_per_s': ceil[0] if ceil else None,
+            'frac': rate / ceil[0] if ceil else None,
+            'ceiling_source': ('%s (table of %d B)' % (ceil[1], ceil[2])) if ceil else None}
+
+
 def cpu_model():
     try:
         for line in open('/proc/cpuinfo'):
@@ -552,6 +595,17 @@ def main():
         for kx in extra_ks:
             if kx != k:
                 extra['k%d' % kx] = time_beam(ctx, dm, piece, raw, order, lo, hi, kx, a, keys)
+        if a.wide_keys:
+            # the same batch and model with every id moved past 2^20: the wide
+            # table format (32 B slots), at the largest extra beam
+            wpiece, wkeys = synth.widen_ids(piece, keys)
+            wdm = _capi.DeviceModel(ctx, wkeys, coefs)
+            kw = max(extra_ks)
+            extra['k%d_wide_keys' % kw] = time_beam(ctx, wdm, wpiece, raw, order, lo, hi, kw, a, wkeys,
+                                                    with_traffic=False)
+            extra['k%d_wide_keys' % kw]['model'] = ('the same model with every interned id + 2^20 '
+                                                    '(synth.widen_ids): the wide table format, 32 B slots')
+            wdm.close()
 
     if root:
         wl = ('config3' if a.sentences == 65536 else 'config4' if a.sentences == 1048576 else 'custom')
@@ -610,6 +664,7 @@ def main():
                 'work_equivalent_bytes_per_launch': B,
                 'work_equivalent_frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                 'layout': LAYOUT,
+                'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots),
             },
             'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                                'table_probes': probes, 'table_slot_loads': table_loads},
@@ -653,7 +708,7 @@ def total_sent_of(a, d, strong):
     return float(a.sentences * a.steps) if strong else d.sum(float(a.sentences * a.steps))
 
 
-def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys):
+def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys, with_traffic=True):
     """The headline's step (decode + result D2H on the copy stream, batch
     resident in HBM) at beam k on the same batch, same warmup / steps, one
     GPU: BASELINE config 3's k=5 secondary and config 5 (k=16).  Results
@@ -683,7 +738,7 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys):
     KB = kernel_bytes(piece, must_move_loads(table_loads, k), k, 0, blocks, d3)
     KI = kernel_bytes(piece, table_loads, k, 0, blocks, d3)              # as issued (both cuckoo slots)
     assert KI / avg_kernel_s / 1e9 <= HBM_PEAK_GBS, 'issued byte model above the HBM peak'
-    traffic = traffic_from_profiles(kernel, k, piece.n_sent, a.features, a.seed)
+    traffic = traffic_from_profiles(kernel, k, piece.n_sent, a.features, a.seed) if with_traffic else None
     return {
         'beam': k,
         'value': piece.n_sent * a.steps / elapsed,
@@ -702,7 +757,8 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys):
                      'work_equivalent_frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                      'traffic': traffic[0] if traffic else None,
                      'traffic_source': traffic[1] if traffic else None,
-                     'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None},
+                     'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
+                     'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots)},
         'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                            'table_probes': probes, 'table_slot_loads': table_loads},
     }

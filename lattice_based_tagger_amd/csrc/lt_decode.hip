@@ -1235,12 +1235,15 @@ lt_viterbi_pk(DecodeParams p) {
 
   // matures = beam[n] + EOS (beam.py:59-61); backtrace, one owner lane per sentence
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  int pdepth = 0;                                // the owner lane's path length
+  const int64_t cumn = own ? p.cum_n[sid] : 0;   // its first path-code slot
   if (own) {
     const VEntry& f = R[lane][nw % RING];
     p.out_count[sid] = 1;
     p.out_score[sid] = f.score + 0.0;
     p.out_len[sid] = (int32_t)f.depth;
-    int32_t* codes = p.out_codes + p.cum_n[sid];
+    pdepth = min((int)f.depth, nw);
+    int32_t* codes = p.out_codes + cumn;
     const uint32_t* bpg = p.bp + p.bp_off[sid];
     int pos = nw;
     // (pos > 0 and the depth bound hold on a consistent beam; they keep a
@@ -1261,7 +1264,16 @@ lt_viterbi_pk(DecodeParams p) {
       codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
       pos -= (int)bp_d(v);
     }
-    for (int j = (int)f.depth; j < nw; ++j) codes[j] = -1;      // padded layout
+  }
+  // the padded layout (-1 past each path): every sentence's tail by the whole
+  // wave, 64 codes per store (instead of one owner lane storing them in turn)
+#pragma unroll 1
+  for (int w = 0; w < W; ++w) {
+    const int nw_w = __builtin_amdgcn_readlane(nw, w), d_w = __builtin_amdgcn_readlane(pdepth, w);
+    if (nw_w <= d_w) continue;                   // (uniform)
+    const int64_t cb = ((int64_t)__builtin_amdgcn_readlane((int)(cumn >> 32), w) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)cumn, w);
+    for (int j = d_w + lane; j < nw_w; j += 64) p.out_codes[cb + j] = -1;
   }
 
   if (COUNT) {
@@ -1402,10 +1414,11 @@ __device__ __forceinline__ void stage_bp_rows(const uint32_t* __restrict__ bpg, 
     if (q < words) lbp[q] = v[u];
   }
 }
-// Mature rank t's path codes (padded with -1 to n) from backpointer rows
-// `bps` (LDS or HBM) of row stride `bstride`.
-template <typename P>
-__device__ __forceinline__ void walk_path(P bps, int bstride, int n, int depth, int t, int k, int32_t* codes) {
+// Mature rank t's path codes (padded with -1 to n unless the caller has)
+// from backpointer rows `bps` (LDS or HBM) of row stride `bstride`.
+template <typename P, typename C>
+__device__ __forceinline__ void walk_path(P bps, int bstride, int n, int depth, int t, int k, C codes,
+                                          bool pad = true) {
   int pos = n, rank = t;
   for (int step = min(depth, n) - 1; step >= 0 && pos > 0; --step) {   // (bounds: lt_viterbi_pk)
     const uint32_t v = bps[pos * bstride + rank];
@@ -1413,7 +1426,20 @@ __device__ __forceinline__ void walk_path(P bps, int bstride, int n, int depth, 
     pos -= (int)bp_d(v);
     rank = min((int)bp_rank(v), k - 1);
   }
-  for (int j = depth; j < n; ++j) codes[j] = -1;                        // padded layout
+  if (pad)
+    for (int j = depth; j < n; ++j) codes[j] = -1;                      // padded layout
+}
+// The sentence's padded codes (k x n words) staged in LDS at lco: filled with
+// -1 by the NL lanes before the walks, copied out coalesced after them.
+template <int NL>
+__device__ __forceinline__ void fill_codes(int32_t* lco, int words, int li) {
+#pragma unroll 1
+  for (int q = li; q < words; q += NL) lco[q] = -1;
+}
+template <int NL>
+__device__ __forceinline__ void copy_codes(int32_t* __restrict__ out, const int32_t* lco, int words, int li) {
+#pragma unroll 1
+  for (int q = li; q < words; q += NL) out[q] = lco[q];
 }
 
 template <int KT, int WPB, bool NARROW, bool COUNT>
@@ -1495,6 +1521,13 @@ lt_beam_pk(DecodeParams p) {
   prefetch(1, n >= 1 ? ssp[0] : 0, n >= 1);
   __builtin_amdgcn_raw_buffer_store_b32(0u, bpr, OOB, 0, 0);      // the invariant's first store
   __builtin_amdgcn_wave_barrier();
+#ifdef PK_PHASES
+  // diagnostic build: as lt_beam_hw's stamps
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long tstart = pk_stamp();
+  unsigned long long tprev = tstart;
+  unsigned long long nsteps_done = 0;
+#endif
 
   for (int e = 1; e <= n; ++e) {
     // vmcnt(1): the prefetched records and span starts landed (VMEM
@@ -1523,6 +1556,7 @@ lt_beam_pk(DecodeParams p) {
       pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)max(ss[j + 1] - ss[j], 1));   // (c <= 256, m < 2^21)
     }
     const int M = pre[MAX_SPAN];
+    PK_STAMP(0);
 #if PK_SPRE
     if (lane <= MAX_SPAN) sstp[wv][lane] = pfs;
     if (lane == 0) {
@@ -1603,6 +1637,7 @@ lt_beam_pk(DecodeParams p) {
         const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
         bm_issue<NARROW>(P, B, slots, seed, h0, c, need, aux);
         asm volatile("" ::: "memory");
+        PK_STAMP(1);
         const VEntry h1 = R[hb][hr];
         double cf[6];
         uint32_t pres = 0;
@@ -1617,6 +1652,7 @@ lt_beam_pk(DecodeParams p) {
         LK[KTP + 64 * t + lane] = myk[t];
         LG[KTP + 64 * t + lane] = myg[t];
       }
+      PK_STAMP(2);
       // Top-k of this chunk's entries and the running top-k.  The rank of an
       // entry is the number of entries with a larger key, or an equal key and
       // a smaller generation index (0 keys -- skipped / idle -- never win).
@@ -1733,6 +1769,7 @@ lt_beam_pk(DecodeParams p) {
     // the next position's records and span starts: issued after this
     // position's last load wait (VMEM operations retire in order, so any wait
     // for a younger load would also wait for these)
+    PK_STAMP(3);
     prefetch(e + 1, ss[MAX_SPAN], e < n);
 
     // beam[e] = the running top-k (Sequence.add, beam.py:112-116).  Winners
@@ -1770,7 +1807,14 @@ lt_beam_pk(DecodeParams p) {
     }
     if (lane == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
+    PK_STAMP(4);
+#ifdef PK_PHASES
+    ++nsteps_done;
+#endif
   }
+#ifdef PK_PHASES
+  const unsigned long long tloop = pk_stamp();
+#endif
 
   // matures = beam[n] + EOS (beam.py:59-61); backtrace per mature rank
   __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): the backpointer stores are done
@@ -1791,24 +1835,36 @@ lt_beam_pk(DecodeParams p) {
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    const int words = (n + 1) * bstride;
+    const int words = (n + 1) * bstride, cw = k * n;
+    int32_t* const cout = p.out_codes + (int64_t)k * p.cum_n[s];   // the k padded paths
     uint32_t* const lbp = reinterpret_cast<uint32_t*>(&R[0][0]);
+    int32_t* const lco = reinterpret_cast<int32_t*>(lbp + words);
     const bool inl = words <= CAP;              // (wave-uniform)
+    const bool cinl = words + cw <= CAP;        // the codes staged too
     if (inl) stage_bp_rows<64, CAP>(bp, words, lbp, lane);
+    if (cinl) fill_codes<64>(lco, cw, lane);
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     if (t < k) {
       const int64_t o = (int64_t)s * k + t;
-      int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n;
+      int32_t* codes = cout + (int64_t)t * n;
       p.out_score[o] = t < nm ? fs + 0.0 : 0.0;
       p.out_len[o] = t < nm ? fd : 0;
       if (t >= nm) {                            // unused mature slots read as empty
-        for (int j = 0; j < n; ++j) codes[j] = -1;
+        if (!cinl)
+          for (int j = 0; j < n; ++j) codes[j] = -1;
+      } else if (cinl) {
+        walk_path(static_cast<const uint32_t*>(lbp), bstride, n, fd, t, k, lco + t * n, false);
       } else if (inl) {
         walk_path(static_cast<const uint32_t*>(lbp), bstride, n, fd, t, k, codes);
       } else {
         walk_path(static_cast<const uint32_t*>(bp), bstride, n, fd, t, k, codes);
       }
+    }
+    if (cinl) {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      copy_codes<64>(cout, lco, cw, lane);
     }
   } else {
     for (int t = lane; t < k; t += 64) {        // mature rank t (beams above 64: several passes)
@@ -1827,6 +1883,18 @@ lt_beam_pk(DecodeParams p) {
                 p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)t * n);
     }
   }
+#ifdef PK_PHASES
+  {
+    const unsigned long long tend = pk_stamp();
+    ph[5] += tend - tloop;
+    if (lane == 0) {
+      for (int i = 0; i < 8; ++i) atomicAdd(p.counters + 4 + i, ph[i]);
+      atomicAdd(p.counters + 12, nsteps_done);
+      atomicAdd(p.counters + 13, tend - tstart);
+      atomicAdd(p.counters + 14, 1ull);
+    }
+  }
+#endif
   if (COUNT) {
     const unsigned long long ex = group_sum<64>(cnt.exp), tu = group_sum<64>(cnt.tup),
                              pb = group_sum<64>(cnt.probe), ld = group_sum<64>(cnt.load);
@@ -2110,7 +2178,10 @@ lt_beam_hw(DecodeParams p) {
         if (!skip) {
           const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
-          myg[t] = (uint32_t)g;
+          // the list entry's payload: the expansion as its backpointer word
+          // (ranks are by list position, so nothing reads g itself; the
+          // writer of beam[e] takes node, span and parent rank from it)
+          myg[t] = bp_pack(imp ? UNK_LOCAL : (uint32_t)node, (uint32_t)d, (uint32_t)hr);
         }
         LK[KTP + G * t + hl] = myk[t];
         LG[KTP + G * t + hl] = myg[t];
@@ -2194,17 +2265,14 @@ lt_beam_hw(DecodeParams p) {
 
     // beam[e] of each half (Sequence.add, beam.py:112-116)
     VEntry ne;
-    uint32_t bpv = 0;
     const bool writer = live && hl < nrun;
-    int wj = 0, wr = 0, wi = 0, wsj = 0, wm = 1;
-    bool wimp = false;
-    if (writer) decode((int)LG[KTP - nrun + hl], wj, wr, wi, wsj, wimp, wm);
-    const int wd = MAX_SPAN - wj;
-    const uint32_t wnode = wimp ? UNK_LOCAL : (uint32_t)(wsj + wi);
+    const uint32_t bpv = writer ? LG[KTP - nrun + hl] : bp_pack(0u, 1u, 0u);   // node, span, parent rank
+    const int wd = (int)bp_d(bpv), wr = (int)bp_rank(bpv);
+    const uint32_t wnode = bp_node(bpv);
+    const bool wimp = wnode == UNK_LOCAL;
     const bool far = writer && !wimp && (int)wnode - A0 >= STAGE;
     auto build = [&](const Cand& c) {
       ne = v_grow<false>(R[ring_back(em9, wd)][wr], c, ord_score(LK[KTP - nrun + hl]), wnode);
-      bpv = bp_pack(wnode, (uint32_t)wd, (uint32_t)wr);
     };
     auto near = [&]() {                          // staged record or implicit Unknown
       const int so = min((int)wnode - A0, STAGE - 1);
@@ -2247,27 +2315,37 @@ lt_beam_hw(DecodeParams p) {
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
-  const int words = (n + 1) * bstride;
+  const int words = (n + 1) * bstride, cw = k * n;
+  int32_t* const cout = p.out_codes + (hv ? (int64_t)k * p.cum_n[s] : 0);   // the k padded paths
   uint32_t* const lbp = reinterpret_cast<uint32_t*>(&R[0][0]);
+  int32_t* const lco = reinterpret_cast<int32_t*>(lbp + words);
   const uint32_t* const bpg = p.bp + bpo;
   const bool inl = hv && words <= CAP;          // (group-uniform)
+  const bool cinl = inl && words + cw <= CAP;   // the codes staged too
   if (inl) stage_bp_rows<G, CAP>(bpg, words, lbp, hl);
+  if (cinl) fill_codes<G>(lco, cw, hl);
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   if (hv && hl < k) {
     if (hl == 0) p.out_count[s] = nm;
     const int64_t o = (int64_t)s * k + hl;
-    int32_t* codes = p.out_codes + (int64_t)k * p.cum_n[s] + (int64_t)hl * n;
+    int32_t* codes = cout + (int64_t)hl * n;
     p.out_score[o] = hl < nm ? fs + 0.0 : 0.0;
     p.out_len[o] = hl < nm ? fd : 0;
     if (hl >= nm) {
-      for (int j = 0; j < n; ++j) codes[j] = -1;
+      if (!cinl)
+        for (int j = 0; j < n; ++j) codes[j] = -1;
+    } else if (cinl) {
+      walk_path(static_cast<const uint32_t*>(lbp), bstride, n, fd, hl, k, lco + hl * n, false);
     } else if (inl) {
       walk_path(static_cast<const uint32_t*>(lbp), bstride, n, fd, hl, k, codes);
     } else {
       walk_path(bpg, bstride, n, fd, hl, k, codes);
     }
   }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  if (cinl) copy_codes<G>(cout, lco, cw, hl);
 #ifdef PK_PHASES
   {
     // [5] the matures and backtraces

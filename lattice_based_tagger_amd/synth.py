@@ -440,6 +440,25 @@ def pack_fast(raw, model, lay=None, cols=None, implicit_unk=True):
     return batch, keys, coef[model.probed_idx].astype(np.float64)
 
 
+def widen_ids(packed, keys, offset=1 << 20):
+    """The same batch and model with every interned id moved up by `offset`
+    (id 0 -- "occurs in no key" -- stays 0).  Ids of 2^20 and more put the
+    model in the wide table format (32 B slots, lattice_decode.h
+    lt_model_desc.narrow = 0); id equality, hence every feature match and
+    every result, is unchanged."""
+    import copy
+    wp = copy.copy(packed)
+    shift = lambda a: np.where(np.asarray(a) != 0, np.asarray(a) + offset, 0).astype(np.asarray(a).dtype)  # noqa: E731
+    for f in ('node_word', 'node_morph0', 'node_tag'):
+        setattr(wp, f, shift(getattr(packed, f)))
+    if getattr(packed, 'unk_n', 0):
+        for f in ('unk_word', 'unk_morph0', 'unk_tag'):
+            setattr(wp, f, shift(getattr(packed, f)))
+    wk = np.array(keys, copy=True).reshape(-1, 4)
+    wk[:, :3] = shift(wk[:, :3])
+    return wp, wk
+
+
 # ---------------------------------------------------------------------------
 # Word rendering (reference input form)
 # ---------------------------------------------------------------------------

@@ -154,6 +154,26 @@ def test_class46_pair_escape_matches_c_oracle(gpu_decoder, k):
     assert (ex, tu) == (o_ex, o_tu)
 
 
+@pytest.mark.parametrize('k', [1, 5, 16])
+def test_wide_key_model_matches_narrow_and_oracle(gpu_decoder, k):
+    """A model whose interned ids pass 2^20 (synth.widen_ids) lives in the
+    wide table format (32 B slots, four 32-bit key compares): every kernel
+    decodes it byte-equal to the same batch under the narrow model and to the
+    C restatement, operation counts included."""
+    packed, keys, coefs = _synthetic(2048 if k < 16 else 1024, seed=1700 + k, n_features=200_000)
+    wp, wk = synth.widen_ids(packed, keys)
+    narrow, n_ops = _gpu_decode(gpu_decoder.ctx, packed, keys, coefs, k)
+    wide, w_ops = _gpu_decode(gpu_decoder.ctx, wp, wk, coefs, k)
+    for a, b in zip(narrow, wide):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    assert n_ops[:2] == w_ops[:2]
+    o = lt_oracle.decode(wp, wk, coefs, k, nthreads=16)
+    assert np.array_equal(wide[0], o[0]) and np.array_equal(wide[1], o[1])
+    assert np.array_equal(wide[2].view(np.uint64), o[2].view(np.uint64))
+    assert np.array_equal(wide[3], o[3])
+    assert (w_ops[0], w_ops[1]) == (o[4], o[5])
+
+
 def test_long_sentences_cross_the_lds_backpointer_window(gpu_decoder):
     """k=1 keeps the backpointers of end positions < PK_BPL (87) in LDS and
     the rest in HBM: 40-eojeol sentences (about 140 characters) put most

@@ -152,3 +152,23 @@ def test_c_oracle_matches_python_oracle_at_large_beams(k):
             off = k * cum[s] + t * len(c)
             assert [tuple(w) for w in path[1:-1]] == [tuple(objs[s][x]) for x in codes[off:off + L]]
     assert n_full > 0
+
+
+def test_widened_ids_decode_identically():
+    """synth.widen_ids moves every interned id past 2^20 (the wide, 32 B slot
+    table format on the device): the C restatement decodes the widened batch
+    and model exactly as the original -- the premise of the wide-key GPU
+    parity test and bench entry."""
+    raw = synth.make_lattices(200, seed=5)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=5, n_features=20_000)
+    packed, keys, coefs = synth.pack_fast(raw, sm, lay, cols)
+    wp, wk = synth.widen_ids(packed, keys)
+    assert int(wk[:, :3].max()) >= (1 << 20) and int(wp.node_word.max()) >= (1 << 20)
+    for k in (1, 5):
+        a = lt_oracle.decode(packed, keys, coefs, k)
+        b = lt_oracle.decode(wp, wk, coefs, k)
+        for x, y in zip(a[:4], b[:4]):
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+        assert a[4:] == b[4:]
