@@ -392,21 +392,29 @@ def gather_ceiling(table_bytes):
     return max(r['loads_per_s'] for r in fit if r['table_bytes'] == tb), os.path.relpath(files[-1], ROOT), tb
 
 
-def probe_rate(table_loads, kernel_s, keys, slots):
-    """The feature-table slot loads the kernel issued per second against the
-    measured random-gather ceiling for the model's table size: the probes are
-    uniformly spread 16 B loads, so this is the roofline that binds them (the
-    byte roofline credits 16 B per load; the hardware moves a 128 B line per
-    miss).  Above 1.0 means cache reuse beyond uniform random (the beams'
-    hypotheses of one beam probe the same lines)."""
+def probe_rate(table_loads, kernel_s, keys, slots, traffic=None):
+    """The feature-table probes against the measured random-gather ceiling
+    for the model's table size (tools/gather_ceiling.hip): the probes are
+    spread 16 B loads, each L2 miss moves a 128 B line, so the roofline that
+    binds them is a line rate, not HBM bytes.
+      frac        issued slot loads per second / the uniform-random ceiling;
+                  above 1.0 = cache reuse beyond uniform random (line groups,
+                  Zipf-popular words, the hypotheses of one beam)
+      fabric_frac the kernel's L2-miss traffic (PMC, roofline.traffic) per
+                  second / the ceiling's line rate (loads/s x 128 B)"""
     keys = np.asarray(keys).reshape(-1, 4)
     narrow = keys.size == 0 or int(keys[:, :3].max()) < (1 << 20)
     table_bytes = int(slots) * (16 if narrow else 32)
     rate = table_loads / kernel_s
     ceil = gather_ceiling(table_bytes)
+    line_gbps = ceil[0] * 128 / 1e9 if ceil else None
+    fabric_gbps = traffic / kernel_s / 1e9 if traffic else None
     return {'loads_per_s': rate, 'table_bytes': table_bytes,
             'ceiling_loads_per_s': ceil[0] if ceil else None,
             'frac': rate / ceil[0] if ceil else None,
+            'ceiling_line_GBps': line_gbps,
+            'fabric_GBps': fabric_gbps,
+            'fabric_frac': fabric_gbps / line_gbps if (line_gbps and fabric_gbps) else None,
             'ceiling_source': ('%s (table of %d B)' % (ceil[1], ceil[2])) if ceil else None}
 
 
@@ -664,7 +672,7 @@ def main():
                 'work_equivalent_bytes_per_launch': B,
                 'work_equivalent_frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                 'layout': LAYOUT,
-                'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots),
+                'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots, traffic[0] if traffic else None),
             },
             'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                                'table_probes': probes, 'table_slot_loads': table_loads},
@@ -758,7 +766,8 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys, with_traffic=True)
                      'traffic': traffic[0] if traffic else None,
                      'traffic_source': traffic[1] if traffic else None,
                      'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
-                     'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots)},
+                     'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots,
+                                              traffic[0] if traffic else None)},
         'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                            'table_probes': probes, 'table_slot_loads': table_loads},
     }
