@@ -1398,6 +1398,25 @@ __device__ __forceinline__ void rank_into(const unsigned long long* LK, int q0, 
 // chain walks are then LDS reads only.  Walking HBM instead costs one memory
 // round trip per path word, the code stores of the word before waited for
 // behind it.
+// A scoring round's candidate past the staged block (a position with more
+// than STAGE candidates): a global load in a wave-uniform branch that waits for
+// its own loads.  With the loads' wait inside the branch, no load is in flight
+// into a register the common path writes; otherwise the compiler's
+// write-after-write wait at the next round (a vmcnt(0), VMEM operations counted
+// in order) would also wait for the previous position's backpointer store
+// before the round's probes are issued.
+__device__ __forceinline__ void beam_far(Cand& c, bool far, const Bufs& B, uint32_t gn) {
+  if (__builtin_amdgcn_ballot_w64(far) != 0ull) {
+    if (far) c = load_cand(B, gn);
+    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+  }
+}
+// End of a scoring round: every load of the round has been waited for by its
+// use (the probes by the checks of the lanes that issued them, the records and
+// pairs by the sum), so this wait costs nothing; it tells the compiler so, and
+// the next round's first writes to those registers carry no wait.
+__device__ __forceinline__ void round_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 constexpr int BP_STAGE_PER_LANE = 27;
 template <int NL, int CAP>
 __device__ __forceinline__ void stage_bp_rows(const uint32_t* __restrict__ bpg, int words, uint32_t* lbp, int li) {
@@ -1620,14 +1639,14 @@ lt_beam_pk(DecodeParams p) {
         const int d = MAX_SPAN - j;
         const int node = sj + i;
         const int so = node - A0;
-        Cand c;
-        if (!act) {
-          c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
-        } else if (imp || so < STAGE) {
-          c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + 2 * so, 1, B.pairs, B, imp ? INV : nbase + (uint32_t)node);
-        } else {
-          c = load_cand(B, nbase + (uint32_t)node);
-        }
+        // the staged record (or implicit Unknown) for every lane, then a record
+        // past the staged block by a wave-uniform branch that waits for its own
+        // loads (beam_far): the common path has no load in flight into a
+        // register it writes
+        const bool far = act && !imp && so >= STAGE;
+        Cand c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + 2 * min(max(so, 0), STAGE - 1), 1, B.pairs, B,
+                            (imp || !act) ? INV : nbase + (uint32_t)node);
+        beam_far(c, far, B, nbase + (uint32_t)node);
         const int hb = act ? ring_back(em9, d) : 0;
         const int hr = act ? r : 0;
         const VEntry h0 = R[hb][hr];
@@ -1651,6 +1670,7 @@ lt_beam_pk(DecodeParams p) {
         }
         LK[KTP + 64 * t + lane] = myk[t];
         LG[KTP + 64 * t + lane] = myg[t];
+        round_done();
       }
       PK_STAMP(2);
       // Top-k of this chunk's entries and the running top-k.  The rank of an
@@ -2155,15 +2175,10 @@ lt_beam_hw(DecodeParams p) {
         const int d = MAX_SPAN - j;
         const int node = sj + i;
         const int so = node - A0;
-        Cand c;
-        if (!act) {
-          c = Cand{0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, 0.0};
-        } else if (imp || so < STAGE) {
-          c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + CPG * hf + 2 * so, 1, pxl, B,
-                         imp ? INV : nbase + (uint32_t)node);
-        } else {
-          c = load_cand(B, nbase + (uint32_t)node);
-        }
+        const bool far = act && !imp && so >= STAGE;   // (beam_far, as lt_beam_pk)
+        Cand c = cand_lds32(imp ? ucan + 2 * (d - 1) : cst + CPG * hf + 2 * min(max(so, 0), STAGE - 1), 1, pxl, B,
+                            (imp || !act) ? INV : nbase + (uint32_t)node);
+        beam_far(c, far, B, nbase + (uint32_t)node);
         const int hb = act ? ring_back(em9, d) : 0;
         const int hr = act ? r : 0;
         const VEntry h0 = R[hb][hr];
@@ -2185,6 +2200,7 @@ lt_beam_hw(DecodeParams p) {
         }
         LK[KTP + G * t + hl] = myk[t];
         LG[KTP + G * t + hl] = myg[t];
+        round_done();
       }
       PK_STAMP(2);
       // top-k of this half's chunk entries and its running top-k
