@@ -687,8 +687,9 @@ struct BMProbe {
 
 // INIT: give the slots of lanes that load nothing a (frozen) value -- needed by
 // branch-free checks; with exec-masked checks it only shapes register
-// allocation (lt_beam_hw spills less with it, lt_beam_pk runs fewer copies
-// without it)
+// allocation: the frozen value is materialised as zeros (two 64-bit moves per
+// probed class and round), so only lt_beam_hw with wide keys takes it (it
+// spills without it)
 template <bool NARROW, bool INIT = !BM_BRANCHY>
 __device__ __forceinline__ void bm_issue(BMProbe<NARROW>& P, const Bufs& B, uint32_t slots, uint32_t seed,
                                          const VEntry& h, const Cand& c, uint32_t need, const Aux& aux) {
@@ -1483,15 +1484,21 @@ lt_beam_pk(DecodeParams p) {
   __shared__ unsigned long long tkey[WPB][KT];
   __shared__ uint32_t tgen[WPB][KT];
   constexpr bool USE_D3 = KT <= 4;              // (its 8 KiB would cost a block per CU above)
-  __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   // the position's span starts and expansion prefixes, for the decode of an
   // expansion index (a lane-variable index into wave-uniform values)
-  __shared__ __attribute__((aligned(16))) int sstp[WPB][PK_SPRE ? 12 : 1];
-  __shared__ __attribute__((aligned(16))) int sprep[WPB][PK_SPRE ? 12 : 1];
+  // (sized to the entries read: at KT = 16 every byte counts -- 16 one-wave
+  // blocks per CU need at most 10,240 B each)
+  __shared__ int sstp[WPB][PK_SPRE ? MAX_SPAN + 1 : 1];
+  __shared__ __attribute__((aligned(16))) int sprep[WPB][PK_SPRE ? MAX_SPAN : 4];
   __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records
   stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
-  if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
+  if constexpr (USE_D3) {
+    // (declared only where used: a 1-element placeholder's 8 B would cost
+    // KT = 16 its sixteenth 1-wave block per CU -- 10,248 B > 160 KiB / 16)
+    __shared__ double d3l[D3_DIM * D3_DIM];
+    aux = stage_aux<NARROW>(p, d3l);
+  }
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
@@ -1970,14 +1977,16 @@ lt_beam_hw(DecodeParams p) {
   __shared__ __attribute__((aligned(16))) int sst[WPB][S][12];   // each group's span starts of the position
   __shared__ __attribute__((aligned(16))) int spre[WPB][S][HW_SPRE ? 12 : 1];   // and expansion prefixes
   constexpr bool USE_D3 = KT <= 4;
-  __shared__ double d3l[USE_D3 ? D3_DIM * D3_DIM : 1];
   __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records
   // the batch's class-4/6 pair table (read per expansion: LDS, not the caches)
   __shared__ F46 pxl[MAX_PAIRS];
   for (int i = (int)threadIdx.x; i < p.n_pairs; i += (int)blockDim.x) pxl[i] = p.pairs[i];
   stage_unk(p, ucan);
   Aux aux{nullptr, 0u, p.hk};
-  if (USE_D3) aux = stage_aux<NARROW>(p, d3l);
+  if constexpr (USE_D3) {
+    __shared__ double d3l[D3_DIM * D3_DIM];
+    aux = stage_aux<NARROW>(p, d3l);
+  }
 
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = (int)(threadIdx.x & 63);
@@ -2185,7 +2194,7 @@ lt_beam_hw(DecodeParams p) {
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
         const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
         BMProbe<NARROW> P;
-        bm_issue<NARROW, true>(P, B, slots, seed, h0, c, need, aux);
+        bm_issue<NARROW, !NARROW>(P, B, slots, seed, h0, c, need, aux);   // (INIT: wide keys only)
         asm volatile("" ::: "memory");
         PK_STAMP(1);
         const VEntry h1 = R[hb][hr];
