@@ -757,9 +757,22 @@ static void arena_free(lt_arena& a) {
   a = lt_arena{};
 }
 
-// Arenas up to this size are kept for reuse, at most SPARE_N per context.
+// Arenas up to this size are kept for reuse, at most SPARE_N per context
+// (Tagger.tag_batch keeps three chunk batches in flight, one more is queued).
 constexpr size_t SPARE_MAX = (size_t)1 << 30;
-constexpr size_t SPARE_N = 2;
+constexpr size_t SPARE_N = 4;
+
+// New arenas are sized with headroom and rounded up to one of eight size
+// classes per power of two, so that a recycled arena fits the next batches
+// of similar size (chunks of one pipeline differ by a few per cent) instead
+// of each slightly larger batch paying a device and a pinned host allocation.
+static size_t arena_class(size_t n) {
+  if (n == 0) return 0;
+  n += n / 16;
+  size_t g = 256;
+  while ((g << 4) <= n) g <<= 1;                 // granule: 1/8 .. 1/16 of n
+  return (n + g - 1) / g * g;
+}
 
 // An arena with at least (dn, hn) bytes: the smallest fitting spare, else a
 // new allocation (a spare that does not fit stays for a later batch).
@@ -778,6 +791,8 @@ static hipError_t arena_take(lt_ctx* c, size_t dn, size_t hn, lt_arena& out) {
     }
   }
   out = lt_arena{};
+  dn = arena_class(dn);
+  hn = arena_class(hn);
   hipError_t e = hipSuccess;
   if (dn) e = hipMalloc((void**)&out.d, dn);
   if (e == hipSuccess) out.d_bytes = dn;
@@ -787,6 +802,8 @@ static hipError_t arena_take(lt_ctx* c, size_t dn, size_t hn, lt_arena& out) {
   return e;
 }
 
+// Back to the spares; with SPARE_N kept, the smallest of them and this one
+// is freed.
 static void arena_give(lt_ctx* c, lt_arena& a) {
   if (!a.d && !a.h) return;
   if (a.d_bytes <= SPARE_MAX) {
@@ -796,6 +813,10 @@ static void arena_give(lt_ctx* c, lt_arena& a) {
       a = lt_arena{};
       return;
     }
+    int small = 0;
+    for (int i = 1; i < (int)c->spare.size(); ++i)
+      if (c->spare[i].d_bytes + c->spare[i].h_bytes < c->spare[small].d_bytes + c->spare[small].h_bytes) small = i;
+    if (c->spare[small].d_bytes + c->spare[small].h_bytes < a.d_bytes + a.h_bytes) std::swap(c->spare[small], a);
   }
   arena_free(a);
 }
