@@ -255,7 +255,7 @@ def workgroups(k, n_sent):
     """Workgroups of the decode launch (lt_decode.hip launch_k): each stages
     the dense class-3 table and the implicit-Unknown records."""
     if k == 1:
-        return -(-n_sent // (6 * 4))                   # W = 6 sentences per wave, 4 waves per block
+        return -(-n_sent // (8 * 8))                   # W = 8 sentences per wave, 8 waves per block (narrow keys)
     if k <= 8:
         return -(-n_sent // ((64 // (16 if k <= 3 else 32)) * 4))
     return -(-n_sent // (1 if k <= 16 else 2))

@@ -832,6 +832,7 @@ static void batch_free(lt_batch* b) {
     for (lt_piece& pc : b->pieces) {
       dfree(pc.d_sched);
       dfree(pc.d_wave_off);
+      dfree(pc.d_place);
     }
   arena_give(b->ctx, b->arena);
   delete b;
@@ -902,6 +903,11 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p);
 // The batch's device preparation, queued on `st` unless done: the k=1 lane
 // schedule of every piece (lt_k1_sched), between the batch's prep events.  No
 // allocation (arena memory) and no wait.
+// characters (end positions) of piece q
+static int64_t piece_chars(const lt_batch* b, size_t q) {
+  return (q + 1 < b->pieces.size() ? b->pieces[q + 1].chars0 : b->total_chars) - b->pieces[q].chars0;
+}
+
 static hipError_t prep_fill(lt_batch* b, hipStream_t st) {
   if (!b->has_sched || b->prep_done) return hipSuccess;
   hipError_t e = hipSuccess;
@@ -938,9 +944,11 @@ static lt_status lazy_sched(lt_ctx* c, lt_batch* b) {
     HIP_TRY(hipMalloc((void**)&d_off, ((size_t)waves + 1) * 8));
     pc.d_wave_off = d_off;                     // (freed with the batch from here on)
     b->lazy_sched = true;
+    HIP_TRY(hipMalloc((void**)&pc.d_place, (size_t)std::max<int64_t>(piece_chars(b, q), 1) * 4));
     DecodeParams p{};
     piece_params(b, q, 1, p);
     p.max_len = b->max_len;
+    p.k1_place = pc.d_place;                   // (has_sched is set once the schedule exists)
     HIP_TRY(launch_k1_sched_count(p, d_off, c->stream));
     offs[q].assign((size_t)waves + 1, 0);
     HIP_TRY(hipMemcpyAsync(offs[q].data(), d_off, (size_t)waves * 8, hipMemcpyDeviceToHost, c->stream));
@@ -952,6 +960,8 @@ static lt_status lazy_sched(lt_ctx* c, lt_batch* b) {
     int64_t run = 0;
     for (size_t w = 0; w + 1 < wo.size(); ++w) {   // exclusive prefix sum
       const int64_t x = wo[w];
+      if (x >= ((int64_t)1 << K1_TBITS))
+        return fail(LT_EUNSUPPORTED, "decode: %lld macro-steps in one beam-1 wave schedule", (long long)x);
       wo[w] = run;
       run += x;
     }
@@ -1058,6 +1068,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   b->has_sched = d->max_len <= MAX_SPAN && max_k == 1;
   b->n_unk = d->n_unk;
   std::vector<std::vector<int64_t>> wave_off(P);
+  std::vector<std::vector<uint32_t>> place(P);   // k=1 placements, uploaded with the batch
   if (b->has_sched) {
     for (size_t q = 0; q < P; ++q) {
       lt_piece& pc = b->pieces[q];
@@ -1068,26 +1079,36 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       const int waves = k1_waves(pc.n_sent);
       std::vector<int64_t>& wo = wave_off[q];
       wo.assign((size_t)waves + 1, 0);
+      place[q].assign((size_t)pcum[q][(size_t)pc.n_sent], 0u);
+      std::atomic<int64_t> longest{0};
       parallel_ranges(waves, [&](int, int64_t lo, int64_t hi) {
         for (int64_t w = lo; w < hi; ++w) {
-          const int32_t* ssw[K1_W];
-          int nw[K1_W], cnt = 0, nmax = 0;
+          const int32_t* ssw[K1_W] = {};
+          int nw[K1_W] = {}, cnt = 0;
+          uint32_t* plw[K1_W] = {};
           for (int i = 0; i < K1_W && w * K1_W + i < pc.n_sent; ++i, ++cnt) {
-            const int32_t s = pc.s0 + order[q][(size_t)(w * K1_W + i)];
+            const int32_t sl = order[q][(size_t)(w * K1_W + i)];
+            const int32_t s = pc.s0 + sl;
             ssw[cnt] = d->span_start + d->sent_span_off[s];
             nw[cnt] = d->sent_n[s];
-            nmax = std::max(nmax, nw[cnt]);
+            plw[cnt] = place[q].data() + pcum[q][(size_t)sl];
           }
-          int64_t steps = 0;
-          for (int e = 1; e <= nmax; ++e) {
-            int run = 0;
-            for (int i = 0; i < cnt; ++i)
-              if (e <= nw[i]) run += k1_candidates(ssw[i], e, d->max_len);
-            steps += std::max(1, (run + 63) >> 6);
-          }
+          const int64_t steps = k1_schedule(
+              cnt, nw, [&](int i, int e) { return k1_candidates(ssw[i], e, d->max_len); },
+              [&](int64_t t, int i, int e, int off, int) {
+                plw[i][e - 1] = (uint32_t)t | ((uint32_t)off << K1_TBITS);   // (t < 2^K1_TBITS: checked below)
+              });
           wo[(size_t)w + 1] = steps;
+          int64_t m = longest.load();
+          while (steps > m && !longest.compare_exchange_weak(m, steps)) {
+          }
         }
       }, 64);
+      if (longest.load() >= ((int64_t)1 << K1_TBITS)) {
+        delete b;
+        return fail(LT_EUNSUPPORTED, "lt_batch_create: %lld macro-steps in one beam-1 wave schedule",
+                    (long long)longest.load());
+      }
       for (int w = 0; w < waves; ++w) wo[(size_t)w + 1] += wo[(size_t)w];
       pc.sched_steps = wo[(size_t)waves];
     }
@@ -1114,7 +1135,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   Carve cv;
   struct PieceOff {
     size_t order, sent_n, node_off, span_off, bp_off, cum_n, span_start, nodes, post, bp, edge_base, edge_val,
-        sched, wave_off;
+        sched, wave_off, place;
   };
   std::vector<PieceOff> po(P);
   for (size_t q = 0; q < P; ++q) {
@@ -1128,7 +1149,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
                      cv.dev(ed ? (size_t)pc.n_nodes * 8 : 0),
                      cv.dev(ed ? (size_t)d->n_edge * (size_t)pc.n_edges * 8 : 0),
                      cv.dev(b->has_sched ? (size_t)std::max<int64_t>(pc.sched_steps, 1) * 64 * 4 : 0),
-                     cv.dev(b->has_sched ? wave_off[q].size() * 8 : 0)};
+                     cv.dev(b->has_sched ? wave_off[q].size() * 8 : 0), cv.dev(place[q].size() * 4)};
   }
   const size_t o_sent_n = cv.dev((size_t)S * 4), o_cum_n = cv.dev(((size_t)S + 1) * 8);
   const size_t o_unk = cv.dev((size_t)d->n_unk * sizeof(NodeRec)),
@@ -1179,6 +1200,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     pc.d_edge_val = d->n_edge > 0 ? at<double>(D, po[q].edge_val) : nullptr;
     pc.d_sched = at<uint32_t>(D, po[q].sched);
     pc.d_wave_off = at<int64_t>(D, po[q].wave_off);
+    pc.d_place = at<uint32_t>(D, po[q].place);
   }
   b->d_sent_n = at<int32_t>(D, o_sent_n);
   b->d_cum_n = at<int64_t>(D, o_cum_n);
@@ -1300,7 +1322,10 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       for (int32_t t = 0; t < d->n_edge; ++t)
         up(pc.d_edge_val + (size_t)t * pc.n_edges, d->edge_val + (size_t)t * d->n_edges + pc.edge0, (size_t)pc.n_edges);
     }
-    if (b->has_sched) up(pc.d_wave_off, wave_off[q].data(), wave_off[q].size());
+    if (b->has_sched) {
+      up(pc.d_wave_off, wave_off[q].data(), wave_off[q].size());
+      up(pc.d_place, place[q].data(), place[q].size());
+    }
   }
   // a beam-1 batch gets its lane schedule now, behind its uploads (a
   // pipeline's upload thread prepares chunk i+1 while chunk i decodes)
@@ -1423,6 +1448,7 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
   p.npost = pc.d_post;
   p.sched = b->has_sched ? pc.d_sched : nullptr;
   p.wave_off = b->has_sched ? pc.d_wave_off : nullptr;
+  p.k1_place = b->has_sched ? pc.d_place : nullptr;
   p.n_edges = pc.n_edges;
   p.edge_base = pc.d_edge_base;
   p.edge_val = pc.d_edge_val;

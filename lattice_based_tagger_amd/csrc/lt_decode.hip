@@ -797,26 +797,26 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 }
 
 // ---------------------------------------------------------------------------
-// beam_size = 1, packed lanes.  A wave owns W sentences and walks their end
-// positions in lockstep; at each position the candidates of all W sentences
-// are packed onto the 64 lanes (one contiguous lane segment per sentence,
-// segment starts from scalar prefix sums), so lanes are not left idle by short
-// positions or finished sentences.  If the candidates exceed the lanes, each
-// segment is shrunk and its lanes take candidates g, g+L, g+2L...
-// Per-sentence argmax: LDS max over an order-preserving 64-bit score key, then
-// LDS min over the generation index among the lanes holding the maximum --
-// exactly the reference's (score desc, generation asc) order.
+// beam_size = 1, packed lanes.  A wave owns W sentences; the lane schedule
+// (k1_schedule) packs the candidates of several sentences' next end positions
+// onto the 64 lanes of each macro-step (one contiguous lane segment per
+// sentence), the sentences advancing independently, so lanes are not left idle
+// by short positions or finished sentences.  Per-sentence argmax: LDS max over
+// an order-preserving 64-bit score key, then LDS min over the generation index
+// among the lanes holding the maximum -- exactly the reference's (score desc,
+// generation asc) order.
 // ---------------------------------------------------------------------------
 #ifndef PK_WAVES
 #define PK_WAVES 4
 #endif
 #ifndef PK_BPL
-// end positions whose backpointer stays in LDS: 87 fills a 4-block CU's LDS
-// (40,928 B per block; 64: 1.010-1.016 ms, 76: 1.000, 87: 0.987-0.995 ms)
-#define PK_BPL 87
+// end positions whose backpointer stays in LDS: 96 fills a CU's LDS with two
+// 8-wave blocks of W = 8 (81,904 B per block; round 2 at W = 6 and 4-wave
+// blocks: window 64: 1.010-1.016 ms, 76: 1.000, 87: 0.987-0.995 ms)
+#define PK_BPL 96
 #endif
 #ifndef PK_WPB
-#define PK_WPB 4
+#define PK_WPB 8                        // (one dense class-3 table and pair table per 8 waves)
 #endif
 #ifndef PK_DMA_AUX
 #define PK_DMA_AUX 2                    // k=1 record DMA nontemporal (streamed once): 0.771 -> 0.766 ms
@@ -830,7 +830,10 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #ifndef PK_SPRE
 #define PK_SPRE 1
 #endif
-constexpr int P_WPB = PK_WPB;           // waves per block
+// waves per block of lt_viterbi_pk: wide keys (more registers, 3 waves per
+// SIMD) in 4-wave blocks, three of which fit a CU
+template <bool NARROW>
+constexpr int k1_wpb() { return NARROW ? PK_WPB : 4; }
 // (k=1 lane-schedule entries: K1_* in lt_internal.h)
 
 // Stage the records of the wave's packed candidates (lane l's node gn, INV =
@@ -881,19 +884,15 @@ struct alignas(16) SentRec {
 // ---------------------------------------------------------------------------
 // The k=1 lane schedule (a static function of the lattice shapes, filled on
 // the device once per batch by lt_k1_sched into memory sized by the host,
-// lt_batch_create): the candidates of the W sentences of a wave at end
-// position e form one list in sentence order, each sentence's in generation
-// order (beam.py:31-42 -- span slot j = 8 - d ascending, i.e. begin ascending;
-// the slot's nodes in bindex order, or its implicit Unknown); macro-step r of
-// e covers list entries [64r, 64r + 64).  Entry of lane l: lt_internal.h K1_*.
+// lt_batch_create): lt_internal.h k1_schedule -- the sentences of a wave
+// advance through their end positions independently, each macro-step packing
+// the candidates of the positions it takes.  Entry of lane l: K1_*.
 // ---------------------------------------------------------------------------
-constexpr int SCH_ROW = 65;                     // LDS row stride (words)
 // The W sentences of wave schedule `wave` (wave-uniform): lengths, first
-// nodes, span-table offsets, the longest length.
+// nodes, span-table offsets, first placement (cum_n: one per end position).
 template <int W>
-__device__ __forceinline__ int k1_wave_sents(const DecodeParams& p, int slot0, int (&nS)[W], uint32_t (&nbS)[W],
-                                             int64_t (&soS)[W]) {
-  int nmax = 0;
+__device__ __forceinline__ void k1_wave_sents(const DecodeParams& p, int slot0, int (&nS)[W], uint32_t (&nbS)[W],
+                                              int64_t (&soS)[W], int64_t (&cnS)[W]) {
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     const bool v = slot0 + w < p.n_sent;
@@ -901,177 +900,247 @@ __device__ __forceinline__ int k1_wave_sents(const DecodeParams& p, int slot0, i
     nS[w] = v ? p.sent_n[sid] : 0;
     nbS[w] = v ? (uint32_t)p.node_off[sid] : 0u;
     soS[w] = v ? p.span_off[sid] : 0;
-    nmax = max(nmax, nS[w]);
+    cnS[w] = v ? p.cum_n[sid] : 0;
   }
-  return nmax;
-}
-// End position e (pos: e <= the wave's longest sentence) of the W sentences:
-// their span starts, and the number of candidates -- a slot's nodes, or its
-// implicit Unknown when it is empty and in range (beam.py:31-38).
-template <int W>
-__device__ __forceinline__ int k1_position(const DecodeParams& p, int e, bool pos, const int (&nS)[W],
-                                           const int64_t (&soS)[W], int (&ss)[W][MAX_SPAN + 1]) {
-  const int dmax = min(e, p.max_len);
-#pragma unroll
-  for (int w = 0; w < W; ++w) {                 // every sentence's loads before any use
-    const bool live = pos && e <= nS[w];
-    const int32_t* const src = p.span_start + soS[w] + (int64_t)(max(e, 1) - 1) * MAX_SPAN;
-#pragma unroll
-    for (int j = 0; j <= MAX_SPAN; ++j) ss[w][j] = live ? src[j] : 0;
-  }
-  int run = 0;
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    const bool live = pos && e <= nS[w];
-#pragma unroll
-    for (int j = 0; j < MAX_SPAN; ++j) {
-      const int c = ss[w][j + 1] - ss[w][j];
-      run += (live && c == 0 && MAX_SPAN - j <= dmax) ? 1 : c;
-    }
-  }
-  return run;
 }
 
-// Macro-steps of every wave schedule of a piece (the count lt_batch_create
-// makes on the host), for a batch that gets its schedule at its first beam-1
-// decode: steps[wave] = sum over its end positions of max(1, ceil(run / 64)).
-template <int W>
-__global__ void __launch_bounds__(64) lt_k1_sched_count(DecodeParams p, int64_t* steps) {
-  const int wave = blockIdx.x;
-  const int lane = (int)threadIdx.x;
-  const int slot0 = wave * W;
-  if (slot0 >= p.n_sent) return;
-  int nS[W];
-  uint32_t nbS[W];
-  int64_t soS[W];
-  const int nmax = k1_wave_sents<W>(p, slot0, nS, nbS, soS);
-  int64_t total = 0;
-  for (int e0 = 1; e0 <= nmax; e0 += 64) {
-    const int e = e0 + lane;
-    const bool pos = e <= nmax;
-    int ss[W][MAX_SPAN + 1];
-    const int run = k1_position<W>(p, e, pos, nS, soS, ss);
-    int rounds = pos ? max(1, (run + 63) >> 6) : 0;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) rounds += __shfl_xor(rounds, o);
-    total += rounds;
-  }
-  if (lane == 0) steps[wave] = total;
-}
+constexpr int K1_NCAP = 192;                    // end positions per sentence whose counts the schedule kernel keeps in LDS
+constexpr int K1_RT = 16;                       // schedule rows per LDS tile of the fill
 
-// One wave per wave schedule, a lane pair per end position (32 positions per
-// chunk; the even lane takes sentences 0 .. H-1, the odd one H .. W-1): every
-// lane loads its position's span starts of its sentences and counts their
-// candidates at once, the pair adds its counts (run), a wave prefix sum of the
-// macro-steps (max(1, ceil(run / 64))) places each position's rows, and each
-// lane writes its entries in generation order into the position's row of an
-// LDS tile (32 rows, stride 65 words), the odd lane behind the even one's;
-// each row is copied out by one coalesced 256 B store.  A position with more
-// than 64 entries (dense lattices) writes its further rows directly.
+// The schedule of a wave on the device, k1_schedule's rule with a lane per
+// sentence (lane w < W: sentence w's positions left, next end position, its
+// candidate count): priority ranks by one readlane and compare per sentence,
+// the greedy pass over the ranks on wave-uniform values.  The candidate counts
+// of end positions e <= K1_NCAP are counted lane-parallel into LDS first,
+// those of later positions (long sentences) from the span table when needed.
+// Every (sentence, end position) gets its placement -- first macro-step |
+// first lane << K1_TBITS -- at p.k1_place[cum_n + e - 1].  Returns the
+// macro-steps.  (The host does the same at lt_batch_create, k1_schedule; this
+// runs for a batch that gets its schedule at its first beam-1 decode.)
 template <int W>
-__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
-  static_assert(W < 8, "the sentence field holds W - 1");
-  constexpr int H = (W + 1) / 2;                // sentences per lane of a pair
-  __shared__ uint32_t rows[32 * SCH_ROW];
-  const int wave = blockIdx.x;
+__device__ __forceinline__ int64_t k1_lane_schedule(const DecodeParams& p, const int (&nS)[W], const int64_t (&soS)[W],
+                                                    const int64_t (&cnS)[W], uint16_t (*runs)[K1_NCAP]) {
+  static_assert(W == K1_W && W <= 8, "one schedule layout, the priority key holds the sentence in 3 bits");
   const int lane = (int)threadIdx.x;
-  const int slot0 = wave * W;
-  if (slot0 >= p.n_sent) return;
-  int nS[W];
-  uint32_t nbS[W];
-  int64_t soS[W];
-  const int nmax = k1_wave_sents<W>(p, slot0, nS, nbS, soS);
-  const int part = lane & 1, pl = lane >> 1;
-  // this lane's sentences w = part * H + u
-  int nU[H];
-  uint32_t nbU[H];
-  int64_t soU[H];
+  // the (sentence, position) pairs flattened, four per lane in flight
+  int pre[W + 1];
+  pre[0] = 0;
 #pragma unroll
-  for (int u = 0; u < H; ++u) {
-    const bool hi = part && H + u < W;
-    nU[u] = part ? (hi ? nS[(H + u) % W] : 0) : nS[u];
-    nbU[u] = hi ? nbS[(H + u) % W] : nbS[u];
-    soU[u] = hi ? soS[(H + u) % W] : soS[u];
-  }
-  // the wave's schedule rows as a buffer (stores past its rows are dropped)
-  const int64_t w0 = wave_off[wave];
-  const rsrc_t out = make_rsrc(sched + w0 * 64, (uint64_t)(wave_off[wave + 1] - w0) * 256u);
-  uint32_t* const myrow = rows + pl * SCH_ROW;
-  int base = 0;                                 // rows of the chunks before
-  for (int e0 = 1; e0 <= nmax; e0 += 32) {
-    const int e = e0 + pl;
-    const bool pos = e <= nmax;
-    const int dmax = min(e, p.max_len);
-    int ss[H][MAX_SPAN + 1];
-    const int own = k1_position<H>(p, e, pos, nU, soU, ss);
-    const int other = __shfl_xor(own, 1);
-    const int run = own + other;                // the position's candidates
-    const int rounds = pos ? max(1, (run + 63) >> 6) : 0;
-    int incl = part ? 0 : rounds;               // inclusive prefix over the positions (even lanes)
+  for (int w = 0; w < W; ++w) pre[w + 1] = pre[w] + min(nS[w], K1_NCAP);
+  constexpr int U = 4;
+  for (int i0 = 0; i0 < pre[W]; i0 += 64 * U) {
+    int c[U], wu[U], eu[U];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(incl, (unsigned)o);
-      incl += lane >= o ? t : 0;
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 64 * u + lane;
+      int w = 0;
+#pragma unroll
+      for (int v = 1; v < W; ++v) w += i >= pre[v] ? 1 : 0;
+      int64_t so = soS[0];
+      int pw = 0;
+#pragma unroll
+      for (int v = 1; v < W; ++v)
+        if (w == v) { so = soS[v]; pw = pre[v]; }
+      wu[u] = w;
+      eu[u] = i - pw + 1;
+      c[u] = i < pre[W] ? k1_candidates(p.span_start + so, eu[u], p.max_len) : 0;
     }
-    const int off = base + incl - rounds;       // the position's first row (both lanes of the pair)
-    const int total = __shfl(incl, 63);
-    // entries in generation order (sentence, span slot = begin ascending,
-    // the slot's nodes): the first 64 into the position's LDS row (row 0;
-    // the copy below adds K1_FIRST and the idle entries past run), the rest
-    // (dense lattices) straight to the position's later rows
-    int q = part ? other : 0;
 #pragma unroll
-    for (int u = 0; u < H; ++u) {
-      const bool live = pos && e <= nU[u];
-      const uint32_t wb = (uint32_t)(part * H + u) << 26;
+    for (int u = 0; u < U; ++u)
+      if (i0 + 64 * u + lane < pre[W]) runs[wu[u]][eu[u] - 1] = (uint16_t)min(c[u], 65535);
+  }
+  __builtin_amdgcn_wave_barrier();               // (one wave: its LDS operations complete in order)
+  asm volatile("" ::: "memory");
+  // lane w's sentence
+  int n = 0;
+  int64_t so = 0, cn = 0;
 #pragma unroll
-      for (int j = 0; j < MAX_SPAN; ++j) {
-        const int a = ss[u][j];
-        const bool unk = live && a == ss[u][j + 1] && MAX_SPAN - j <= dmax;
-        const int c = live ? (unk ? 1 : ss[u][j + 1] - a) : 0;
-        // entry i: node nbU[u] + a + i, or the slot's implicit Unknown (d - 1 = 7 - j)
-        const uint32_t e0v = (unk ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - j)) : nbU[u] + (uint32_t)a) | wb;
-        const int n1 = min(c, max(64 - q, 0));
-        int i = 0;
-#pragma unroll 1
-        for (; i < n1; ++i) myrow[q + i] = e0v + (uint32_t)i;
-#pragma unroll 1
-        for (; i < c; ++i) __builtin_amdgcn_raw_buffer_store_b32(e0v + (uint32_t)i, out, (uint32_t)(off * 256 + (q + i) * 4), 0, 0);
-        q += c;
+  for (int w = 0; w < W; ++w)
+    if (lane == w) { n = nS[w]; so = soS[w]; cn = cnS[w]; }
+  auto run_at = [&](int e) -> int {              // (e <= n; 65535: a count too large for the LDS copy)
+    const int x = e <= K1_NCAP ? (int)runs[lane < W ? lane : 0][e - 1] : 65535;
+    return x < 65535 ? x : k1_candidates(p.span_start + so, e, p.max_len);
+  };
+  int rem = n, pos = 1;
+  int run = rem > 0 ? run_at(1) : 0;
+  int64_t t = 0;
+  for (;;) {
+    const int key = rem > 0 ? rem * 8 + (7 - lane) : -1;   // priority: positions left, then the lower index
+    int rank = 0;
+#pragma unroll
+    for (int v = 0; v < W; ++v) rank += __builtin_amdgcn_readlane(key, v) > key ? 1 : 0;
+    if (__builtin_amdgcn_ballot_w64(key >= 0) == 0ull) return t;
+    uint32_t take = 0;
+    int room = 64, steps = 1, off = 0;
+#pragma unroll
+    for (int r = 0; r < W && room > 0; ++r) {
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(key >= 0 && rank == r);
+      if (m == 0ull) break;                      // (ranks 0 .. live - 1)
+      const int w = __builtin_ctzll(m);
+      const int rw = __builtin_amdgcn_readlane(run, w);
+      if (rw > 64) {
+        if (r == 0) {                            // a dense position, alone
+          take = 1u << w;
+          steps = (rw + 63) >> 6;
+          room = 0;
+        }
+      } else if (rw <= room) {
+        take |= 1u << w;
+        off = lane == w ? 64 - room : off;
+        room -= rw;
       }
     }
-    if (part) {
+    const bool mine = lane < W && ((take >> lane) & 1u);   // (a shift by 32 or more is not a zero)
+    if (mine) p.k1_place[cn + pos - 1] = (uint32_t)t | ((uint32_t)off << K1_TBITS);
+    t += steps;
+    if (mine) {
+      ++pos;
+      --rem;
+      run = rem > 0 ? run_at(pos) : 0;
+    }
+  }
+}
+
+// The macro-steps and placements of every wave schedule of a piece, for a
+// batch that gets its schedule at its first beam-1 decode (lt_batch_create
+// counts and places on the host for a beam-1 batch).
+template <int W>
+__global__ void __launch_bounds__(64) lt_k1_sched_count(DecodeParams p, int64_t* steps) {
+  __shared__ uint16_t runs[W][K1_NCAP];
+  const int wave = blockIdx.x;
+  const int slot0 = wave * W;
+  if (slot0 >= p.n_sent) return;
+  int nS[W];
+  uint32_t nbS[W];
+  int64_t soS[W], cnS[W];
+  k1_wave_sents<W>(p, slot0, nS, nbS, soS, cnS);
+  const int64_t total = k1_lane_schedule<W>(p, nS, soS, cnS, runs);
+  if (threadIdx.x == 0) steps[wave] = total;
+}
+
+// The schedule fill: one wave per wave schedule, its rows built K1_RT at a
+// time in an LDS tile -- idle entries, then the entries of the positions
+// placed in it (lanes over (sentence, position) pairs: the placement and the
+// position's span starts loaded together) -- and copied out by coalesced
+// 256 B stores.  A sentence's positions are placed in increasing macro-steps,
+// so a cursor per sentence (its first position not yet complete) bounds the
+// positions a tile can hold: at most one per macro-step, K1_RT.
+template <int W>
+__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
+  __shared__ uint32_t tile[K1_RT][64];
+  __shared__ int curs[W];
+  const int wave = blockIdx.x;
+  const int lane = (int)threadIdx.x;
+  const int slot0 = wave * W;
+  if (slot0 >= p.n_sent) return;
+  int nS[W];
+  uint32_t nbS[W];
+  int64_t soS[W], cnS[W];
+  k1_wave_sents<W>(p, slot0, nS, nbS, soS, cnS);
+  if (lane < W) curs[lane] = 1;
+  // the wave's rows as a buffer (stores past its rows are dropped)
+  const int64_t w0 = wave_off[wave];
+  const int nrow = (int)(wave_off[wave + 1] - w0);
+  const rsrc_t out = make_rsrc(sched + w0 * 64, (uint64_t)nrow * 256u);
+  // lane (sentence g, slot j8) of an 8 x 8 pass over (sentence, position) pairs
+  const int g = lane >> 3, j8 = lane & 7;
+  int ng = 0;
+  uint32_t nbg = 0;
+  int64_t sog = 0, cng = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (g == w) { ng = nS[w]; nbg = nbS[w]; sog = soS[w]; cng = cnS[w]; }
+  const uint32_t wb = (uint32_t)g << 26;
+  static_assert(K1_RT == 16, "two positions per lane per tile");
+  for (int R0 = 0; R0 < nrow; R0 += K1_RT) {
+#pragma unroll
+    for (int r = 0; r < K1_RT; ++r) tile[r][lane] = K1_IDLE;
+    const int cur = g < W ? curs[g] : 1;
+    // positions cur + j8 and cur + 8 + j8: placements and span starts together
+    int ss[2][MAX_SPAN + 1], t0[2], q0[2];
+    bool in[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = cur + 8 * h + j8;
+      in[h] = g < W && e <= ng;
+      const uint32_t v = in[h] ? p.k1_place[cng + e - 1] : 0u;
+      const int32_t* const src = p.span_start + sog + (int64_t)(max(e, 1) - 1) * MAX_SPAN;
+#pragma unroll
+      for (int jj = 0; jj <= MAX_SPAN; ++jj) ss[h][jj] = in[h] ? src[jj] : 0;
+      t0[h] = (int)(v & ((1u << K1_TBITS) - 1u));
+      in[h] = in[h] && t0[h] < R0 + K1_RT;
+      q0[h] = (int)(v >> K1_TBITS);
+    }
+    int done = 0;                                // positions of sentence g completed in this tile
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = cur + 8 * h + j8;
+      int q = q0[h];
+      int last = t0[h];                          // the position's last row
+      if (in[h]) {
+        const int dmax = min(e, p.max_len);
+        int cnt[MAX_SPAN];
+        uint32_t e0v[MAX_SPAN];
+        int run = 0;
+#pragma unroll
+        for (int jj = 0; jj < MAX_SPAN; ++jj) {
+          const int a = ss[h][jj];
+          const bool unk = a == ss[h][jj + 1] && MAX_SPAN - jj <= dmax;
+          cnt[jj] = unk ? 1 : ss[h][jj + 1] - a;
+          // entry i: node nbg + a + i, or the slot's implicit Unknown (d - 1 = 7 - jj)
+          e0v[jj] = (unk ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - jj)) : nbg + (uint32_t)a) | wb;
+          run += cnt[jj];
+        }
+        if (run <= 64) {
+          // the usual position: one segment of its first row (t0 is in this tile)
+          uint32_t* const rowp = &tile[t0[h] - R0][0];
+#pragma unroll
+          for (int jj = 0; jj < MAX_SPAN; ++jj) {
 #pragma unroll 1
-      for (int r = max(q, 64); r < rounds * 64; ++r)   // the rest of a dense position's last row
-        __builtin_amdgcn_raw_buffer_store_b32(K1_IDLE, out, (uint32_t)(off * 256 + r * 4), 0, 0);
+            for (int i = 0; i < cnt[jj]; ++i) rowp[q + i] = (e0v[jj] + (uint32_t)i) | K1_FIRST;
+            q += cnt[jj];
+          }
+        } else {
+          // a dense position: rows t0, t0 + 1, ..., of which this tile's
+#pragma unroll
+          for (int jj = 0; jj < MAX_SPAN; ++jj) {
+#pragma unroll 1
+            for (int i = 0; i < cnt[jj]; ++i, ++q) {
+              const int row = t0[h] + (q >> 6) - R0;
+              if (row >= 0 && row < K1_RT) tile[row][q & 63] = (e0v[jj] + (uint32_t)i) | (q < 64 ? K1_FIRST : 0u);
+            }
+          }
+        }
+        last = t0[h] + ((q - 1) >> 6);
+      }
+      const bool complete = in[h] && last < R0 + K1_RT;
+      const unsigned long long cm = __builtin_amdgcn_ballot_w64(complete);
+      done += __builtin_popcount((uint32_t)(cm >> (g * 8)) & 0xFFu);
     }
-    // (one wave: its LDS operations complete in issue order)
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    unsigned long long live_rows = __ballot(pos && !part);
-    while (live_rows) {                         // row 0 of every position, coalesced
-      const int pp = __builtin_ctzll(live_rows);
-      live_rows &= live_rows - 1ull;
-      const int offp = __builtin_amdgcn_readlane(off, pp), runp = __builtin_amdgcn_readlane(run, pp);
-      const uint32_t v = lane < runp ? rows[(pp >> 1) * SCH_ROW + lane] : K1_IDLE;
-      __builtin_amdgcn_raw_buffer_store_b32(v | K1_FIRST, out, (uint32_t)lane * 4u, offp * 256, 0);
-    }
+    if (j8 == 0 && g < W) curs[g] = cur + done;
+    const int nr = min(K1_RT, nrow - R0);
+#pragma unroll
+    for (int r = 0; r < K1_RT; ++r)
+      if (r < nr) __builtin_amdgcn_raw_buffer_store_b32(tile[r][lane], out, (uint32_t)lane * 4u, (R0 + r) * 256, 0);
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    base += total;
   }
 }
 
 template <int W, bool NARROW, bool COUNT>
-__global__ void __launch_bounds__(64 * P_WPB, (NARROW && W <= 8) ? PK_WAVES : 3)
+__global__ void __launch_bounds__(64 * k1_wpb<NARROW>(), (NARROW && W <= 8) ? PK_WAVES : 3)
 lt_viterbi_pk(DecodeParams p) {
   constexpr int BPL = PK_BPL;                   // end positions whose backpointer stays in LDS
+  constexpr int P_WPB = k1_wpb<NARROW>();
   __shared__ VEntry ring[P_WPB][W][RING];
   __shared__ uint32_t bpl[P_WPB][W][BPL];
   __shared__ uint4 stg[P_WPB][REC_CHUNKS * 64];
   __shared__ SentRec srec[P_WPB][W];
   __shared__ unsigned long long amax[P_WPB][2][W];
   __shared__ uint32_t amin[P_WPB][2][W];
+  __shared__ uint32_t sep[P_WPB][W];            // sentence w's current end position e | (e % RING) << 24
   __shared__ double d3l[D3_DIM * D3_DIM];
   __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records (as staged ones)
   __shared__ F46 pxl[MAX_PAIRS];                // the batch's class-4/6 pair table
@@ -1080,7 +1149,7 @@ lt_viterbi_pk(DecodeParams p) {
   // is sized to the last byte of it
   static_assert(!(NARROW && W <= 8) ||
                     (sizeof(ring) + sizeof(bpl) + sizeof(stg) + sizeof(srec) + sizeof(amax) + sizeof(amin) +
-                     sizeof(d3l) + sizeof(ucan) + sizeof(pxl)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
+                     sizeof(sep) + sizeof(d3l) + sizeof(ucan) + sizeof(pxl)) * (4 * PK_WAVES / P_WPB) <= 160u * 1024u,
                 "lt_viterbi_pk LDS exceeds the CU's share for PK_WAVES waves per SIMD");
   for (int i = (int)threadIdx.x; i < p.n_pairs; i += 64 * P_WPB) pxl[i] = p.pairs[i];
   stage_unk(p, ucan);                           // (its barrier publishes pxl too)
@@ -1095,6 +1164,11 @@ lt_viterbi_pk(DecodeParams p) {
   const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
   const int bstride = p.bp_stride;
+  // backpointers past the LDS window (long sentences) as a buffer: every
+  // macro-step issues exactly one store instruction (non-writer lanes: an
+  // out-of-range offset, dropped), so the wait at the top of the next step
+  // leaves it in flight
+  const rsrc_t bpr = make_rsrc(p.bp, (uint64_t)p.bp_bytes);
   uint4* const wst = stg[wv];
   VEntry (*const R)[RING] = ring[wv];
   Counts cnt;
@@ -1121,6 +1195,7 @@ lt_viterbi_pk(DecodeParams p) {
   if (lane < W) {
     amax[wv][0][lane] = 0ull; amax[wv][1][lane] = 0ull;
     amin[wv][0][lane] = INV; amin[wv][1][lane] = INV;
+    sep[wv][lane] = 0u;
   }
   // this wave's macro-steps in the lane schedule
   const int64_t soff = p.wave_off[wave];
@@ -1132,25 +1207,36 @@ lt_viterbi_pk(DecodeParams p) {
   };
   uint32_t ent = nsteps > 0 ? sch[0] : K1_IDLE;   // (a wave of empty sentences has no step)
   dma_packed(B, node_of(ent), wst, lane);
+  __builtin_amdgcn_raw_buffer_store_b32(0u, bpr, OOB, 0, 0);      // the invariant's first store
+  __builtin_amdgcn_wave_barrier();
 
-  int e = 0, em9 = 0;
   for (int t = 0; t < nsteps; ++t) {
     PK_STAMP(0);                                 // [0] loop bookkeeping of the previous step
-    __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): staged records, this step's schedule
+    // vmcnt(1): staged records, this step's schedule entry (VMEM operations
+    // retire in order; the one younger operation is the previous step's
+    // backpointer store)
+    __builtin_amdgcn_s_waitcnt(0x0F71);
     PK_STAMP(1);                                 // [1] wait for the staged records
     // the next macro-step's schedule entry: arrives under this step's probes
     const uint32_t ent1 = t + 1 < nsteps ? sch[(int64_t)(t + 1) * 64] : K1_IDLE;
-    const bool first = (__builtin_amdgcn_readfirstlane(ent) & K1_FIRST) != 0;   // a new end position
-    if (first) {
-      ++e;
-      em9 = em9 == RING - 1 ? 0 : em9 + 1;
-    }
-    const int dmax = min(e, p.max_len);
-    const int cb = e & 1;
     const uint32_t gn0 = node_of(ent);
     const bool imp = (ent & K1_UNK) != 0;        // an implicit Unknown (its record from ucan)
     const bool act = gn0 != INV || imp;
-    const int msr = act ? (int)((ent >> 26) & 7u) : 0;
+    const int msr = (int)((ent >> 26) & 7u);     // (0 for an idle lane)
+    // the lane's sentence's end position: it moves to the next one at the
+    // first macro-step of that position (every lane of the segment writes the
+    // same value; a wave's LDS operations complete in order)
+    const bool first = (ent & K1_FIRST) != 0;
+    const uint32_t sp0 = sep[wv][msr];
+    int e = (int)(sp0 & 0xFFFFFFu), em9 = (int)(sp0 >> 24);
+    if (first) {
+      ++e;
+      em9 = em9 == RING - 1 ? 0 : em9 + 1;
+      sep[wv][msr] = (uint32_t)e | ((uint32_t)em9 << 24);
+    }
+    const uint32_t spo = lane < W ? sep[wv][lane] : 0u;   // (owner lanes: their sentence's, updated)
+    const int dmax = min(e, p.max_len);
+    const int cb = e & 1;
     // this lane's candidate: its staged record, or the implicit Unknown's
     const Cand cur = cand_lds32(imp ? ucan + 2u * (ent & 7u) : wst + 2 * lane, 1, pxl, B, imp ? INV : gn0);
     const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
@@ -1211,21 +1297,21 @@ lt_viterbi_pk(DecodeParams p) {
     if (top && mk != mprev) amin[wv][cb][msr] = INV;
     if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], gk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t mgw = top ? amin[wv][cb][msr] : INV;
-    if (lane < W) {                              // reset the other parity for the next position
-      amax[wv][cb ^ 1][lane] = 0ull;
-      amin[wv][cb ^ 1][lane] = INV;
+    if (lane < W) {                              // reset the other parity for the sentence's next position
+      const int cbo = (int)(spo & 1u) ^ 1;
+      amax[wv][cbo][lane] = 0ull;
+      amin[wv][cbo][lane] = INV;
     }
+    uint32_t bpv = 0u, bpoff = OOB;
     if (top && mgw == gk) {                      // the (step's) winner writes beam[e]
       const SentRec si = srec[wv][msr];
       const uint32_t local = imp ? UNK_LOCAL : gn0 - si.nbase;
       R[msr][em9] = v_grow<COUNT>(h1, cur, best_s, local);   // Sequence.add (beam.py:112-116)
-      const uint32_t bpv = bp_pack(local, (uint32_t)d0, 0u);
-      if (e < BPL) {
-        bpl[wv][msr][e] = bpv;
-      } else {                                   // positions past the LDS window (long sentences)
-        p.bp[(((int64_t)si.bp_hi << 32) | si.bp_lo) + (int64_t)e * bstride] = bpv;
-      }
+      bpv = bp_pack(local, (uint32_t)d0, 0u);
+      if (e < BPL) bpl[wv][msr][e] = bpv;
+      else bpoff = (uint32_t)(((((int64_t)si.bp_hi << 32) | si.bp_lo) + (int64_t)e * bstride) * 4);   // past the window
     }
+    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, bpoff, 0, 0);
     __builtin_amdgcn_wave_barrier();
     PK_STAMP(7);                                 // [7] argmax (LDS atomics), ring + backpointer write
 #ifdef PK_PHASES
@@ -1325,6 +1411,7 @@ static_assert(P_W <= 8, "k=1 schedule entries hold the sentence in 3 bits");
 
 template <int W, bool NARROW, bool COUNT>
 hipError_t launch_pk(const DecodeParams& p, const Launch& L) {
+  constexpr int P_WPB = k1_wpb<NARROW>();
   constexpr int SPB = W * P_WPB;
   const int blocks = (p.n_sent + SPB - 1) / SPB;
   if (blocks == 0) return hipSuccess;

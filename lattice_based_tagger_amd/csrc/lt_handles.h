@@ -57,6 +57,7 @@ struct lt_piece {
   // device by the fill kernel, lt_batch_create or the first beam-1 decode)
   uint32_t* d_sched = nullptr;                   // [sched_steps * 64]
   int64_t* d_wave_off = nullptr;                 // [waves + 1]
+  uint32_t* d_place = nullptr;                   // [piece chars] k=1 placements (DecodeParams.k1_place)
   int64_t sched_steps = 0;
   int64_t* d_edge_base = nullptr;                // [n_nodes], rebased to the piece
   double* d_edge_val = nullptr;                  // [n_edge][n_edges]

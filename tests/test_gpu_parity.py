@@ -187,6 +187,36 @@ def test_long_sentences_cross_the_lds_backpointer_window(gpu_decoder):
     assert np.array_equal(codes, o[3])
 
 
+@pytest.mark.parametrize('case', ['long', 'dense', 'long_lazy', 'dense_lazy'])
+def test_k1_schedule_long_and_dense(gpu_decoder, case):
+    """The k=1 lane schedule (lt_internal.h k1_schedule): sentences advance
+    independently, several end positions per macro-step.  'long': 90-eojeol
+    sentences (about 300 characters) -- positions past the schedule kernels'
+    LDS counts (K1_NCAP = 192: counts from the span table, placements in the
+    backpointer rows) and past the kernel's LDS backpointer window; 'dense':
+    about 64 candidates per end position, so positions above 64 candidates
+    take several macro-steps alone.  '_lazy': the batch is created for beam 5
+    and decoded at beam 1 (schedule counted on the device).  Byte-equal to
+    the C restatement."""
+    if case.startswith('long'):
+        packed, keys, coefs = _synthetic(600, seed=5151, n_features=100_000, eojeols=90)
+        assert int(packed.sent_n.max()) > 192
+    else:
+        packed, keys, coefs = _synthetic(300, seed=5252, n_features=100_000, eojeols=6,
+                                         extra_lambda=45.0, dup_rate=0.4)
+    dm = _capi.DeviceModel(gpu_decoder.ctx, keys, coefs)
+    db = _capi.DeviceBatch(gpu_decoder.ctx, packed, max_k=5 if case.endswith('lazy') else 1)
+    try:
+        count, length, score, codes = db.decode(dm, 1)
+    finally:
+        db.close()
+        dm.close()
+    o = lt_oracle.decode(packed, keys, coefs, 1, nthreads=16)
+    assert np.array_equal(count, o[0]) and np.array_equal(length, o[1])
+    assert np.array_equal(score.view(np.uint64), o[2].view(np.uint64))
+    assert np.array_equal(codes, o[3])
+
+
 def test_full_size_properties(gpu_decoder):
     """64K sentences, k=16: deterministic, sorted, and every path is a chain of
     spans from 0 to n made of the sentence's own nodes."""
