@@ -2041,7 +2041,9 @@ hipError_t launch_bp(const DecodeParams& p, const Launch& L) {
 // pruning, per group.
 // ---------------------------------------------------------------------------
 template <int KT, int G, int WPB, bool NARROW>
-__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu((G == 16 && KT > 2) ? 2 : 3, 3)))
+// (wide keys at KT = 4, G = 32: 3 waves per SIMD would spill 4 VGPRs -- 2)
+__global__ void __launch_bounds__(64 * WPB)
+__attribute__((amdgpu_waves_per_eu(((G == 16 && KT > 2) || (!NARROW && KT == 4)) ? 2 : 3, 3)))
 lt_beam_hw(DecodeParams p) {
   constexpr int S = 64 / G;                     // sentences per wave, one per lane group
   constexpr int RPC = 2;                        // scoring rounds (of G) per chunk

@@ -18,10 +18,16 @@ echo SMOKE_OK
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider \
   > $O/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -60 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
+# the profile set first: its PMC traffic summary goes where bench.py reads it
+# (profiles/<TAG>_traffic.json), so the default line below carries this
+# build's fabric bytes
+cd $R && TAG=$TAG bash tools/gpu_prof.sh || exit 1
+cp $R/gpurun_out/prof_$TAG/traffic.json $R/profiles/${TAG}_traffic.json
+cp $R/gpurun_out/prof_$TAG/traffic.json $O/traffic.json
+cd $R
 timeout -k 10 600 python3 -u bench.py > $O/bench_default.log 2>&1 || { echo BENCH_FAIL; tail -30 $O/bench_default.log; exit 1; }
 tail -1 $O/bench_default.log > $O/bench_default.jsonl
-python3 -c "import json;d=json.load(open('$O/bench_default.jsonl'));r=d['roofline'];print('k=1', round(d['value']), 'sents/s kernel_ms', round(r['avg_kernel_ms'],4), 'frac', round(r['frac'],4), 'fresh_ms', d['fresh_batch']['ms_per_step'], {k: (v['avg_kernel_ms'], v['value']) for k, v in d['extra'].items()})"
-cd $R && TAG=$TAG bash tools/gpu_prof.sh || exit 1
+python3 -c "import json;d=json.load(open('$O/bench_default.jsonl'));r=d['roofline'];print('k=1', round(d['value']), 'sents/s kernel_ms', round(r['avg_kernel_ms'],4), 'frac', round(r['frac'],4), 'traffic', r['traffic'], 'fresh_ms', d['fresh_batch']['ms_per_step'], {k: (v['avg_kernel_ms'], v['value']) for k, v in d['extra'].items()})"
 cd $R && bash tools/gpu_tagger_e2e.sh || exit 1
 for K in 1 5; do tail -1 $R/gpurun_out/bench_tagger_k$K.log > $O/tagger_e2e_k$K.jsonl; done
 echo EVIDENCE_OK
