@@ -185,7 +185,7 @@ def algorithmic_bytes(piece, n_dict, tuples, length, count, k):
     return 32 * n_dict + int(np.sum(8 * (8 * n + 1) + 4 * 8 * n)) + 24 * tuples + 8 * T * n_dict + out
 
 
-PK_BPL = 87                    # k=1: end positions whose backpointers stay in LDS (lt_decode.hip)
+PK_BPL = 96                    # k=1: end positions whose backpointers stay in LDS (lt_decode.hip)
 
 
 def must_move_loads(table_loads, k):
