@@ -195,12 +195,14 @@ typedef struct {
  * Device preparation: the beam-1 decoder reads a lane schedule (which
  * candidate each lane scores at each step), a function of the lattice shapes
  * alone.  A batch created with max_k = 1 (and max_len <= LT_MAX_SPAN) gets
- * one: its size is counted here on the host, its memory is part of the
- * batch's allocation, and it is built on the device by a kernel on the upload
- * stream (after lt_batch_reset_prep: queued on the decode stream in front of
- * the next decode).  Neither blocks nor allocates.  A batch created for
- * larger beams gets none here (no host counting, no arena bytes); its first
- * beam-1 decode builds one: the macro-steps counted on the device, one host
+ * one: the schedule's steps and every (sentence, end position)'s placement
+ * are computed here on the host (4 bytes per character, uploaded with the
+ * batch), its memory is part of the batch's allocation, and its rows are
+ * built on the device by a kernel on the upload stream (after
+ * lt_batch_reset_prep: queued on the decode stream in front of the next
+ * decode).  Neither blocks nor allocates.  A batch created for larger beams
+ * gets none here (no host work, no arena bytes); its first beam-1 decode
+ * builds one: steps and placements computed on the device, one host
  * synchronisation, buffers of its own (freed with the batch). */
 lt_status lt_batch_create(lt_ctx* ctx, const lt_batch_desc* desc, int max_k, lt_batch** out);
 lt_status lt_batch_destroy(lt_batch* batch);
