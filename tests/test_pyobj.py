@@ -69,3 +69,24 @@ def test_refusals(ext):
     with pytest.raises(TypeError):
         ext.words(dict, out, np.zeros(0, np.int64), ([],) * 5, (np.zeros(0, np.int32),) * 5,
                   (np.zeros(0, np.int64),) * 3 + (np.zeros(0, np.uint8),))
+
+
+def test_words_untracked_by_cyclic_gc(ext):
+    """Words of str / int / bool / None cannot form cycles; CPython never
+    untracks tuple subclasses by itself, so `_ltpy` does (a full collection
+    after a 64K-sentence call otherwise walks 1-2 million of them)."""
+    import gc
+    uniq = (['가'], ['가'], ['이'], ['Noun'], ['Josa'])
+    codes = tuple(np.zeros(3, np.int32) for _ in uniq)
+    ints = (np.ones(3, np.int64), np.zeros(3, np.int64), np.ones(3, np.int64), np.zeros(3, np.uint8))
+    out = [None] * 3
+    ext.words(Word, out, np.arange(3, dtype=np.int64), uniq, codes, ints)
+    assert not any(gc.is_tracked(w) for w in out)
+    # a container field keeps the Word tracked
+    uniq_c = (['가'], ['가'], [['x']], ['Noun'], ['Josa'])
+    ext.words(Word, out, np.arange(3, dtype=np.int64), uniq_c, codes, ints)
+    assert all(gc.is_tracked(w) for w in out)
+    unk = [None] * 2
+    ext.unknowns(Word, unk, np.arange(2, dtype=np.int64), ['가나다'], np.zeros(2, np.int64),
+                 np.array([0, 1], np.int64), np.array([1, 2], np.int64), Unk)
+    assert not any(gc.is_tracked(w) for w in unk) and unk[1].word == '나다'
