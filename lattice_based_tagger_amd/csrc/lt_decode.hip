@@ -63,6 +63,19 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* ptr, uint64_t bytes) {
   const uint32_t nr = bytes >= 0x80000000ull ? 0x7FFFFFFFu : (uint32_t)bytes;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, (int)nr, 0x00020000);
 }
+// make_rsrc for a resource used inside a loop: its base and size pass
+// through an empty asm, so the compiler cannot re-derive them from the kernel
+// argument.  The argument load is merged with its neighbours (one 16-dword
+// s_load of the result pointers).  Under SGPR pressure that tuple is spilled
+// and restored whole, 16 v_readlane, at every use.  Opaque, the base and the
+// size are three SGPRs of their own.  (lt_beam_hw's backpointer store:
+// k=5 4.099 -> 4.057 ms, k=2 2.120 -> 2.091 ms, profiles/r05/ab_bp_opaque/.)
+__device__ __forceinline__ rsrc_t make_rsrc_own(const void* ptr, uint64_t bytes) {
+  uint64_t base = (uint64_t)(uintptr_t)ptr;
+  uint32_t nr = bytes >= 0x80000000ull ? 0x7FFFFFFFu : (uint32_t)bytes;
+  asm volatile("" : "+s"(base), "+s"(nr));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)base, (short)0, (int)nr, 0x00020000);
+}
 __device__ __forceinline__ u32x4 ld128(rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
@@ -2109,7 +2122,7 @@ lt_beam_hw(DecodeParams p) {
     nbS[h] = (uint32_t)__builtin_amdgcn_readlane((int)nbase, h * G);
     nS[h] = __builtin_amdgcn_readlane(n, h * G);
   }
-  const rsrc_t bpr = make_rsrc(p.bp, (uint64_t)p.bp_bytes);
+  const rsrc_t bpr = make_rsrc_own(p.bp, (uint64_t)p.bp_bytes);
   VEntry (*const R)[KT] = ring[wv][hf];
   int32_t* const cnt9 = cntl[wv][hf];
   unsigned long long* const LK = lkey[wv][hf];
