@@ -1,7 +1,7 @@
 """Decode launches of the bench workload for counter passes (rocprofv3 --pmc):
-the 64K config-3 batch is generated once and cached as .npz (in --cache),
-then: one counting launch (lt_count_ops), --warmup and --steps decodes with
-the result copy, as bench.py's step.  Prints one JSON line with the kernel
+the 64K config-3 batch (bench.make_workload), then one counting launch
+(lt_count_ops), --warmup and --steps decodes with the result copy, as
+bench.py's step.  Prints one JSON line with the kernel
 name and the dispatch count, so a counter table can be read per dispatch.
 
     python tools/prof_decode.py --k 1 [--steps 3] [--cache /tmp/ltw]
@@ -15,26 +15,15 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-
 from lattice_based_tagger_amd import _capi  # noqa: E402
-from lattice_based_tagger_amd.packer import PackedBatch  # noqa: E402
-
-FIELDS = ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start', 'node_word', 'node_morph0',
-          'node_tag', 'node_mask', 'node_pre', 'node_f4', 'node_f5', 'node_f6')
 
 
-def workload(cache, sentences, seed):
-    path = os.path.join(cache, 'w_%d_%d.npz' % (sentences, seed))
-    if os.path.exists(path):
-        z = np.load(path)
-        packed = PackedBatch(max_len=8, n_post=0, has_trigram=1, node_post=np.zeros((0, len(z['node_word']))),
-                             **{f: z[f] for f in FIELDS})
-        return packed, z['keys'], z['coefs']
+def workload(sentences, seed):
+    """The bench batch (bench.make_workload), generated in this process (a
+    cache of selected PackedBatch fields went stale when the batch gained
+    implicit-Unknown records)."""
     import bench
     _, _, _, packed, keys, coefs = bench.make_workload(sentences, seed, 1_000_000)
-    os.makedirs(cache, exist_ok=True)
-    np.savez(path, keys=keys, coefs=coefs, **{f: getattr(packed, f) for f in FIELDS})
     return packed, keys, coefs
 
 
@@ -45,10 +34,10 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--sentences', type=int, default=65536)
     ap.add_argument('--seed', type=int, default=0)
-    ap.add_argument('--cache', default='/tmp/ltw')
+    ap.add_argument('--cache', default=None, help='(ignored; kept for the scripts that pass it)')
     a = ap.parse_args()
     lib = _capi.load()
-    packed, keys, coefs = workload(a.cache, a.sentences, a.seed)
+    packed, keys, coefs = workload(a.sentences, a.seed)
     ctx = _capi.Context(0)
     dm = _capi.DeviceModel(ctx, keys, coefs)
     db = _capi.DeviceBatch(ctx, packed, max_k=a.k)
