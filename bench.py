@@ -257,7 +257,8 @@ def workgroups(k, n_sent):
     if k == 1:
         return -(-n_sent // (8 * 8))                   # W = 8 sentences per wave, 8 waves per block (narrow keys)
     if k <= 8:
-        return -(-n_sent // ((64 // (16 if k <= 3 else 32)) * 4))
+        wpb = 1 if k >= 5 else 4                       # HW8_WPB (k = 5..8, KT = 8), HW_WPB below
+        return -(-n_sent // ((64 // (16 if k <= 3 else 32)) * wpb))
     return -(-n_sent // (1 if k <= 16 else 2))
 
 

@@ -2567,7 +2567,10 @@ __global__ void __launch_bounds__(256) lt_eval_paths_k(EvalParams p) {
 }
 
 #ifndef HW_WPB
-#define HW_WPB 4                        // waves per block of lt_beam_hw
+#define HW_WPB 4                        // waves per block of lt_beam_hw, k = 2..4
+#endif
+#ifndef HW8_WPB
+#define HW8_WPB 1                       // waves per block of lt_beam_hw, k = 5..8 (k=5: 4.044 ms at 4)
 #endif
 #ifndef BP16_WPB
 #define BP16_WPB 1                      // waves per block of lt_beam_pk, k = 9..16 (1: 15.9 ms at k=16, 2: 16.7, 4: 16.7)
@@ -2592,7 +2595,7 @@ hipError_t launch_k(const DecodeParams& p, int kt, const Launch& L) {
     }
     switch (kt) {
       case 4: return launch_hw<4, 32, HW_WPB, NARROW>(p, L);
-      case 8: return launch_hw<8, 32, HW_WPB, NARROW>(p, L);
+      case 8: return launch_hw<8, 32, HW8_WPB, NARROW>(p, L);
       default: return hipErrorInvalidValue;
     }
   }
