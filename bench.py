@@ -46,6 +46,15 @@ from lattice_based_tagger_amd import _capi, synth, lowering as Lw  # noqa: E402
 
 METRIC = 'sentences/sec Viterbi decode, 64K-sentence batch; achieved HBM GB/s vs 8 TB/s'
 HBM_PEAK_GBS = 8000.0
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles
+# per SIMD (16 lanes wide; f64 adds at the same rate on CDNA4), 2.4 GHz
+SIMDS = 1024
+CLOCK_HZ = 2.4e9
+VALU_PEAK_PER_S = SIMDS * CLOCK_HZ / 4
+# the byte model's revision (roofline.byte_model_version): 2 = round 5 on,
+# one slot load per probe must-move for the tuned beams (both issued);
+# 1 = rounds 1-4, every issued slot load
+BYTE_MODEL_VERSION = 2
 # batch layout of this revision (implicit Unknowns, lattice_decode.h ABI 5): PMC
 # traffic summaries are only matched to a run of the same layout
 LAYOUT = 'abi5-rec32'
@@ -72,7 +81,11 @@ def parse():
     ap.add_argument('--gather', type=int, default=None,
                     help='1: gather every rank\'s results to rank 0 with RCCL inside each step '
                          '(default: on when WORLD_SIZE > 1; a failed RCCL setup then fails the run); '
-                         '0: no result exchange (labelled in the JSON line)')
+                         '0: local delivery -- every rank copies its own shard\'s compact results to '
+                         'pinned host memory over its own PCIe link, no RCCL (labelled in the JSON line)')
+    ap.add_argument('--d2h', choices=('padded', 'packed'), default=None,
+                    help='result delivery without the gather: padded arrays (the N=1 default) or the '
+                         'compact slab (lt_result_fetch_packed; the default of --gather 0 at N > 1)')
     ap.add_argument('--no-wide-keys', dest='wide_keys', action='store_false',
                     help='skip the wide-key (ids >= 2^20) model entry under "extra"')
     ap.add_argument('--extra-k', default='5,16',
@@ -81,61 +94,42 @@ def parse():
     return ap.parse_args()
 
 
-class Dist:
-    """Rank bookkeeping; gloo process group for barrier / max (host only)."""
+class Dist(object):
+    """Rank bookkeeping; barrier / max / sum / the RCCL id over the torch-free
+    host group (lattice_based_tagger_amd/dist.py HostGroup: TCP, host only)."""
 
     def __init__(self, want):
-        self.rank = int(os.environ.get('RANK', 0))
-        self.world = int(os.environ.get('WORLD_SIZE', 1))
-        self.local = int(os.environ.get('LOCAL_RANK', 0))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist          # after liblt is loaded
-            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-            dist.init_process_group('gloo', rank=self.rank, world_size=self.world)
-            self.pg = dist
+        from lattice_based_tagger_amd.dist import HostGroup, Ranks
+        r = Ranks()
+        self.rank, self.world, self.local = r.rank, r.world, r.local
+        self.g = HostGroup(r) if self.world > 1 else None
         if want != self.world and self.rank == 0:
             print('warning: --gpus %d but WORLD_SIZE %d' % (want, self.world), file=sys.stderr)
 
     def barrier(self):
-        if self.pg:
-            self.pg.barrier()
+        if self.g:
+            self.g.barrier()
 
     def max(self, v):
-        if not self.pg:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
-        return float(t.item())
+        return self.g.max(v) if self.g else v
 
     def min(self, v):
-        if not self.pg:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MIN)
-        return float(t.item())
+        return self.g.min(v) if self.g else v
 
     def sum(self, v):
-        if not self.pg:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
-        return float(t.item())
+        return self.g.sum(v) if self.g else v
 
     def broadcast_bytes(self, data):
-        """Rank 0's bytes on every rank (gloo; host only)."""
-        if not self.pg:
-            return data
-        obj = [data]
-        self.pg.broadcast_object_list(obj, src=0)
-        return obj[0]
+        """Rank 0's bytes on every rank (host only)."""
+        return self.g.broadcast_bytes(data) if self.g else data
+
+    def gather(self, obj):
+        """Per-rank objects on rank 0 (list in rank order), None elsewhere."""
+        return self.g.gather(obj) if self.g else [obj]
 
     def close(self):
-        if self.pg:
-            self.pg.destroy_process_group()
+        if self.g:
+            self.g.close()
 
 
 def make_workload(n_sent, seed, n_features):
@@ -370,6 +364,63 @@ def traffic_from_profiles(kernel, k, sentences, features, seed):
     return best
 
 
+def decode_src_sha():
+    """sha256 of the decode kernels' source (first 16 hex digits): ties a
+    committed counter summary to the build it was measured on."""
+    import hashlib
+    p = os.path.join(ROOT, 'lattice_based_tagger_amd', 'csrc', 'lt_decode.hip')
+    try:
+        return hashlib.sha256(open(p, 'rb').read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def issue_from_profiles(kernel, k, sentences, features, seed, kernel_s, expansions):
+    """The VALU issue roofline of this configuration from the newest committed
+    SQ counter summary of this batch layout (profiles/**/sq_summary*.json,
+    tools/sq_summary.py over tools/gpu_sq_ab.sh): VALU wave-instructions per
+    launch over this run's kernel time against the VALU issue peak, and the
+    VALU busy fraction (SQ_ACTIVE_INST_VALU x 4 cycles / (SIMDs x kernel
+    cycles)).  same_build: the summary's source hash equals this tree's
+    lt_decode.hip.  None without a summary."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '**', 'sq_summary*.json'), recursive=True)):
+        try:
+            entries = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for e in entries:
+            if (e.get('kernel'), e.get('k'), e.get('sentences'), e.get('features'), e.get('seed'),
+                    e.get('layout')) == (kernel, k, sentences, features, seed, LAYOUT):
+                if best is None or e.get('src_sha') == decode_src_sha() or best[0].get('src_sha') != decode_src_sha():
+                    best = (e, os.path.relpath(f, ROOT))
+    if best is None:
+        return None
+    e, src = best
+    c = e['counters_per_launch']
+    valu = c.get('SQ_INSTS_VALU')
+    act = c.get('SQ_ACTIVE_INST_VALU', valu)
+    if not valu:
+        return None
+    out = {'bound': 'valu', 'achieved': valu / kernel_s, 'peak': VALU_PEAK_PER_S,
+           'unit': 'VALU wave-instructions/s', 'frac': valu / kernel_s / VALU_PEAK_PER_S,
+           'valu_busy': act * 4 / (SIMDS * CLOCK_HZ * kernel_s),
+           'valu_per_launch': valu, 'valu_per_expansion': valu / expansions if expansions else None,
+           'source': src, 'same_build': e.get('src_sha') == decode_src_sha()}
+    if c.get('SQ_LDS_IDX_ACTIVE'):
+        out['lds_conflict_frac'] = c.get('SQ_LDS_BANK_CONFLICT', 0.0) / c['SQ_LDS_IDX_ACTIVE']
+    return out
+
+
+def roofline_bound(hbm_frac, traffic_frac, issue):
+    """The resource the kernel runs closest to its peak on: 'valu' when the
+    VALU busy fraction exceeds both the must-move byte fraction and the
+    measured fabric-traffic fraction, else 'hbm'."""
+    b = max(hbm_frac, traffic_frac or 0.0)
+    return 'valu' if issue and issue['valu_busy'] > b else 'hbm'
+
+
 def gather_ceiling(table_bytes):
     """Random 16 B gather ceiling of the MI355X for a table of table_bytes:
     the newest committed tools/gather_ceiling run (profiles/*/gather_ceiling.jsonl:
@@ -398,9 +449,11 @@ def probe_rate(table_loads, kernel_s, keys, slots, traffic=None):
     for the model's table size (tools/gather_ceiling.hip): the probes are
     spread 16 B loads, each L2 miss moves a 128 B line, so the roofline that
     binds them is a line rate, not HBM bytes.
-      frac        issued slot loads per second / the uniform-random ceiling;
+      ratio_to_uniform_ceiling
+                  issued slot loads per second / the uniform-random ceiling;
                   above 1.0 = cache reuse beyond uniform random (line groups,
-                  Zipf-popular words, the hypotheses of one beam)
+                  Zipf-popular words, the hypotheses of one beam) -- so not a
+                  roofline fraction (kept out of `roofline` since round 6)
       fabric_frac the kernel's L2-miss traffic (PMC, roofline.traffic) per
                   second / the ceiling's line rate (loads/s x 128 B)"""
     keys = np.asarray(keys).reshape(-1, 4)
@@ -412,7 +465,7 @@ def probe_rate(table_loads, kernel_s, keys, slots, traffic=None):
     fabric_gbps = traffic / kernel_s / 1e9 if traffic else None
     return {'loads_per_s': rate, 'table_bytes': table_bytes,
             'ceiling_loads_per_s': ceil[0] if ceil else None,
-            'frac': rate / ceil[0] if ceil else None,
+            'ratio_to_uniform_ceiling': rate / ceil[0] if ceil else None,
             'ceiling_line_GBps': line_gbps,
             'fabric_GBps': fabric_gbps,
             'fabric_frac': fabric_gbps / line_gbps if (line_gbps and fabric_gbps) else None,
@@ -461,6 +514,7 @@ def main():
     t_up = time.perf_counter()
     db = _capi.DeviceBatch(ctx, piece, max_k=k)          # H2D, outside the timed region
     t_up = time.perf_counter() - t_up
+    host_sched_ms = db.host_sched_ms()
     expansions, tuples, probes, table_loads = db.count_ops(dm, k)
 
     # result gather to rank 0 over RCCL/xGMI (the path's one exchange step)
@@ -487,6 +541,7 @@ def main():
             d.close()
             sys.exit(3)
     root = d.rank == 0
+    d2h_mode = a.d2h or ('packed' if (d.world > 1 and not comm) else 'padded')
 
     def step():
         db.launch(dm, k)
@@ -494,6 +549,8 @@ def main():
             comm.launch(db)            # pack into the send slot + ncclGather (own stream)
             if root:
                 comm.fetch()           # every rank's used bytes -> pinned host (copy stream)
+        elif d2h_mode == 'packed':
+            db.fetch_packed()          # compact slab on the device, its used bytes -> pinned host
         else:
             db.fetch()                 # DMA of the results -> pinned host (copy stream)
 
@@ -542,7 +599,8 @@ def main():
         fel = d.max(tf1 - tf0)
         fresh = {'value': total_sent_of(a, d, strong) / fel, 'unit': 'sentences/s',
                  'ms_per_step': fel / a.steps * 1e3, 'prep_ms_last': db.prep_ms(),
-                 'prep_bytes': db.prep_bytes(),
+                 'prep_bytes': db.prep_bytes(), 'host_sched_ms': host_sched_ms,
+                 'ms_per_step_with_host_sched': fel / a.steps * 1e3 + (host_sched_ms or 0.0),
                  'step': 'lane-schedule build (lt_k1_sched) + decode + result D2H of a batch not decoded '
                          'before, batch resident in HBM (H2D excluded, as the headline)'}
     total_sent = total_sent_of(a, d, strong)
@@ -552,7 +610,7 @@ def main():
     if comm and root:
         got = [comm.view(r) for r in range(d.world)]
     elif not comm:
-        got = [padded_as_packed(db.results(k), piece.sent_n, k)]
+        got = [db.results_packed() if d2h_mode == 'packed' else padded_as_packed(db.results(k), piece.sent_n, k)]
     else:
         got = None
     mine = db.decode(dm, k)                                   # padded layout, this rank's shard
@@ -590,8 +648,11 @@ def main():
     # the roofline's byte model is what the kernel must move: it cannot run
     # faster than HBM moves it
     assert achieved <= HBM_PEAK_GBS, 'byte model above the HBM peak: %.0f GB/s' % achieved
+    issue = issue_from_profiles(kernel, k, piece.n_sent, a.features, a.seed, avg_kernel_s, expansions) \
+        if (d.world == 1 or not strong) else None
+    traffic_frac = traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None
     al = lambda x: (x + 15) // 16 * 16                      # noqa: E731
-    if comm:
+    if comm or d2h_mode == 'packed':
         d2h = sum(32 + al(4 * g.n_sent) + al(4 * g.length.size) + al(8 * g.length.size) +
                   al(4 * g.codes.size) for g in got) if got is not None else None
     else:
@@ -649,7 +710,7 @@ def main():
                 'parallelism': 'dp%d' % d.world,
             },
             'roofline': {
-                'bound': 'hbm',
+                'bound': roofline_bound(achieved / HBM_PEAK_GBS, traffic_frac, issue),
                 'achieved': achieved,
                 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s',
@@ -658,42 +719,55 @@ def main():
                 'traffic_unit': 'fabric bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE: HBM and '
                                 'Infinity-Cache hits)',
                 'traffic_source': traffic[1] if traffic else None,
-                'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
+                'traffic_frac': traffic_frac,
+                'issue': issue,
                 'kernel': kernel,
                 'bytes_per_launch': KB,
+                'byte_model_version': BYTE_MODEL_VERSION,
                 'avg_kernel_ms': avg_kernel_s * 1e3,
                 'launch': 'rank 0 shard' if d.world > 1 else 'whole batch',
                 'frac_note': 'achieved = bytes the kernel must move per launch (bench.kernel_bytes: node records '
                              'once, lane schedule, offsets, 16 B per feature-table slot load a kernel of this '
                              'table layout cannot avoid (bench.must_move_loads), staged '
                              'tables, HBM backpointers, results) / average kernel time (HIP events over the '
-                             'timed steps); work_equivalent_frac = SURVEY 8(d) bytes (24 B per reference '
-                             'feature tuple, most never loaded: node pre-filter, class 3 in LDS, classes 4-6 '
-                             'per node) / the same time -- a work rate, not a memory measurement',
-                'work_equivalent_bytes_per_launch': B,
-                'work_equivalent_frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
+                             'timed steps); issue = VALU wave-instructions per launch (committed SQ counter '
+                             'summary, same_build: of this source) / the same time against the VALU issue '
+                             'peak (1,024 SIMDs, 2.4 GHz, 4 cycles each); bound = the larger of the byte, '
+                             'fabric-traffic and VALU-busy fractions',
                 'layout': LAYOUT,
-                'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots, traffic[0] if traffic else None),
             },
+            'work_equivalent': {'bytes_per_launch': B, 'GBps': B / avg_kernel_s / 1e9,
+                                'note': 'SURVEY 8(d) bytes (24 B per reference feature tuple, most never '
+                                        'loaded: node pre-filter, class 3 in LDS, classes 4-6 per node) / '
+                                        'kernel time -- a work rate, not a memory measurement (exceeds '
+                                        'the HBM peak)'},
+            'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots, traffic[0] if traffic else None),
             'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                                'table_probes': probes, 'table_slot_loads': table_loads},
             'kernel_only_sentences_per_s': piece.n_sent / avg_kernel_s,
             'fresh_batch': fresh,
-            'd2h': {'bytes_per_step': d2h, 'in_timed_region': True,
+            'd2h': {'bytes_per_step': d2h, 'in_timed_region': True, 'mode': 'root' if comm else d2h_mode,
                     'how': ('rank 0: every rank\'s packed results (gathered slabs), used bytes to '
                             'pinned host memory on a copy stream' if comm else
+                            'this rank\'s compact result slab (packed on the device), used bytes to '
+                            'pinned host memory on a copy stream' if d2h_mode == 'packed' else
                             'padded results by DMA to pinned host memory on a copy stream') +
                            ', under the next decode'},
             'gather': ({'collective': 'one ncclGather of packed result slabs (RCCL), root 0, on its '
                                       'own stream: gather of step i overlaps decode of step i+1',
                         'rccl': (lib.lt_comm_library() or b'?').decode(),
                         'last_gather_ms': gather_ms, 'in_timed_region': True} if comm else
-                       {'disabled': '--gather 0: every rank decodes its shard, no result exchange; '
-                                    'not a multi-GPU result of the north star'}
+                       {'mode': 'local',
+                        'disabled': '--gather 0: every rank decodes its shard and copies its own compact '
+                                    'results to pinned host memory over its own PCIe link (no RCCL); the '
+                                    'results end in N processes of one node, not in rank 0 (the north '
+                                    'star\'s single gather is the default mode)'}
                        if d.world > 1 else None),
             'check': check,
-            'host': {'gen_s': t_gen, 'h2d_s': t_up, 'nproc': os.cpu_count(), 'cpu': cpu_model(),
-                     'visible_gpus': ndev},
+            'host': {'gen_s': t_gen, 'h2d_s': t_up, 'sched_ms': host_sched_ms, 'nproc': os.cpu_count(),
+                     'cpu': cpu_model(), 'visible_gpus': ndev,
+                     'note': 'h2d_s = lt_batch_create (validation, records, the k=1 schedule on the host '
+                             'threads -- sched_ms of it -- uploads, the schedule fill), outside the timed region'},
         }
         if extra is not None:
             line['extra'] = extra
@@ -748,6 +822,9 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys, with_traffic=True)
     KI = kernel_bytes(piece, table_loads, k, 0, blocks, d3)              # as issued (both cuckoo slots)
     assert KI / avg_kernel_s / 1e9 <= HBM_PEAK_GBS, 'issued byte model above the HBM peak'
     traffic = traffic_from_profiles(kernel, k, piece.n_sent, a.features, a.seed) if with_traffic else None
+    traffic_frac = traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None
+    issue = issue_from_profiles(kernel, k, piece.n_sent, a.features, a.seed, avg_kernel_s, expansions) \
+        if with_traffic else None
     return {
         'beam': k,
         'value': piece.n_sent * a.steps / elapsed,
@@ -757,18 +834,19 @@ def time_beam(ctx, dm, piece, raw, order, lo, hi, k, a, keys, with_traffic=True)
         'kernel': kernel,
         'avg_kernel_ms': avg_kernel_s * 1e3,
         'kernel_only_sentences_per_s': piece.n_sent / avg_kernel_s,
-        'roofline': {'bound': 'hbm', 'achieved': KB / avg_kernel_s / 1e9, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'roofline': {'bound': roofline_bound(KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS, traffic_frac, issue),
+                     'achieved': KB / avg_kernel_s / 1e9, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': KB / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                      'bytes_per_launch': KB,
+                     'byte_model_version': BYTE_MODEL_VERSION,
                      'issued_bytes_per_launch': KI,
                      'issued_frac': KI / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
-                     'work_equivalent_bytes_per_launch': B,
-                     'work_equivalent_frac': B / avg_kernel_s / 1e9 / HBM_PEAK_GBS,
                      'traffic': traffic[0] if traffic else None,
                      'traffic_source': traffic[1] if traffic else None,
-                     'traffic_frac': traffic[0] / avg_kernel_s / 1e9 / HBM_PEAK_GBS if traffic else None,
-                     'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots,
-                                              traffic[0] if traffic else None)},
+                     'traffic_frac': traffic_frac,
+                     'issue': issue},
+        'work_equivalent': {'bytes_per_launch': B, 'GBps': B / avg_kernel_s / 1e9},
+        'probe_rate': probe_rate(table_loads, avg_kernel_s, keys, dm.slots, traffic[0] if traffic else None),
         'ops_per_launch': {'expansions': expansions, 'feature_tuples': tuples,
                            'table_probes': probes, 'table_slot_loads': table_loads},
     }

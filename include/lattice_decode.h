@@ -213,8 +213,21 @@ lt_status lt_batch_reset_prep(lt_batch* batch);
  * valid once that work is complete (after lt_sync).  0 when none ran. */
 lt_status lt_batch_prep_ms(lt_batch* batch, float* ms);
 /* Bytes of the batch's device preparation (the lane schedules and their wave
- * offsets) -- what a beam-1 decode reads of them. */
+ * offsets) -- what a beam-1 decode reads of them.  Not counted: the
+ * per-character placements the fill reads (4 bytes per character), which are
+ * uploaded with the batch (or, for a lazily prepared batch, live in a buffer
+ * of their own). */
 int64_t lt_batch_prep_bytes(const lt_batch* batch);
+/* Wall time (ms) lt_batch_create spent computing the beam-1 schedule's steps
+ * and placements on the host threads (0 for a batch created for larger
+ * beams, whose schedule is computed on the device). */
+double lt_batch_host_sched_ms(const lt_batch* batch);
+/* Build the beam-1 device preparation of a batch created for larger beams
+ * now, instead of at its first beam-1 decode: allocates, synchronises the
+ * context stream once, and queues the schedule fill on it.  A pipeline calls
+ * this off its launch path, so that no lt_decode_launch blocks.  No-op for a
+ * batch that has one (or for max_len > LT_MAX_SPAN, decoded without). */
+lt_status lt_batch_prepare_k1(lt_batch* batch);
 /* Total path-code slots of the results for beam k: k * sum_s n_s. */
 int64_t lt_batch_code_slots(const lt_batch* batch, int k);
 /* Kernel launches per decode of the batch: a batch of any size is decoded in

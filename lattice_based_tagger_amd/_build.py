@@ -71,7 +71,8 @@ def build(force=False, verbose=True, defines=(), out=None):
         return lib
     objs = []
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + '.o')
+        # (objects named after the library too: experiment builds can run in parallel)
+        obj = os.path.join(LIBDIR, os.path.splitext(os.path.basename(lib))[0] + '_' + os.path.splitext(src)[0] + '.o')
         extra = os.environ.get('LT_EXTRA_FLAGS', '').split() if out is not None else []   # experiment builds only
         cmd = [HIPCC, '--offload-arch=' + ARCH] + COMMON_FLAGS + extra + ['-D' + d for d in defines] + [
             '-c', os.path.join(CSRC, src), '-o', obj]

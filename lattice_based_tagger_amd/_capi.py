@@ -23,7 +23,8 @@ EXPORTED_SYMBOLS = (
     'lt_abi_version', 'lt_hash_version', 'lt_last_error', 'lt_device_count', 'lt_ctx_create', 'lt_ctx_destroy',
     'lt_sync', 'lt_model_create', 'lt_model_destroy', 'lt_model_slots', 'lt_batch_create',
     'lt_batch_destroy', 'lt_batch_code_slots', 'lt_batch_pieces', 'lt_set_piece_bytes', 'lt_batch_reset_prep',
-    'lt_batch_prep_ms', 'lt_batch_prep_bytes', 'lt_decode_launch', 'lt_last_kernel_ms',
+    'lt_batch_prep_ms', 'lt_batch_prep_bytes', 'lt_batch_host_sched_ms', 'lt_batch_prepare_k1',
+    'lt_decode_launch', 'lt_last_kernel_ms',
     'lt_kernel_ms_recent', 'lt_kernel_name',
     'lt_result_fetch', 'lt_result_view', 'lt_decode', 'lt_count_ops',
     'lt_result_fetch_packed', 'lt_result_view_packed', 'lt_slab_parse',
@@ -149,6 +150,8 @@ def load(path=None):
             'lt_batch_reset_prep': (i32, [vp]),
             'lt_batch_prep_ms': (i32, [vp, C.POINTER(C.c_float)]),
             'lt_batch_prep_bytes': (i64, [vp]),
+            'lt_batch_host_sched_ms': (C.c_double, [vp]),
+            'lt_batch_prepare_k1': (i32, [vp]),
             'lt_decode_launch': (i32, [vp, vp, vp, C.c_int]),
             'lt_last_kernel_ms': (i32, [vp, C.POINTER(C.c_float)]),
             'lt_kernel_ms_recent': (i32, [vp, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int)]),
@@ -203,7 +206,7 @@ def load(path=None):
 
 
 # entry points an A/B build of an earlier revision may lack (tools/gpu_ab.sh)
-OPTIONAL_CALLS = ('lt_hash_version',)
+OPTIONAL_CALLS = ('lt_hash_version', 'lt_batch_host_sched_ms', 'lt_batch_prepare_k1')
 
 # lt_* entry points that return in microseconds (see load)
 HELD_CALLS = ('lt_decode_launch', 'lt_result_fetch', 'lt_result_view', 'lt_result_fetch_packed',
@@ -437,6 +440,18 @@ class DeviceBatch:
         v = C.c_float()
         check(self.ctx._lib.lt_batch_prep_ms(self.handle, C.byref(v)))
         return float(v.value)
+
+    def host_sched_ms(self):
+        """Wall time (ms) lt_batch_create spent on the host half of the
+        beam-1 schedule (steps and placements); None from a library without
+        the call."""
+        fn = getattr(self.ctx._lib, 'lt_batch_host_sched_ms', None)
+        return float(fn(self.handle)) if fn else None
+
+    def prepare_k1(self):
+        """Build the beam-1 schedule of a batch created for larger beams now
+        (lattice_decode.h lt_batch_prepare_k1), off the launch path."""
+        check(self.ctx._lib.lt_batch_prepare_k1(self.handle))
 
     def fetch(self):
         check(self.ctx._lib.held.lt_result_fetch(self.ctx.handle, self.handle))

@@ -758,9 +758,14 @@ static void arena_free(lt_arena& a) {
 }
 
 // Arenas up to this size are kept for reuse, at most SPARE_N per context
-// (Tagger.tag_batch keeps three chunk batches in flight, one more is queued).
+// (Tagger.tag_batch keeps three chunk batches in flight, one more is queued)
+// and at most SPARE_BYTES (device + pinned host) in all: the largest batches
+// seen do not pin gigabytes for the context's lifetime.
 constexpr size_t SPARE_MAX = (size_t)1 << 30;
 constexpr size_t SPARE_N = 4;
+constexpr size_t SPARE_BYTES = (size_t)3 << 30;
+
+static size_t arena_bytes(const lt_arena& a) { return a.d_bytes + a.h_bytes; }
 
 // New arenas are sized with headroom and rounded up to one of eight size
 // classes per power of two, so that a recycled arena fits the next batches
@@ -775,7 +780,9 @@ static size_t arena_class(size_t n) {
 }
 
 // An arena with at least (dn, hn) bytes: the smallest fitting spare, else a
-// new allocation (a spare that does not fit stays for a later batch).
+// new allocation (a spare that does not fit stays for a later batch).  When
+// the allocation fails, the spares (none of which fit) are freed and it is
+// tried once more, so idle pooled memory never causes LT_ENOMEM.
 static hipError_t arena_take(lt_ctx* c, size_t dn, size_t hn, lt_arena& out) {
   {
     std::lock_guard<std::mutex> g(c->mu);
@@ -790,15 +797,27 @@ static hipError_t arena_take(lt_ctx* c, size_t dn, size_t hn, lt_arena& out) {
       return hipSuccess;
     }
   }
-  out = lt_arena{};
   dn = arena_class(dn);
   hn = arena_class(hn);
   hipError_t e = hipSuccess;
-  if (dn) e = hipMalloc((void**)&out.d, dn);
-  if (e == hipSuccess) out.d_bytes = dn;
-  if (e == hipSuccess && hn) e = hipHostMalloc((void**)&out.h, hn, hipHostMallocDefault);
-  if (e == hipSuccess) out.h_bytes = hn;
-  if (e != hipSuccess) arena_free(out);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    out = lt_arena{};
+    e = hipSuccess;
+    if (dn) e = hipMalloc((void**)&out.d, dn);
+    if (e == hipSuccess) out.d_bytes = dn;
+    if (e == hipSuccess && hn) e = hipHostMalloc((void**)&out.h, hn, hipHostMallocDefault);
+    if (e == hipSuccess) out.h_bytes = hn;
+    if (e == hipSuccess) return e;
+    arena_free(out);
+    std::vector<lt_arena> drop;
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      drop.swap(c->spare);
+    }
+    if (drop.empty()) break;                    // nothing pooled to give back
+    (void)hipGetLastError();                    // (clear the failed allocation's error)
+    for (lt_arena& a : drop) arena_free(a);
+  }
   return e;
 }
 
@@ -808,15 +827,21 @@ static void arena_give(lt_ctx* c, lt_arena& a) {
   if (!a.d && !a.h) return;
   if (a.d_bytes <= SPARE_MAX) {
     std::lock_guard<std::mutex> g(c->mu);
-    if (c->spare.size() < SPARE_N) {
+    size_t held = 0;
+    for (const lt_arena& x : c->spare) held += arena_bytes(x);
+    if (c->spare.size() < SPARE_N && held + arena_bytes(a) <= SPARE_BYTES) {
       c->spare.push_back(a);
       a = lt_arena{};
       return;
     }
+    // full: the smallest of the spares and this one is freed, as long as the
+    // swap keeps the pool within SPARE_BYTES
     int small = 0;
     for (int i = 1; i < (int)c->spare.size(); ++i)
-      if (c->spare[i].d_bytes + c->spare[i].h_bytes < c->spare[small].d_bytes + c->spare[small].h_bytes) small = i;
-    if (c->spare[small].d_bytes + c->spare[small].h_bytes < a.d_bytes + a.h_bytes) std::swap(c->spare[small], a);
+      if (arena_bytes(c->spare[i]) < arena_bytes(c->spare[small])) small = i;
+    if (!c->spare.empty() && arena_bytes(c->spare[small]) < arena_bytes(a) &&
+        held - arena_bytes(c->spare[small]) + arena_bytes(a) <= SPARE_BYTES)
+      std::swap(c->spare[small], a);
   }
   arena_free(a);
 }
@@ -933,44 +958,78 @@ static hipError_t prep_fill(lt_batch* b, hipStream_t st) {
 // batch.
 static lt_status lazy_sched(lt_ctx* c, lt_batch* b) {
   if (b->has_sched || b->max_len > MAX_SPAN) return LT_OK;
-  std::vector<std::vector<int64_t>> offs(b->pieces.size());
-  for (size_t q = 0; q < b->pieces.size(); ++q) {
-    lt_piece& pc = b->pieces[q];
-    if (pc.n_nodes >= (int64_t)K1_NODE)
+  // every buffer in locals first, published to the pieces only once all of
+  // them exist (a failure frees what it allocated: a later decode retries
+  // from scratch, nothing leaks)
+  const size_t P = b->pieces.size();
+  std::vector<int64_t*> d_off(P, nullptr);
+  std::vector<uint32_t*> d_place(P, nullptr), d_sched(P, nullptr);
+  std::vector<int64_t> steps(P, 0);
+  auto undo = [&]() {
+    (void)hipStreamSynchronize(c->stream);
+    for (size_t q = 0; q < P; ++q) {
+      dfree(d_off[q]);
+      dfree(d_place[q]);
+      dfree(d_sched[q]);
+    }
+  };
+  std::vector<std::vector<int64_t>> offs(P);
+  for (size_t q = 0; q < P; ++q) {
+    const lt_piece& pc = b->pieces[q];
+    if (pc.n_nodes >= (int64_t)K1_NODE) {
+      undo();
       return fail(LT_EUNSUPPORTED, "decode: %lld nodes in one launch piece for the beam-1 schedule",
                   (long long)pc.n_nodes);
+    }
     const int waves = k1_waves(pc.n_sent);
-    int64_t* d_off = nullptr;
-    HIP_TRY(hipMalloc((void**)&d_off, ((size_t)waves + 1) * 8));
-    pc.d_wave_off = d_off;                     // (freed with the batch from here on)
-    b->lazy_sched = true;
-    HIP_TRY(hipMalloc((void**)&pc.d_place, (size_t)std::max<int64_t>(piece_chars(b, q), 1) * 4));
+    hipError_t e = hipMalloc((void**)&d_off[q], ((size_t)waves + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_place[q], (size_t)std::max<int64_t>(piece_chars(b, q), 1) * 4);
     DecodeParams p{};
-    piece_params(b, q, 1, p);
-    p.max_len = b->max_len;
-    p.k1_place = pc.d_place;                   // (has_sched is set once the schedule exists)
-    HIP_TRY(launch_k1_sched_count(p, d_off, c->stream));
+    if (e == hipSuccess) {
+      piece_params(b, q, 1, p);
+      p.max_len = b->max_len;
+      p.k1_place = d_place[q];
+      e = launch_k1_sched_count(p, d_off[q], c->stream);
+    }
     offs[q].assign((size_t)waves + 1, 0);
-    HIP_TRY(hipMemcpyAsync(offs[q].data(), d_off, (size_t)waves * 8, hipMemcpyDeviceToHost, c->stream));
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(offs[q].data(), d_off[q], (size_t)waves * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) {
+      undo();
+      return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "decode: beam-1 schedule: %s", hipGetErrorString(e));
+    }
   }
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  for (size_t q = 0; q < b->pieces.size(); ++q) {
-    lt_piece& pc = b->pieces[q];
+  hipError_t e = hipStreamSynchronize(c->stream);
+  for (size_t q = 0; e == hipSuccess && q < P; ++q) {
     std::vector<int64_t>& wo = offs[q];
     int64_t run = 0;
     for (size_t w = 0; w + 1 < wo.size(); ++w) {   // exclusive prefix sum
       const int64_t x = wo[w];
-      if (x >= ((int64_t)1 << K1_TBITS))
+      if (x >= ((int64_t)1 << K1_TBITS)) {
+        undo();
         return fail(LT_EUNSUPPORTED, "decode: %lld macro-steps in one beam-1 wave schedule", (long long)x);
+      }
       wo[w] = run;
       run += x;
     }
     wo.back() = run;
-    pc.sched_steps = run;
-    HIP_TRY(hipMalloc((void**)&pc.d_sched, (size_t)std::max<int64_t>(run, 1) * 64 * 4));
-    HIP_TRY(hipMemcpyAsync(pc.d_wave_off, wo.data(), wo.size() * 8, hipMemcpyHostToDevice, c->stream));
+    steps[q] = run;
+    e = hipMalloc((void**)&d_sched[q], (size_t)std::max<int64_t>(run, 1) * 64 * 4);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_off[q], wo.data(), wo.size() * 8, hipMemcpyHostToDevice, c->stream);
   }
-  HIP_TRY(hipStreamSynchronize(c->stream));        // (the host offsets go out of scope)
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);        // (the host offsets go out of scope)
+  if (e != hipSuccess) {
+    undo();
+    return fail(e == hipErrorOutOfMemory ? LT_ENOMEM : LT_EHIP, "decode: beam-1 schedule: %s", hipGetErrorString(e));
+  }
+  for (size_t q = 0; q < P; ++q) {
+    lt_piece& pc = b->pieces[q];
+    pc.d_wave_off = d_off[q];
+    pc.d_place = d_place[q];
+    pc.d_sched = d_sched[q];
+    pc.sched_steps = steps[q];
+  }
+  b->lazy_sched = true;
   b->has_sched = true;
   b->prep_done = false;
   return LT_OK;
@@ -1069,6 +1128,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   b->n_unk = d->n_unk;
   std::vector<std::vector<int64_t>> wave_off(P);
   std::vector<std::vector<uint32_t>> place(P);   // k=1 placements, uploaded with the batch
+  const double t_sched0 = b->has_sched ? now_s() : 0.0;
   if (b->has_sched) {
     for (size_t q = 0; q < P; ++q) {
       lt_piece& pc = b->pieces[q];
@@ -1112,6 +1172,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       for (int w = 0; w < waves; ++w) wo[(size_t)w + 1] += wo[(size_t)w];
       pc.sched_steps = wo[(size_t)waves];
     }
+    b->host_sched_ms = (now_s() - t_sched0) * 1e3;
   }
 
   // the class-4/6 pair table of the records (NodeRec): the implicit
@@ -1356,6 +1417,18 @@ int64_t lt_batch_prep_bytes(const lt_batch* b) {
   int64_t bytes = 0;
   for (const lt_piece& pc : b->pieces) bytes += pc.sched_steps * 64 * 4 + ((int64_t)k1_waves(pc.n_sent) + 1) * 8;
   return bytes;
+}
+
+double lt_batch_host_sched_ms(const lt_batch* b) { return b ? b->host_sched_ms : 0.0; }
+
+lt_status lt_batch_prepare_k1(lt_batch* b) {
+  if (!b) return fail(LT_EINVAL, "lt_batch_prepare_k1: NULL batch");
+  lt_ctx* c = b->ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  lt_status st = lazy_sched(c, b);
+  if (st != LT_OK) return st;
+  HIP_TRY(prep_fill(b, c->stream));
+  return LT_OK;
 }
 
 lt_status lt_batch_prep_ms(lt_batch* b, float* ms) {

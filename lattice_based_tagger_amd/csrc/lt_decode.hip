@@ -238,11 +238,13 @@ struct Tab<true> {
                                    uint32_t, uint32_t slots) {
     return narrow_slot2(x.hk, a, b, c, cls, slots);
   }
-  // a frozen arbitrary value (no instruction): lanes that load nothing keep a
-  // defined slot, so a check can select on it instead of branching
+  // an arbitrary value (no instruction): lanes that load nothing keep a
+  // defined slot, so a check can select on it instead of branching.  An empty
+  // asm defines the registers (__builtin_nondeterministic_value is a frozen
+  // poison, which the compiler materialised as zeros: two 64-bit moves per
+  // probed class and macro-step in the k=1 kernel)
   __device__ static void arbitrary(S& s) {
-    s.key = __builtin_nondeterministic_value(s.key);
-    s.coef = __builtin_nondeterministic_value(s.coef);
+    asm volatile("" : "=v"(s.key), "=v"(s.coef));
   }
   __device__ static S load(rsrc_t t, uint32_t off) {
     const u32x4 v = ld128(t, off);
@@ -351,16 +353,31 @@ __device__ __forceinline__ uint32_t probe_need(const Hyp& h, const Cand& c) {
   return c.mask & hyp_probe_bits(h.jmask, h.imask, (h.imask & F_WI) != 0) & DQ_ALL;
 }
 
+// The dense class-3 table in LDS: row d3_index(t_j), column d3_index(t_k)
+// XOR the row, so that lanes reading one t_k under different t_j (a common
+// tag after several hypotheses' tags) hit different banks (ds_read_b64:
+// bank pair = element index mod 32, which unswizzled was the column alone).
+#ifndef LT_D3_SWIZZLE
+#define LT_D3_SWIZZLE 1                 // 0: the unswizzled layout (A/B builds)
+#endif
+__device__ __forceinline__ uint32_t d3_lds(uint32_t jtag, uint32_t ktag, uint32_t mul) {
+  const uint32_t r = d3_index(jtag, mul);
+  return (r << D3_BITS) | (d3_index(ktag, mul) ^ (LT_D3_SWIZZLE ? r : 0u));
+}
+// copy the host-layout table src (row-major) into the swizzled LDS layout
+__device__ __forceinline__ void d3_stage(const double* __restrict__ src, double* dst) {
+  for (int i = threadIdx.x; i < D3_DIM * D3_DIM; i += blockDim.x) {
+    const int r = i >> D3_BITS, c = i & (D3_DIM - 1);
+    dst[(r << D3_BITS) | (c ^ (LT_D3_SWIZZLE ? r : 0))] = src[i];
+  }
+}
+
 // Stage the LDS parts of the model (all threads of the block, before any
 // early exit): the dense class-3 table when the model has one.
 template <bool NARROW>
 __device__ __forceinline__ Aux stage_aux(const DecodeParams& p, double* d3l) {
   Aux a;
-  if (p.d3) {
-    const uint4* src = reinterpret_cast<const uint4*>(p.d3);
-    uint4* dst = reinterpret_cast<uint4*>(d3l);
-    for (int i = threadIdx.x; i < D3_DIM * D3_DIM / 2; i += blockDim.x) dst[i] = src[i];
-  }
+  if (p.d3) d3_stage(p.d3, d3l);
   if (p.d3) __syncthreads();
   a.d3 = p.d3 ? d3l : nullptr;
   a.d3mul = p.d3mul;
@@ -377,7 +394,7 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW, BOTH>& P, const Bufs& 
   const Keys K = make_keys(h, c, use_j8_of(h, c));
   uint32_t gneed = need, lpres = 0;
   if (aux.d3 && ((need >> 3) & 1u)) {        // class 3 from the dense LDS table
-    const double v = aux.d3[d3_index(h.jtag, aux.d3mul) * D3_DIM + d3_index(c.tag, aux.d3mul)];
+    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3mul)];
     P.s1[3].coef = v;
     gneed &= ~8u;
     lpres |= (__builtin_bit_cast(uint64_t, v) != D3_ABSENT) ? 8u : 0u;
@@ -497,8 +514,14 @@ __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_
 // edge from wj (local node jl) to the candidate gn.  unk_d > 0: the candidate
 // is the implicit Unknown of that span length (its post terms from p.unk_post;
 // a batch with implicit Unknowns has no edge terms).
+// GEN = false: the composite has no term after the trigram (p.n_post == 0,
+// p.n_edge == 0; launch_k picks it), so inc = pre + tri and the kernel keeps
+// none of the post / edge arrays or their loops live (round 6: the k=1
+// kernel's SGPR spills 43 -> 6, their v_readlane restores out of the loop).
+template <bool GEN = true>
 __device__ __forceinline__ double increment(const DecodeParams& p, const Cand& c, double tri,
                                             uint32_t gn, uint32_t jl, int unk_d = 0) {
+  if constexpr (!GEN) return c.pre + tri;
   if (p.n_edge == 0) {
     double inc = c.pre + tri;
     for (int t = 0; t < p.n_post; ++t)
@@ -597,7 +620,7 @@ __device__ __forceinline__ void v1_issue(V1Probe<NARROW>& P, const Bufs& B, uint
   uint32_t gneed = need, pres = 0;
   P.cf[3] = -0.0;
   if (aux.d3 && ((need >> 3) & 1u)) {        // class 3 from the dense LDS table
-    const double v = aux.d3[d3_index(h.jtag, aux.d3mul) * D3_DIM + d3_index(c.tag, aux.d3mul)];
+    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3mul)];
     const bool present = __builtin_bit_cast(uint64_t, v) != D3_ABSENT;
     P.cf[3] = present ? v : -0.0;
     pres = present ? 8u : 0u;
@@ -712,7 +735,7 @@ __device__ __forceinline__ void bm_issue(BMProbe<NARROW>& P, const Bufs& B, uint
   P.cf3 = -0.0;
   P.pres3 = 0;
   if (aux.d3 && ((need >> 3) & 1u)) {
-    const double v = aux.d3[d3_index(h.jtag, aux.d3mul) * D3_DIM + d3_index(c.tag, aux.d3mul)];
+    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3mul)];
     const bool present = __builtin_bit_cast(uint64_t, v) != D3_ABSENT;
     P.cf3 = present ? v : -0.0;
     P.pres3 = present ? 8u : 0u;
@@ -830,6 +853,9 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #endif
 #ifndef PK_WPB
 #define PK_WPB 8                        // (one dense class-3 table and pair table per 8 waves)
+#endif
+#ifndef PK_PAIR_MAX
+#define PK_PAIR_MAX 0                   // 1: lane pairs compare in registers before the LDS max (A/B)
 #endif
 #ifndef PK_DMA_AUX
 #define PK_DMA_AUX 2                    // k=1 record DMA nontemporal (streamed once): 0.771 -> 0.766 ms
@@ -1142,7 +1168,7 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
   }
 }
 
-template <int W, bool NARROW, bool COUNT>
+template <int W, bool NARROW, bool COUNT, bool GEN = true>
 __global__ void __launch_bounds__(64 * k1_wpb<NARROW>(), (NARROW && W <= 8) ? PK_WAVES : 3)
 lt_viterbi_pk(DecodeParams p) {
   constexpr int BPL = PK_BPL;                   // end positions whose backpointer stays in LDS
@@ -1288,7 +1314,7 @@ lt_viterbi_pk(DecodeParams p) {
       v1_second<NARROW>(P, h1, cur);
       const double tri = has_tri ? v1_sum(P.cf, P.pres, cur, h1) : 0.0;
       if (COUNT) v_count(cnt, h1, cur, need, __builtin_popcount(P.gneed) + __builtin_popcount(P.need2));
-      best_s = h1.score + increment(p, cur, tri, gn0, h1.jnode, imp ? d0 : 0);   // beam.py:115
+      best_s = h1.score + increment<GEN>(p, cur, tri, gn0, h1.jnode, imp ? d0 : 0);   // beam.py:115
     }
 
     // per-sentence argmax over the macro-steps of e (beam.py:112-116): max
@@ -1302,7 +1328,23 @@ lt_viterbi_pk(DecodeParams p) {
     // it (earlier steps hold smaller positions).
     PK_STAMP(6);                                 // [6] numpy-order sum, increment
     const uint32_t gk = (uint32_t)t * 64u + (uint32_t)lane;
+#if PK_PAIR_MAX
+    // lanes (l, l ^ 1) of one sentence first compare in registers (a DPP
+    // quad permute): only the better of the two -- on a tie the lower lane,
+    // whose position is smaller -- takes part in the LDS max / min, which
+    // halves the lanes contending for one sentence's LDS word
+    unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
+    {
+      const uint32_t plo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)key, 0xB1, 0xF, 0xF, false);
+      const uint32_t phi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(key >> 32), 0xB1, 0xF, 0xF, false);
+      const int pmsr = __builtin_amdgcn_mov_dpp(msr, 0xB1, 0xF, 0xF, false);
+      const unsigned long long pk = ((unsigned long long)phi << 32) | plo;
+      const bool beaten = pmsr == msr && ((lane & 1) ? pk >= key : pk > key);
+      key = beaten ? 0ull : key;
+    }
+#else
     const unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
+#endif
     const unsigned long long mprev = (key && !first) ? amax[wv][cb][msr] : 0ull;
     if (key) __hip_atomic_fetch_max(&amax[wv][cb][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const unsigned long long mk = key ? amax[wv][cb][msr] : 0ull;
@@ -1341,8 +1383,10 @@ lt_viterbi_pk(DecodeParams p) {
     const VEntry& f = R[lane][nw % RING];
     p.out_count[sid] = 1;
     p.out_score[sid] = f.score + 0.0;
-    p.out_len[sid] = (int32_t)f.depth;
-    pdepth = min((int)f.depth, nw);
+    // (depth <= n on a consistent beam: the unsigned clamp keeps a corrupted
+    // entry from sending the stores below out of the sentence's code rows)
+    pdepth = (int)min(f.depth, (uint32_t)nw);
+    p.out_len[sid] = (int32_t)pdepth;
     int32_t* codes = p.out_codes + cumn;
     const uint32_t* bpg = p.bp + p.bp_off[sid];
     int pos = nw;
@@ -1352,7 +1396,7 @@ lt_viterbi_pk(DecodeParams p) {
     // of LDS reads only, so its stores are never waited for (one loop reading
     // either memory compiles to a flat load, whose wait covers the stores of
     // the step before -- a store round trip per path word)
-    int step = min((int)f.depth, nw) - 1;
+    int step = pdepth - 1;
     for (; step >= 0 && pos >= BPL; --step) {
       const uint32_t v = bpg[(int64_t)pos * bstride];
       codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
@@ -1422,13 +1466,13 @@ __device__ __forceinline__ Hyp read_entry(const Entry& e) {
 constexpr int P_W = K1_W;
 static_assert(P_W <= 8, "k=1 schedule entries hold the sentence in 3 bits");
 
-template <int W, bool NARROW, bool COUNT>
+template <int W, bool NARROW, bool COUNT, bool GEN = true>
 hipError_t launch_pk(const DecodeParams& p, const Launch& L) {
   constexpr int P_WPB = k1_wpb<NARROW>();
   constexpr int SPB = W * P_WPB;
   const int blocks = (p.n_sent + SPB - 1) / SPB;
   if (blocks == 0) return hipSuccess;
-  hipExtLaunchKernelGGL((lt_viterbi_pk<W, NARROW, COUNT>), dim3(blocks), dim3(64 * P_WPB), 0, L.st, L.e0, L.e1, 0, p);
+  hipExtLaunchKernelGGL((lt_viterbi_pk<W, NARROW, COUNT, GEN>), dim3(blocks), dim3(64 * P_WPB), 0, L.st, L.e0, L.e1, 0, p);
   return hipGetLastError();
 }
 
@@ -1562,7 +1606,7 @@ __device__ __forceinline__ void copy_codes(int32_t* __restrict__ out, const int3
   for (int q = li; q < words; q += NL) out[q] = lco[q];
 }
 
-template <int KT, int WPB, bool NARROW, bool COUNT>
+template <int KT, int WPB, bool NARROW, bool COUNT, bool GEN = true>
 __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PK_WPE(KT, NARROW), 8)))
 lt_beam_pk(DecodeParams p) {
   constexpr int RPC = KT <= 16 ? 2 : 4;         // scoring rounds per chunk
@@ -1771,7 +1815,7 @@ lt_beam_pk(DecodeParams p) {
         if (!skip) {
           const double tri = has_tri ? v1_sum(cf, pres, c, h1) : 0.0;
           if (COUNT) v_count(cnt, h1, c, need, 2 * __builtin_popcount(P.gneed));
-          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
+          const double sc = h1.score + increment<GEN>(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
           myg[t] = (uint32_t)g;
         }
@@ -2034,11 +2078,11 @@ lt_beam_pk(DecodeParams p) {
   }
 }
 
-template <int KT, int WPB, bool NARROW, bool COUNT>
+template <int KT, int WPB, bool NARROW, bool COUNT, bool GEN = true>
 hipError_t launch_bp(const DecodeParams& p, const Launch& L) {
   const int blocks = (p.n_sent + WPB - 1) / WPB;
   if (blocks == 0) return hipSuccess;
-  hipExtLaunchKernelGGL((lt_beam_pk<KT, WPB, NARROW, COUNT>), dim3(blocks), dim3(64 * WPB), 0, L.st, L.e0, L.e1, 0, p);
+  hipExtLaunchKernelGGL((lt_beam_pk<KT, WPB, NARROW, COUNT, GEN>), dim3(blocks), dim3(64 * WPB), 0, L.st, L.e0, L.e1, 0, p);
   return hipGetLastError();
 }
 
@@ -2053,7 +2097,7 @@ hipError_t launch_bp(const DecodeParams& p, const Launch& L) {
 // within a group; top-k is lt_beam_pk's exact rank counting and threshold
 // pruning, per group.
 // ---------------------------------------------------------------------------
-template <int KT, int G, int WPB, bool NARROW>
+template <int KT, int G, int WPB, bool NARROW, bool GEN = true>
 // (wide keys at KT = 4, G = 32: 3 waves per SIMD would spill 4 VGPRs -- 2)
 __global__ void __launch_bounds__(64 * WPB)
 __attribute__((amdgpu_waves_per_eu(((G == 16 && KT > 2) || (!NARROW && KT == 4)) ? 2 : 3, 3)))
@@ -2302,7 +2346,7 @@ lt_beam_hw(DecodeParams p) {
         const VEntry h1 = R[hb][hr];
         const double tri = has_tri ? bm_score<NARROW>(P, h1, c) : 0.0;
         if (!skip) {
-          const double sc = h1.score + increment(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
+          const double sc = h1.score + increment<GEN>(p, c, tri, nbase + (uint32_t)node, h1.jnode, imp ? d : 0);   // beam.py:115
           myk[t] = ord_key(sc);
           // the list entry's payload: the expansion as its backpointer word
           // (ranks are by list position, so nothing reads g itself; the
@@ -2488,12 +2532,12 @@ lt_beam_hw(DecodeParams p) {
 #endif
 }
 
-template <int KT, int G, int WPB, bool NARROW>
+template <int KT, int G, int WPB, bool NARROW, bool GEN = true>
 hipError_t launch_hw(const DecodeParams& p, const Launch& L) {
   constexpr int SPB = (64 / G) * WPB;
   const int blocks = (p.n_sent + SPB - 1) / SPB;
   if (blocks == 0) return hipSuccess;
-  hipExtLaunchKernelGGL((lt_beam_hw<KT, G, WPB, NARROW>), dim3(blocks), dim3(64 * WPB), 0, L.st, L.e0, L.e1, 0, p);
+  hipExtLaunchKernelGGL((lt_beam_hw<KT, G, WPB, NARROW, GEN>), dim3(blocks), dim3(64 * WPB), 0, L.st, L.e0, L.e1, 0, p);
   return hipGetLastError();
 }
 
@@ -2513,9 +2557,7 @@ __global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
   __shared__ double d3l[D3_DIM * D3_DIM];
   Aux aux{nullptr, p.d3mul, p.hk};
   if (p.d3) {
-    const uint4* src = reinterpret_cast<const uint4*>(p.d3);
-    uint4* dst = reinterpret_cast<uint4*>(d3l);
-    for (int i = threadIdx.x; i < D3_DIM * D3_DIM / 2; i += blockDim.x) dst[i] = src[i];
+    d3_stage(p.d3, d3l);
     __syncthreads();
     aux.d3 = d3l;
   }
@@ -2581,6 +2623,21 @@ __global__ void __launch_bounds__(256) lt_eval_paths_k(EvalParams p) {
 
 template <bool NARROW, bool COUNT>
 hipError_t launch_k(const DecodeParams& p, int kt, const Launch& L) {
+  // the composite's usual shape (node-local terms, then the trigram, nothing
+  // after it) takes the kernels without the post / edge term code (GEN =
+  // false; narrow keys, the tuned beams up to 32)
+  if constexpr (NARROW && !COUNT) {
+    if (p.n_post == 0 && p.n_edge == 0) switch (kt) {
+      case 1: return launch_pk<P_W, NARROW, COUNT, false>(p, L);
+      case 2: if (beam_group_lanes(p.k) == 16) return launch_hw<2, 16, HW_WPB, NARROW, false>(p, L); break;
+      case 4: return beam_group_lanes(p.k) == 16 ? launch_hw<4, 16, HW_WPB, NARROW, false>(p, L)
+                                                  : launch_hw<4, 32, HW_WPB, NARROW, false>(p, L);
+      case 8: return launch_hw<8, 32, HW8_WPB, NARROW, false>(p, L);
+      case 16: return launch_bp<16, BP16_WPB, NARROW, COUNT, false>(p, L);
+      case 32: return launch_bp<32, BP32_WPB, NARROW, COUNT, false>(p, L);
+      default: break;
+    }
+  }
   if (kt == 1) return launch_pk<P_W, NARROW, COUNT>(p, L);
   // k = 2..8: lane groups (16 lanes for k <= 3, 32 above); the operation
   // counts of those beams come from lt_beam_pk's COUNT variant (one sentence

@@ -85,6 +85,7 @@ struct lt_batch {
   // beam-1 decode -- lazy_sched: then in buffers of their own, not the
   // arena); prep_done = the fill kernels are queued
   bool has_sched = false, prep_done = false, lazy_sched = false;
+  double host_sched_ms = 0.0;          // lt_batch_create's host schedule pass (wall time)
   hipEvent_t prep_ev0 = nullptr, prep_ev1 = nullptr;   // around the last fill
   // device inputs, per launch piece (lt_batch_create: node records and
   // backpointers of a piece stay below 2^31 B)

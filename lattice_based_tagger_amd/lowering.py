@@ -158,6 +158,7 @@ class LoweredModel:
                     % (name, ', '.join(NODE_LOCAL_SCORERS), TRIGRAM_SCORER))
         if len(self.plan) > MAX_TERMS:
             raise NotImplementedError('more than %d scorers after the leading node-local ones' % MAX_TERMS)
+        _warn_slow_path(self)
         self.vocab = {}
         self.vmask = np.zeros(1, dtype=np.uint32)
         self.keys = np.zeros((0, 4), dtype=np.uint32)
@@ -287,6 +288,34 @@ class LoweredModel:
         return (None if i4 is None else float(coef[i4]),
                 None if i5 is None else float(coef[i5]),
                 None if i6 is None else float(coef[i6]))
+
+
+_WARNED = set()
+
+
+def _warn_slow_path(model):
+    """One warning per composite shape whose plugins take the slow host path
+    (INTEGRATION.md "edge-local plugins"): an edge_local plugin is evaluated in
+    Python once per lattice edge, and any user plugin turns the implicit
+    Unknown records off (every Unknown a node record of its own, about 3.5x
+    the records on dictionary lattices) and the native packer off (the Python
+    packer, about 70x slower).  The decode itself stays on the device."""
+    user = [type(f).__name__ for f in list(model.pre_funcs) + list(model.post_funcs)
+            if type(f).__name__ not in NODE_LOCAL_SCORERS]
+    edge = [type(f).__name__ for f in model.edge_funcs]
+    if not (user or edge):
+        return
+    sig = (tuple(user), tuple(edge))
+    if sig in _WARNED:
+        return
+    _WARNED.add(sig)
+    import warnings
+    what = ', '.join(['%s (edge_local)' % n for n in edge] + ['%s (node_local)' % n for n in user])
+    warnings.warn('lattice_based_tagger_amd: scorer plugin(s) %s: packed by the Python packer%s, '
+                  'without implicit Unknown records (each Unknown its own node record); the decode '
+                  'stays on the GPU, the host packing is about 70x slower than the native packer'
+                  % (what, ', their values evaluated per lattice edge in Python' if edge else ''),
+                  RuntimeWarning, stacklevel=4)
 
 
 def lower_scorers(score_functions):

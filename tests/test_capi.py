@@ -16,7 +16,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 def declared_symbols():
     text = open(HEADER).read()
     text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
-    return sorted(set(re.findall(r'\b(lt_[a-z_]+)\s*\(', text)))
+    return sorted(set(re.findall(r'\b(lt_[a-z0-9_]+)\s*\(', text)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,15 +1,18 @@
-"""Multi-process (gloo, world_size 2, CPU) coverage of the sharding path: shard
+"""Multi-process (world_size 2 and 3, CPU) coverage of the sharding path: shard
 ranges tile the batch, per-rank decodes of the shards reassemble to the
-single-process decode, and the host group's barrier/max/sum/gather work.
-The per-rank decode here is the C restatement (oracle) standing in for the
-device, which the CPU container does not have."""
+single-process decode, and the torch-free host group's (dist.HostGroup, TCP)
+barrier/max/sum/gather/id broadcast work.  The processes are started with the
+standard library's multiprocessing and never import torch.  The per-rank
+decode here is the C restatement (oracle) standing in for the device, which
+the CPU container does not have."""
 
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+import multiprocessing as mp
+import sys
 
 from lattice_based_tagger_amd import dist, synth
 
@@ -49,12 +52,13 @@ def _worker(rank, world, port, out_q):
     mine = (lo, hi, count[lo:hi].copy(), length[lo:hi].copy(), score[lo:hi].copy(),
             codes[2 * cum[lo]:2 * cum[hi]].copy())
     g.barrier()
+    no_torch = 'torch' not in sys.modules
     total = g.sum(float(hi - lo))
     mx = g.max(float(rank))
     parts = g.gather(mine)
     if rank == 0:
         full = lt_oracle.decode(packed, keys, coefs, 2)
-        ok = total == len(packed.sent_n) and mx == world - 1
+        ok = total == len(packed.sent_n) and mx == world - 1 and no_torch
         got_count = np.concatenate([p[2] for p in parts])
         got_len = np.concatenate([p[3] for p in parts])
         got_score = np.concatenate([p[4] for p in parts])
@@ -66,7 +70,7 @@ def _worker(rank, world, port, out_q):
     g.close()
 
 
-def test_two_rank_gloo_shards_reassemble():
+def test_two_rank_host_group_shards_reassemble():
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -86,12 +90,14 @@ def _id_worker(rank, world, port, out_q):
     d = bench.Dist(world)
     uid = bytes(range(128)) if rank == 0 else None       # stands in for lt_comm_unique_id()
     got = d.broadcast_bytes(uid)
-    out_q.put((rank, got == bytes(range(128)), d.max(float(rank)), d.sum(1.0)))
+    out_q.put((rank, got == bytes(range(128)), d.max(float(rank)), d.sum(1.0), d.min(float(rank)),
+               'torch' not in sys.modules))
     d.close()
 
 
 def test_bench_dist_shares_the_communicator_id():
-    """bench.py's host group hands rank 0's RCCL id to every rank (gloo)."""
+    """bench.py's host group hands rank 0's RCCL id to every rank (TCP, no
+    torch imported)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -102,7 +108,7 @@ def test_bench_dist_shares_the_communicator_id():
         p.join(timeout=180)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = sorted(q.get(timeout=10) for _ in range(2))
-    assert res == [(0, True, 1.0, 2.0), (1, True, 1.0, 2.0)]
+    assert res == [(0, True, 1.0, 2.0, 0.0, True), (1, True, 1.0, 2.0, 0.0, True)]
 
 
 def _al16(x):
@@ -141,7 +147,7 @@ def _strong_worker(rank, world, port, total, out_q):
     seeded permutations past the generated lattices, as config 4 builds
     it), this rank's shard (``shard_of``), its decode (the C restatement
     standing in for the device), the per-rank results gathered to rank 0
-    (gloo here, RCCL in bench.py) and rank 0's byte-for-byte check against
+    (the TCP host group here, RCCL in bench.py) and rank 0's byte-for-byte check against
     a single-process decode (``check_results``)."""
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -154,14 +160,12 @@ def _strong_worker(rank, world, port, total, out_q):
     lo, hi, piece = bench.shard_of(packed, order, k, world, rank)
     res = lt_oracle.decode(piece, keys, coefs, k)[:4]
     mine = bench.padded_as_packed(res, piece.sent_n, k)
-    g = dist.HostGroup.__new__(dist.HostGroup)
-    g.ranks, g.pg = dist.Ranks(), d.pg
-    parts = g.gather(mine)
+    parts = d.gather(mine)
     # the RCCL path's bytes: every rank's slab (padded to its capacity), laid
     # out by the root at stride cap = the largest capacity, as the receive
     # slot of lt_gather_launch holds them, and read back with lt_slab_parse
     # (lt_gather_view) -- the reassembly that runs only at N > 1 on a node
-    slabs = g.gather(_write_slab(mine, int(np.sum(piece.sent_n))))
+    slabs = d.gather(_write_slab(mine, int(np.sum(piece.sent_n))))
     if rank == 0:
         from lattice_based_tagger_amd import _capi
         ref = bench.padded_as_packed(lt_oracle.decode(packed, keys, coefs, k)[:4], packed.sent_n, k)
