@@ -459,16 +459,23 @@ def _materialise_bulk(*args):
     lattices, the caller's Word list otherwise).  The cyclic GC
     is paused meanwhile: millions of fresh tuples would otherwise trigger
     repeated full collections (4x the construction time)."""
-    enabled = gc.isenabled()
-    gc.disable()
-    try:
-        return _materialise_bulk_body(*args)
-    finally:
-        if enabled:
-            gc.enable()
+    return materialise_prepared(prepare_bulk(*args))
 
 
-def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
+def decode_prepared(packed, views, chars_list, model, k, best_only=False, uploaded=None, decoder=None):
+    """The first half of decode_batch for natively packed lattices, meant for
+    a pipeline's worker thread: the decode (the device; waits release the
+    GIL), the path-node indices and the string coding of their Words (numpy
+    and C calls, no per-word Python objects).  materialise_prepared builds
+    the Sequences from it on the caller's thread."""
+    dec = decoder if decoder is not None else Decoder.get(0)
+    res = dec.decode_packed(model, packed, k, uploaded)
+    return prepare_bulk(packed, views, chars_list, 1 if best_only else k, res, model)
+
+
+def prepare_bulk(packed, objs, chars_list, T, res, model):
+    """Everything of the materialisation but the Python objects (see
+    decode_prepared): a dict materialise_prepared consumes."""
     count, length, score, codes, k = res.count, res.length, res.score, res.codes, res.k
     S = len(chars_list)
     n = np.asarray(packed.sent_n, dtype=np.int64)
@@ -498,18 +505,42 @@ def _materialise_bulk_body(packed, objs, chars_list, T, res, model):
         src[imp] = -2 - ((b << 32) | (d - 1))
         pmask[imp] = np.asarray(packed.unk_mask)[d - 1]
     lat = objs[0].words
-    ext = _pyobj.load()
-    flat = [None] * total
     dic = np.flatnonzero(src >= 0)
     sel = src[dic]
+    # native lattices: the strings coded here, the Words built in C later
+    coded = lat.words_coded(sel) if dic.size and hasattr(lat, 'words_coded') else None
+    unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
+    return dict(packed=packed, chars_list=chars_list, T=T, model=model, count=count, length=length,
+                score=score, n=n, L=L, Lf=Lf, first=first, seg=seg, src=src, pmask=pmask, total=total,
+                lat=lat, dic=dic, sel=sel, coded=coded, unk=unk)
+
+
+def materialise_prepared(prep):
+    """The Sequences of prepare_bulk's result (the GIL-holding half: Word
+    tuples built in C, paths, typed scores).  The cyclic GC is paused (see
+    _materialise_bulk)."""
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        return _materialise_prepared_body(**prep)
+    finally:
+        if enabled:
+            gc.enable()
+
+
+def _materialise_prepared_body(packed, chars_list, T, model, count, length, score, n, L, Lf, first, seg, src,
+                               pmask, total, lat, dic, sel, coded, unk):
+    ext = _pyobj.load()
+    flat = [None] * total
     # native lattices build their Words in C; Word lists hand back the
     # caller's own objects (as the reference's paths hold them)
     if dic.size:
-        if hasattr(lat, 'words_into'):
+        if coded is not None:
+            lat.words_from_coded(flat, dic, coded)
+        elif hasattr(lat, 'words_into'):
             lat.words_into(flat, dic, sel)
         else:
             ext.scatter(flat, dic, [lat[i] for i in sel.tolist()])
-    unk = np.flatnonzero(src < 0)                      # synthesised Unknown nodes (BOS never on a path)
     if unk.size:
         code = -2 - src[unk]
         if hasattr(chars_list, 'cps'):                  # native lattices: straight from their UTF-32 buffer

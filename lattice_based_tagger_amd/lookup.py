@@ -414,9 +414,23 @@ class NativeLattices:
         decoded once, plus an int32 code per node), so a path's repeated tags
         and words share str objects; the Word tuples are built in C
         (`_ltpy.words`, csrc/lt_pyobj.c)."""
+        self.words_from_coded(out, pos, self.words_coded(idx))
+
+    def words_from_coded(self, out, pos, coded):
+        """The object-building half of words_into (holds the GIL)."""
+        if coded is None:
+            return
+        uniqs, codes_all, ints = coded
+        _pyobj.load().words(Word, out, np.ascontiguousarray(pos, dtype=np.int64), uniqs, codes_all, ints)
+
+    def words_coded(self, idx):
+        """The string-coding half of words_into: every field's distinct
+        strings and per-node codes, and the integer fields (C calls that
+        release the GIL, numpy gathers; no per-node Python objects), so a
+        pipeline can run it on a worker thread ahead of words_from_coded."""
         idx = np.ascontiguousarray(np.asarray(idx, dtype=np.int64))
         if idx.size == 0:
-            return
+            return None
         uniqs, codes_all = [], []
         lib = self.lib                      # (CDLL: the GIL is released during each call)
         # one buffer for the five fields' distinct strings (paths repeat few
@@ -447,8 +461,8 @@ class NativeLattices:
             codes_all.append(codes)
         ints = self._int_columns()
         isl = (ints['is_l'][idx] != 0).view(np.uint8)
-        _pyobj.load().words(Word, out, np.ascontiguousarray(pos, dtype=np.int64), tuple(uniqs), tuple(codes_all),
-                            tuple(ints[f][idx].astype(np.int64) for f in ('len', 'b', 'e')) + (isl,))
+        return (tuple(uniqs), tuple(codes_all),
+                tuple(ints[f][idx].astype(np.int64) for f in ('len', 'b', 'e')) + (isl,))
 
     def empty(self, s):
         """True when sentence s has characters but no node: the reference's

@@ -202,10 +202,13 @@ class Tagger:
         """Best ``Sequence`` per sentence.  Raises IndexError like ``tag``
         when a non-empty sentence has no dictionary node at all
         (`beam.py:32`).  With native lattices the batch runs as a
-        three-stage pipeline over chunks of CHUNK sentences: one worker
-        thread builds and packs chunk i+2 (C++, outside the GIL), a second
-        uploads chunk i+1 (node records, host-to-device copies), while this
-        thread decodes and re-materialises chunk i.  The cyclic GC is paused
+        four-stage pipeline over chunks of CHUNK sentences: one worker
+        thread builds and packs chunk i+3 (C++, outside the GIL), a second
+        uploads chunk i+2 (node records, host-to-device copies), a third
+        decodes chunk i+1 and prepares its paths (path-node indices, the
+        dictionary-coded strings of their Words: numpy and C calls that
+        release the GIL), while this thread builds chunk i's Sequences (the
+        only stage that needs the GIL throughout).  The cyclic GC is paused
         meanwhile (millions of fresh tuples, no cycles)."""
         sents = list(sents)
         lex = self.native_lexicon()
@@ -225,7 +228,8 @@ class Tagger:
     def _tag_native(self, lex, sents, beam_size):
         from collections import deque
         from concurrent.futures import ThreadPoolExecutor
-        from .beam import _check_beam, decode_batch, decoders_for, device_list, lowered_model
+        from .beam import (_check_beam, decode_batch, decode_prepared, decoders_for, device_list, lowered_model,
+                           materialise_prepared)
         from .native_packer import packer_for
         k = _check_beam(beam_size)
         chunks = [sents[i:i + self.CHUNK] for i in range(0, len(sents), self.CHUNK)] or [[]]
@@ -277,28 +281,49 @@ class Tagger:
             dbs = dec.upload(model, packed, k) if dec is not None and packed is not None else None
             return finish(0, lat, packed, views, dbs)
 
+        def decode(i, fut):                        # the decode stage (worker): device + path preparation
+            lat, packed, views, dbs = fut.result()
+            if packed is None or dbs is None:      # (Python-packed composites: the caller decodes)
+                return i, lat, packed, views, dbs, None
+            return i, lat, packed, views, None, decode_prepared(packed, views, lat.chars, model, k,
+                                                                best_only=True, uploaded=dbs,
+                                                                decoder=decoder(i))
+
         out = []
-        with ThreadPoolExecutor(max_workers=1) as builder, ThreadPoolExecutor(max_workers=1) as uploader:
+        with ThreadPoolExecutor(max_workers=1) as builder, ThreadPoolExecutor(max_workers=1) as uploader, \
+                ThreadPoolExecutor(max_workers=1) as decoding:
             stages = deque()
 
             def feed(i):
                 if i < len(chunks):
-                    stages.append(uploader.submit(upload, i, builder.submit(front, chunks[i],
-                                                                            lat0 if i == 0 else None)))
+                    up = uploader.submit(upload, i, builder.submit(front, chunks[i], lat0 if i == 0 else None))
+                    stages.append((up, decoding.submit(decode, i, up)))
             feed(0)
             feed(1)
+            feed(2)
             try:
                 for i in range(len(chunks)):
-                    lat, packed, views, dbs = stages.popleft().result()
-                    feed(i + 2)
-                    out += finish(i, lat, packed, views, dbs)
+                    _, dfut = stages.popleft()
+                    _, lat, packed, views, dbs, prep = dfut.result()
+                    feed(i + 3)
+                    if prep is None:
+                        out += finish(i, lat, packed, views, dbs)
+                    else:
+                        out += [m[0] for m in materialise_prepared(prep)]
             finally:
-                for f in stages:                   # an error: drop what is still in flight
-                    f.cancel()
-                    if not f.cancelled():
+                for up, dfut in stages:            # an error: drop what is still in flight
+                    dfut.cancel()
+                    if dfut.cancelled():           # (its batches were not handed to a decode)
+                        up.cancel()
+                        if not up.cancelled():
+                            try:
+                                for _, _, db in up.result()[3] or ():
+                                    db.close()
+                            except BaseException:
+                                pass
+                    else:
                         try:
-                            for _, _, db in f.result()[3] or ():
-                                db.close()
+                            dfut.result()
                         except BaseException:
                             pass
         return out

@@ -75,6 +75,19 @@ def main():
         del out
     print('materialise best of %d: %.3f s (%d sentences, %d path words)' % (a.reps, best, len(sents),
                                                                         int(res.length[:, 0].sum())))
+    # the two halves Tagger.tag_batch runs on different threads (round 6)
+    from lattice_based_tagger_amd.beam import materialise_prepared, prepare_bulk
+    bp = bm = None
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        prep = prepare_bulk(packed, views, lat.chars, 1, res, model)
+        t1 = time.perf_counter()
+        out = materialise_prepared(prep)
+        t2 = time.perf_counter()
+        bp = t1 - t0 if bp is None else min(bp, t1 - t0)
+        bm = t2 - t1 if bm is None else min(bm, t2 - t1)
+        del out, prep
+    print('  prepare (decode-stage worker) %.3f s, build (caller, GIL) %.3f s' % (bp, bm))
     if a.profile:
         import cProfile
         import pstats
