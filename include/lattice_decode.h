@@ -30,11 +30,19 @@
 extern "C" {
 #endif
 
-#define LT_ABI_VERSION 5   /* 2: compact results (slabs), gathers of slabs;
+#define LT_ABI_VERSION 6   /* 2: compact results (slabs), gathers of slabs;
                               3: any max_len / beam (general kernel), lt_trace.exp_link;
                               4: edge terms (lt_batch_desc.n_edge ...);
                               5: implicit Unknown candidates (lt_batch_desc.n_unk ...),
-                                 negative path codes, lt_batch_reset_prep, lt_batch_prep_ms */
+                                 negative path codes, lt_batch_reset_prep, lt_batch_prep_ms;
+                              6: several trigram terms (lt_batch_desc.n_xtri ..., key
+                                 classes + LT_XTRI_CLASS_STRIDE * t), lt_batch_prepare_k1,
+                                 lt_batch_host_sched_ms */
+/* Several trigram scorers in one composite (score_funcs.py:50-54 sums any
+ * BeamScoreFunctions): scorer t's keys carry class + LT_XTRI_CLASS_STRIDE * t
+ * in the one model; at most LT_MAX_TRI scorers. */
+#define LT_XTRI_CLASS_STRIDE 16
+#define LT_MAX_TRI 8
 #define LT_MAX_SPAN 8      /* span slots per end position (reference max_len default, beam.py:5) */
 #define LT_MAX_BEAM 256    /* largest beam_size of the tuned kernels */
 /* Any other configuration -- max_len > 8 (span slots = max_len) or a beam
@@ -185,6 +193,22 @@ typedef struct {
   const double* unk_f5;
   const double* unk_f6;
   const double* unk_post;         /* [n_post][n_unk] or NULL */
+  /* Further trigram terms (ABI 6): the composite's trigram scorers 1..n_xtri
+   * (the first is the has_trigram term above).  Each is a term of its own,
+   * summed in numpy's order over its own features (score_funcs.py:137-144),
+   * placed by term_kinds: the i-th trigram term (kind 0) is scorer i, so
+   * n_terms / term_kinds are read whenever n_xtri > 0 (as with edge terms).
+   * Per scorer t = 1..n_xtri and node: the pre-filter bits + flags (as
+   * node_mask, under scorer t's features) and its class 4 / 5 / 6
+   * coefficients, at [(t-1) * n_nodes + node].  The model's keys of scorer t
+   * carry class + LT_XTRI_CLASS_STRIDE * t (a wide-slot model).  Such a batch
+   * decodes on the general kernel; not combinable with implicit Unknowns
+   * (n_unk > 0).  n_xtri = 0: one trigram term at most (ABI 5). */
+  int32_t n_xtri;
+  const uint32_t* xtri_mask;      /* [n_xtri][n_nodes] */
+  const double* xtri_f4;          /* [n_xtri][n_nodes] */
+  const double* xtri_f5;
+  const double* xtri_f6;
 } lt_batch_desc;
 
 /* Copies the batch to the device (H2D) and allocates result buffers for
@@ -418,6 +442,10 @@ typedef struct {
   int32_t n_terms;              /* node-local scorers */
   const double* terms;          /* [n_terms * n_words], scorer-major */
   int32_t trigram_pos;          /* position of the trigram scorer among the n_terms + 1; -1 = none */
+  int32_t trigram_scorer;       /* ABI 6: which of the composite's trigram scorers the trigram term is
+                                   (its keys' classes + LT_XTRI_CLASS_STRIDE * trigram_scorer; the
+                                   word records then hold that scorer's masks and class 4-6
+                                   coefficients); 0 = the first */
 } lt_paths_desc;
 /* Blocking: scores[n_paths] (host buffer) receives the totals. */
 lt_status lt_evaluate(lt_ctx* ctx, const lt_model* model, const lt_paths_desc* paths, double* scores);

@@ -13,7 +13,7 @@ import numpy as np
 from ._build import LIB
 
 LT_OK = 0
-ABI_VERSION = 5           # include/lattice_decode.h LT_ABI_VERSION
+ABI_VERSION = 6           # include/lattice_decode.h LT_ABI_VERSION
 LT_MAX_BEAM = 256          # tuned kernels (lattice_decode.h)
 LT_MAX_BEAM_ANY = 1 << 20  # the general kernel lt_beam_wide
 LT_EUNSUPPORTED = -4
@@ -58,7 +58,8 @@ class BatchDesc(C.Structure):
                 ('n_edges', C.c_int64), ('sent_edge_off', C.c_void_p), ('node_edge_base', C.c_void_p),
                 ('edge_val', C.c_void_p), ('n_unk', C.c_int32)] + [
         (f, C.c_void_p) for f in ('unk_word', 'unk_morph0', 'unk_tag', 'unk_mask', 'unk_pre', 'unk_f4',
-                                  'unk_f5', 'unk_f6', 'unk_post')]
+                                  'unk_f5', 'unk_f6', 'unk_post')] + [
+        ('n_xtri', C.c_int32)] + [(f, C.c_void_p) for f in ('xtri_mask', 'xtri_f4', 'xtri_f5', 'xtri_f6')]
 
 
 class Result(C.Structure):
@@ -401,15 +402,22 @@ class DeviceBatch:
             unk = tuple(np.ascontiguousarray(getattr(packed, f), dtype=self.UNK_DTYPES[f])
                         for f in self.UNK_DTYPES) + (
                 np.ascontiguousarray(packed.unk_post, dtype=np.float64) if n_post else None,)
-        self._keep = (post,) + edges + unk
+        n_xtri = int(getattr(packed, 'xtri_n', 0))
+        xtri = ()
+        if n_xtri:                   # further trigram scorers (lattice_decode.h n_xtri, ABI 6)
+            xtri = (np.ascontiguousarray(packed.xtri_mask, dtype=np.uint32),) + tuple(
+                np.ascontiguousarray(getattr(packed, f), dtype=np.float64) for f in ('xtri_f4', 'xtri_f5', 'xtri_f6'))
+        self._keep = (post,) + edges + unk + xtri
+        plan = n_edge or n_xtri      # the term plan is read with edge terms or several trigram terms
         desc = BatchDesc(
             self.n_sent, int(packed.max_len), n_post, int(packed.has_trigram),
             int(arr['node_word'].shape[0]), int(arr['span_start'].shape[0]),
             *[_ptr(arr[f]) for f in self.FIELDS], _ptr(post),
-            n_edge, int(getattr(packed, 'n_terms', 0)) if n_edge else 0,
-            int(getattr(packed, 'term_kinds', 0)) if n_edge else 0,
+            n_edge, int(getattr(packed, 'n_terms', 0)) if plan else 0,
+            int(getattr(packed, 'term_kinds', 0)) if plan else 0,
             int(edges[2].shape[1]) if n_edge else 0, *[_ptr(x) for x in edges],
-            n_unk, *([_ptr(x) for x in unk] if n_unk else [None] * 9))
+            n_unk, *([_ptr(x) for x in unk] if n_unk else [None] * 9),
+            n_xtri, *([_ptr(x) for x in xtri] if n_xtri else [None] * 4))
         self.n_unk = n_unk
         h = C.c_void_p()
         check(ctx._lib.lt_batch_create(ctx.handle, C.byref(desc), int(max_k), C.byref(h)))

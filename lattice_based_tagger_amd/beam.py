@@ -369,8 +369,7 @@ def path_score_type(model, path):
     the lowered composite: the increments' values replayed on the host
     (node-local and edge plugins evaluated, trigram presence from the
     encoder), in constructor order (score_funcs.py:50-54)."""
-    from .lowering import KIND_EDGE, EdgeSequence
-    enc = model.trigram.encoder if model.trigram is not None else None
+    from .lowering import KIND_EDGE, KIND_TRI, EdgeSequence
     acc = 0
     for q in range(1, len(path)):
         wk, wj = path[q], path[q - 1]
@@ -379,8 +378,8 @@ def path_score_type(model, path):
         for f in model.pre_funcs:
             inc = inc + f.score(None, wk)
         for kind, f in model.plan:
-            if f is model.trigram:
-                inc = inc + (np.float64(0.0) if enc.encode_word(wi, wj, wk) else 0)
+            if kind == KIND_TRI:                # (each trigram scorer's own encoder)
+                inc = inc + (np.float64(0.0) if f.encoder.encode_word(wi, wj, wk) else 0)
             elif kind == KIND_EDGE:
                 inc = inc + f.score(EdgeSequence(wj), wk)
             else:

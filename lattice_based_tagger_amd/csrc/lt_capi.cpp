@@ -298,6 +298,7 @@ bool cuckoo_build(const std::vector<KeyRec>& keys, uint32_t slots, uint32_t seed
 extern "C" {
 
 int lt_abi_version(void) { return LT_ABI_VERSION; }
+static_assert(LT_XTRI_CLASS_STRIDE == XTRI_CLASS_STRIDE && LT_MAX_TRI == MAX_TRI, "lt_common.h vs lattice_decode.h");
 uint32_t lt_hash_version(void) { return HASH_VERSION; }
 
 const char* lt_last_error(void) { return g_err.c_str(); }
@@ -435,6 +436,7 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
   if (!img) return fail(LT_ENOMEM, "lt_model_create: out of host memory");
   std::vector<KeyRec>& keys = img->keys;
   uint32_t max_id = 0;
+  bool any_x = false;                         // keys of a further trigram scorer: wide slots
   try {
     keys.resize((size_t)d->n_keys);
   } catch (...) {
@@ -443,10 +445,14 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
   for (int64_t i = 0; i < d->n_keys; ++i) {
     const uint32_t a = d->keys[4 * i], b = d->keys[4 * i + 1], cc = d->keys[4 * i + 2],
                    cls = d->keys[4 * i + 3];
-    if (!(cls <= 3 || cls == 7 || cls == 8))
-      return fail(LT_EINVAL, "lt_model_create: key %lld has class %u (only 0,1,2,3,7,8 are probed)",
-                  (long long)i, cls);
-    const bool two = (cls == 1 || cls == 3 || cls == 8);
+    // class + LT_XTRI_CLASS_STRIDE * t: trigram scorer t of the composite
+    const uint32_t base = cls % LT_XTRI_CLASS_STRIDE, scorer = cls / LT_XTRI_CLASS_STRIDE;
+    if (!(base <= 3 || base == 7 || base == 8) || scorer >= LT_MAX_TRI)
+      return fail(LT_EINVAL, "lt_model_create: key %lld has class %u (only 0,1,2,3,7,8 are probed, "
+                             "+ %d per further trigram scorer, at most %d scorers)",
+                  (long long)i, cls, LT_XTRI_CLASS_STRIDE, LT_MAX_TRI);
+    if (scorer > 0) any_x = true;
+    const bool two = (base == 1 || base == 3 || base == 8);
     if (a == 0 || b == 0 || (two ? cc != 0 : cc == 0))
       return fail(LT_EINVAL, "lt_model_create: key %lld has a bad component id", (long long)i);
     if (std::isnan(d->coefs[i]))
@@ -454,7 +460,9 @@ lt_status lt_image_build(const lt_model_desc* d, lt_image** out) {
     keys[(size_t)i] = KeyRec{a, b, cc, cls, d->coefs[i]};
     max_id = std::max(max_id, std::max(a, std::max(b, cc)));
   }
-  const bool narrow = max_id < (1u << NARROW_ID_BITS);
+  // (the narrow key holds a 3-bit class code: a further scorer's classes
+  // need the wide slot)
+  const bool narrow = max_id < (1u << NARROW_ID_BITS) && !any_x;
   const int64_t slot_bytes = narrow ? (int64_t)sizeof(SlotN) : (int64_t)sizeof(SlotW);
   // load factor <= 0.45 (LT_TABLE_LOAD: a lower bound for table-size
   // experiments -- fewer keys displaced to their secondary slot, so fewer
@@ -614,17 +622,28 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
     return fail(LT_EINVAL, "batch: NULL node arrays");
   if (d->n_post > 0 && !d->node_post) return fail(LT_EINVAL, "batch: NULL node_post");
   if (d->n_edge < 0) return fail(LT_EINVAL, "batch: negative n_edge");
-  if (d->n_edge > 0) {
-    // the term plan: every node_post row, every edge row and the trigram (when
-    // the batch has one) exactly once
+  if (d->n_xtri < 0 || d->n_xtri >= LT_MAX_TRI)
+    return fail(LT_EUNSUPPORTED, "batch: n_xtri %d not in 0..%d", d->n_xtri, LT_MAX_TRI - 1);
+  if (d->n_xtri > 0) {
+    if (!d->has_trigram) return fail(LT_EINVAL, "batch: n_xtri > 0 without the first trigram term");
+    if (d->n_unk != 0) return fail(LT_EUNSUPPORTED, "batch: implicit Unknowns (n_unk) with several trigram terms");
+    if (d->n_nodes > 0 && (!d->xtri_mask || !d->xtri_f4 || !d->xtri_f5 || !d->xtri_f6))
+      return fail(LT_EINVAL, "batch: NULL xtri arrays");
+  }
+  if (d->n_edge > 0 || d->n_xtri > 0) {
+    // the term plan: every node_post row, every edge row and every trigram
+    // term (when the batch has them) exactly once
     if (d->n_terms < 1 || d->n_terms > 32) return fail(LT_EINVAL, "batch: n_terms %d not in 1..32", d->n_terms);
     if (d->n_terms < 32 && (d->term_kinds >> (2 * d->n_terms)) != 0)
       return fail(LT_EINVAL, "batch: term_kinds has bits past n_terms");
     int kinds[4] = {0, 0, 0, 0};
     for (int t = 0; t < d->n_terms; ++t) ++kinds[(d->term_kinds >> (2 * t)) & 3u];
-    if (kinds[3] || kinds[1] != d->n_post || kinds[2] != d->n_edge || kinds[0] != (d->has_trigram ? 1 : 0))
-      return fail(LT_EINVAL, "batch: term_kinds does not list the trigram, the %d node_post rows and the %d "
-                             "edge rows once each", d->n_post, d->n_edge);
+    if (kinds[3] || kinds[1] != d->n_post || kinds[2] != d->n_edge ||
+        kinds[0] != (d->has_trigram ? 1 + d->n_xtri : 0))
+      return fail(LT_EINVAL, "batch: term_kinds does not list the %d trigram terms, the %d node_post rows and the %d "
+                             "edge rows once each", d->has_trigram ? 1 + d->n_xtri : 0, d->n_post, d->n_edge);
+  }
+  if (d->n_edge > 0) {
     if (!d->sent_edge_off || (d->n_nodes > 0 && !d->node_edge_base) || (d->n_edges > 0 && !d->edge_val))
       return fail(LT_EINVAL, "batch: NULL edge arrays");
     if (d->sent_edge_off[0] != 0 || d->sent_edge_off[d->n_sent] != d->n_edges || d->n_edges < 0)
@@ -743,6 +762,13 @@ static lt_status validate(const lt_batch_desc* d, int* inf_signs) {
   for (int64_t i = 0; d->n_edge > 0 && i < (int64_t)d->n_edge * d->n_edges; ++i) {
     if (std::isnan(d->edge_val[i])) return fail(LT_EUNSUPPORTED, "batch: NaN edge term %lld", (long long)i);
     signs |= inf_sign_bits(d->edge_val[i]);
+  }
+  for (int64_t i = 0; i < (int64_t)d->n_xtri * d->n_nodes; ++i) {
+    const double v[3] = {d->xtri_f4[i], d->xtri_f5[i], d->xtri_f6[i]};
+    for (double x : v) {
+      if (std::isnan(x)) return fail(LT_EUNSUPPORTED, "batch: NaN trigram coefficient of node entry %lld", (long long)i);
+      signs |= inf_sign_bits(x);
+    }
   }
   if (signs == 3)
     return fail(LT_EUNSUPPORTED, "batch: both +inf and -inf among the node score terms (their sum is a NaN, "
@@ -901,7 +927,11 @@ static T* at(char* base, size_t off) {
 static std::atomic<int64_t> g_piece_bytes{((int64_t)1 << 31) - 1};
 
 // Backpointer words per (position, rank): two for the general kernel.
-static int bp_words(int max_len, int max_k) { return decode_is_wide(max_len, max_k) ? 2 : 1; }
+static int bp_words(int max_len, int max_k, int n_xtri = 0) {
+  return (decode_is_wide(max_len, max_k) || n_xtri > 0) ? 2 : 1;
+}
+// the general kernel decodes every beam of a batch with further trigram terms
+static bool batch_wide(const lt_batch* b, int k) { return decode_is_wide(b->max_len, k) || b->n_xtri > 0; }
 
 static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc* d, int max_k) {
   const int64_t lim = g_piece_bytes.load();
@@ -910,7 +940,7 @@ static std::vector<std::pair<int32_t, int32_t>> piece_ranges(const lt_batch_desc
   int64_t nodes = 0, bp = 0;
   for (int32_t s = 0; s < d->n_sent; ++s) {
     const int64_t sn = (d->sent_node_off[s + 1] - d->sent_node_off[s]) * (int64_t)sizeof(NodeRec);
-    const int64_t sb = ((int64_t)d->sent_n[s] + 1) * max_k * 4 * bp_words(d->max_len, max_k);
+    const int64_t sb = ((int64_t)d->sent_n[s] + 1) * max_k * 4 * bp_words(d->max_len, max_k, d->n_xtri);
     if (s > s0 && (nodes + sn > lim || bp + sb > lim)) {
       out.emplace_back(s0, s);
       s0 = s;
@@ -957,7 +987,7 @@ static hipError_t prep_fill(lt_batch* b, hipStream_t st) {
 // the schedule in buffers of its own; prep_fill then fills it as for a beam-1
 // batch.
 static lt_status lazy_sched(lt_ctx* c, lt_batch* b) {
-  if (b->has_sched || b->max_len > MAX_SPAN) return LT_OK;
+  if (b->has_sched || b->max_len > MAX_SPAN || b->n_xtri > 0) return LT_OK;
   // every buffer in locals first, published to the pieces only once all of
   // them exist (a failure frees what it allocated: a later decode retries
   // from scratch, nothing leaks)
@@ -1068,8 +1098,9 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   b->n_post = d->n_post;
   b->has_tri = d->has_trigram ? 1 : 0;
   b->n_edge = d->n_edge;
-  b->n_terms = d->n_edge ? d->n_terms : 0;
-  b->term_kinds = d->n_edge ? d->term_kinds : 0;
+  b->n_xtri = d->n_xtri;
+  b->n_terms = (d->n_edge || d->n_xtri) ? d->n_terms : 0;
+  b->term_kinds = (d->n_edge || d->n_xtri) ? d->term_kinds : 0;
   b->max_k = max_k;
   b->n_nodes = d->n_nodes;
   b->n_span = d->n_span;
@@ -1113,7 +1144,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       node_off[q][s] = d->sent_node_off[s0 + s] - pc.node0;
       span_off[q][s] = d->sent_span_off[s0 + s] - pc.span0;
       pcum[q][s] = cum_n[s0 + s] - pc.chars0;
-      if (s < n) bp_off[q][s + 1] = bp_off[q][s] + (int64_t)(d->sent_n[s0 + s] + 1) * max_k * bp_words(d->max_len, max_k);
+      if (s < n) bp_off[q][s + 1] = bp_off[q][s] + (int64_t)(d->sent_n[s0 + s] + 1) * max_k * bp_words(d->max_len, max_k, d->n_xtri);
     }
     pc.bp_entries = bp_off[q][n];
     b->bp_entries += pc.bp_entries;
@@ -1124,7 +1155,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   // arena; its entries are filled on the device (prep_fill).  A batch created
   // for larger beams carries none (no host counting, no arena bytes); a k=1
   // decode of it runs on the lane-group beam kernel (launch_decode)
-  b->has_sched = d->max_len <= MAX_SPAN && max_k == 1;
+  b->has_sched = d->max_len <= MAX_SPAN && max_k == 1 && d->n_xtri == 0;
   b->n_unk = d->n_unk;
   std::vector<std::vector<int64_t>> wave_off(P);
   std::vector<std::vector<uint32_t>> place(P);   // k=1 placements, uploaded with the batch
@@ -1196,7 +1227,7 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   Carve cv;
   struct PieceOff {
     size_t order, sent_n, node_off, span_off, bp_off, cum_n, span_start, nodes, post, bp, edge_base, edge_val,
-        sched, wave_off, place;
+        sched, wave_off, place, xmask, xf4, xf5, xf6;
   };
   std::vector<PieceOff> po(P);
   for (size_t q = 0; q < P; ++q) {
@@ -1210,7 +1241,9 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
                      cv.dev(ed ? (size_t)pc.n_nodes * 8 : 0),
                      cv.dev(ed ? (size_t)d->n_edge * (size_t)pc.n_edges * 8 : 0),
                      cv.dev(b->has_sched ? (size_t)std::max<int64_t>(pc.sched_steps, 1) * 64 * 4 : 0),
-                     cv.dev(b->has_sched ? wave_off[q].size() * 8 : 0), cv.dev(place[q].size() * 4)};
+                     cv.dev(b->has_sched ? wave_off[q].size() * 8 : 0), cv.dev(place[q].size() * 4),
+                     cv.dev((size_t)d->n_xtri * (size_t)pc.n_nodes * 4), cv.dev((size_t)d->n_xtri * (size_t)pc.n_nodes * 8),
+                     cv.dev((size_t)d->n_xtri * (size_t)pc.n_nodes * 8), cv.dev((size_t)d->n_xtri * (size_t)pc.n_nodes * 8)};
   }
   const size_t o_sent_n = cv.dev((size_t)S * 4), o_cum_n = cv.dev(((size_t)S + 1) * 8);
   const size_t o_unk = cv.dev((size_t)d->n_unk * sizeof(NodeRec)),
@@ -1262,6 +1295,10 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
     pc.d_sched = at<uint32_t>(D, po[q].sched);
     pc.d_wave_off = at<int64_t>(D, po[q].wave_off);
     pc.d_place = at<uint32_t>(D, po[q].place);
+    pc.d_xmask = at<uint32_t>(D, po[q].xmask);
+    pc.d_xf4 = at<double>(D, po[q].xf4);
+    pc.d_xf5 = at<double>(D, po[q].xf5);
+    pc.d_xf6 = at<double>(D, po[q].xf6);
   }
   b->d_sent_n = at<int32_t>(D, o_sent_n);
   b->d_cum_n = at<int64_t>(D, o_cum_n);
@@ -1361,6 +1398,12 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
   if (has_esc) up(at<F46>(D, o_esc), esc_h.get(), (size_t)d->n_nodes);
   if (d->n_post > 0) up(b->d_unk_post, d->unk_post, (size_t)d->n_post * (size_t)d->n_unk);
   std::vector<std::vector<int64_t>> edge_base_tmp(P);
+  // the further trigram scorers' node masks in the device layout (as the
+  // records' masks: lt_common.h device_mask)
+  std::vector<uint32_t> xdm((size_t)d->n_xtri * (size_t)d->n_nodes);
+  parallel_ranges((int64_t)xdm.size(), [&](int, int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) xdm[(size_t)i] = device_mask(d->xtri_mask[i]);
+  });
   for (size_t q = 0; q < P; ++q) {
     const lt_piece& pc = b->pieces[q];
     const size_t n = (size_t)pc.n_sent;
@@ -1382,6 +1425,13 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
       up(pc.d_edge_base, edge_base_tmp[q].data(), (size_t)pc.n_nodes);
       for (int32_t t = 0; t < d->n_edge; ++t)
         up(pc.d_edge_val + (size_t)t * pc.n_edges, d->edge_val + (size_t)t * d->n_edges + pc.edge0, (size_t)pc.n_edges);
+    }
+    for (int32_t t = 0; t < d->n_xtri; ++t) {       // scorer t+1's rows, rebased to the piece
+      const size_t src = (size_t)t * (size_t)d->n_nodes + (size_t)pc.node0, dst = (size_t)t * (size_t)pc.n_nodes;
+      up(pc.d_xmask + dst, xdm.data() + src, (size_t)pc.n_nodes);
+      up(pc.d_xf4 + dst, d->xtri_f4 + src, (size_t)pc.n_nodes);
+      up(pc.d_xf5 + dst, d->xtri_f5 + src, (size_t)pc.n_nodes);
+      up(pc.d_xf6 + dst, d->xtri_f6 + src, (size_t)pc.n_nodes);
     }
     if (b->has_sched) {
       up(pc.d_wave_off, wave_off[q].data(), wave_off[q].size());
@@ -1472,7 +1522,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   if (m->ctx != c || b->ctx != c) return fail(LT_EINVAL, "decode: handles from another context");
   if (k < 1 || k > b->max_k)
     return fail(LT_EUNSUPPORTED, "decode: beam %d not in 1..%d (batch max_k)", k, b->max_k);
-  if (!decode_is_wide(b->max_len, k) && beam_template_for(k) < 0)
+  if (!batch_wide(b, k) && beam_template_for(k) < 0)
     return fail(LT_EUNSUPPORTED, "decode: beam %d not compiled", k);
   if ((m->inf_signs | b->inf_signs) == 3)
     return fail(LT_EUNSUPPORTED, "decode: both +inf and -inf among the model's and the batch's score terms "
@@ -1480,7 +1530,10 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p = DecodeParams{};
   // beam 1 and the general kernel probe primary first (flags); the tuned beam
   // kernels load both slots of the flag-free copy
-  p.table = (k == 1 || decode_is_wide(b->max_len, k)) ? m->d_table : m->d_plain;
+  p.table = (k == 1 || batch_wide(b, k)) ? m->d_table : m->d_plain;
+  if (b->n_xtri > 0 && m->narrow)
+    return fail(LT_EINVAL, "decode: a batch with several trigram terms needs a model with their keys "
+                           "(classes + %d per further scorer)", LT_XTRI_CLASS_STRIDE);
   p.slots = (uint32_t)m->slots;
   p.seed = m->seed;
   p.hk = narrow_hash(m->seed);
@@ -1491,6 +1544,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.max_len = b->max_len;
   p.n_post = b->n_post;
   p.n_edge = b->n_edge;
+  p.n_xtri = b->n_xtri;
   p.n_terms = b->n_terms;
   p.term_kinds = b->term_kinds;
   p.k = k;
@@ -1525,6 +1579,10 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
   p.n_edges = pc.n_edges;
   p.edge_base = pc.d_edge_base;
   p.edge_val = pc.d_edge_val;
+  p.xmask = pc.d_xmask;
+  p.xf4 = pc.d_xf4;
+  p.xf5 = pc.d_xf5;
+  p.xf6 = pc.d_xf6;
   p.bp = pc.d_bp;
   p.bp_bytes = pc.bp_entries * 4;
   p.bp_off = pc.d_bp_off;
@@ -1588,7 +1646,7 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
   HIP_TRY(hipSetDevice(c->device));
-  const bool wide = decode_is_wide(b->max_len, k);
+  const bool wide = batch_wide(b, k);
   if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
   // the k=1 lane schedule, if the batch has not got it yet: queued in front
   // of the decode on its stream (lt_batch_create builds it for max_k = 1; a
@@ -1630,6 +1688,10 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
     return fail(LT_EUNSUPPORTED, "lt_evaluate: %lld words exceed one launch", (long long)d->n_words);
   if (d->trigram_pos < -1 || d->trigram_pos > d->n_terms)
     return fail(LT_EINVAL, "lt_evaluate: trigram_pos %d out of range", d->trigram_pos);
+  if (d->trigram_scorer < 0 || d->trigram_scorer >= LT_MAX_TRI)
+    return fail(LT_EINVAL, "lt_evaluate: trigram_scorer %d not in 0..%d", d->trigram_scorer, LT_MAX_TRI - 1);
+  if (d->trigram_scorer > 0 && m->narrow)
+    return fail(LT_EINVAL, "lt_evaluate: the model holds no keys of trigram scorer %d", d->trigram_scorer);
   if (!d->path_off || (d->n_words > 0 && (!d->word || !d->morph0 || !d->tag || !d->mask || !d->f4 ||
                                           !d->f5 || !d->f6 || !d->prev1 || !d->prev2)) ||
       (d->n_terms > 0 && d->n_words > 0 && !d->terms))
@@ -1699,6 +1761,7 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
     p.n_terms = d->n_terms;
     p.terms = d_terms;
     p.trigram_pos = d->trigram_pos;
+    p.coff = (uint32_t)(LT_XTRI_CLASS_STRIDE * d->trigram_scorer);
     p.inc = d_inc;
     p.out = d_out;
     e = launch_evaluate(p, st);
@@ -1877,7 +1940,7 @@ lt_status lt_decode_trace(lt_ctx* c, const lt_model* m, lt_batch* b, int k, lt_t
       (t->n_exp > 0 && (!t->exp_score || !t->exp_node || !t->exp_skip)) || t->n_exp < 0)
     return fail(LT_EINVAL, "lt_decode_trace: bad trace arrays");
   if (b->pieces.size() != 1) return fail(LT_EUNSUPPORTED, "lt_decode_trace: batch of several launch pieces");
-  if (decode_is_wide(b->max_len, k) && t->n_exp > 0 && !t->exp_link)
+  if (batch_wide(b, k) && t->n_exp > 0 && !t->exp_link)
     return fail(LT_EINVAL, "lt_decode_trace: exp_link is required past max_len %d / beam %d", MAX_SPAN,
                 LT_MAX_BEAM_COMPILED);
   const int64_t S = b->n_sent;
@@ -1944,7 +2007,7 @@ lt_status lt_count_ops(lt_ctx* c, const lt_model* m, lt_batch* b, int k, int64_t
   DecodeParams p;
   lt_status st = fill_params(c, m, b, k, p);
   if (st != LT_OK) return st;
-  const bool wide = decode_is_wide(b->max_len, k);
+  const bool wide = batch_wide(b, k);
   HIP_TRY(hipSetDevice(c->device));
   if (wide && (st = wide_scratch(c, b, k, p)) != LT_OK) return st;
   if (!wide && beam_template_for(k) == 1) {

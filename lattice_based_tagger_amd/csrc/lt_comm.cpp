@@ -354,9 +354,8 @@ lt_status lt_gather_fetch(lt_comm* c) {
   HIP_TRY(hipSetDevice(x->device));
   // on the ctx's copy stream once the gather is done: each rank's used bytes
   HIP_TRY(hipStreamWaitEvent(x->cstream, c->done[c->last], 0));
-  for (int q = 0; q < c->nranks; ++q)
-    HIP_TRY(lt::launch_slab_to_host(c->recv[c->last] + (size_t)q * c->cap, c->h_slabs + (size_t)q * c->cap, c->cap,
-                                    x->cstream));
+  // (the receive slot holds the ranks' slabs back to back: one DMA)
+  HIP_TRY(lt::launch_slab_to_host(c->recv[c->last], c->h_slabs, (size_t)c->nranks * c->cap, x->cstream));
   HIP_TRY(hipEventRecord(c->fetched[c->last], x->cstream));
   c->fetch_pending[c->last] = true;
   return LT_OK;

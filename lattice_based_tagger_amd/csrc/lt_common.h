@@ -71,6 +71,11 @@ LT_HD uint32_t hyp_probe_bits(uint32_t wj, uint32_t wi, bool has_i) {
          ((((wj >> 11) & 1u) | (((wj >> 12) & 1u) & i8)) << 5);
 }
 
+// several trigram scorers (lattice_decode.h LT_XTRI_CLASS_STRIDE / LT_MAX_TRI):
+// scorer t's key classes + XTRI_CLASS_STRIDE * t
+constexpr int XTRI_CLASS_STRIDE = 16;
+constexpr int MAX_TRI = 8;
+
 constexpr int MAX_SPAN = 8;
 constexpr int RING = MAX_SPAN + 1;     // frontier positions e-8 .. e
 // span slots per end position of a batch with this max_len: 8 (the tuned

@@ -173,6 +173,7 @@ struct Hyp {
   double score, f6;
   uint32_t jword, jmorph, jtag, jmask, iword, imorph, imask, depth;
   uint32_t jnode;                 // local index of wj (edge terms)
+  uint32_t inode;                 // local index of wi (further trigram terms; general kernels)
 };
 
 template <int G>
@@ -385,15 +386,18 @@ __device__ __forceinline__ Aux stage_aux(const DecodeParams& p, double* d3l) {
   return a;
 }
 
+// coff: the class offset of a further trigram scorer (LT_XTRI_CLASS_STRIDE *
+// t, wide tables; 0 otherwise)
 template <bool NARROW, bool BOTH>
 __device__ __forceinline__ void probe_issue(Probe<NARROW, BOTH>& P, const Bufs& B, uint32_t slots,
                                             uint32_t seed, const Hyp& h, const Cand& c,
-                                            uint32_t need, const Aux& aux) {
+                                            uint32_t need, const Aux& aux, uint32_t coff = 0) {
   using T = Tab<NARROW>;
   P.need = need;
   const Keys K = make_keys(h, c, use_j8_of(h, c));
   uint32_t gneed = need, lpres = 0;
-  if (aux.d3 && ((need >> 3) & 1u)) {        // class 3 from the dense LDS table
+  // class 3 from the dense LDS table (the first scorer's class-3 keys only)
+  if (aux.d3 && coff == 0 && ((need >> 3) & 1u)) {
     const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3mul)];
     P.s1[3].coef = v;
     gneed &= ~8u;
@@ -408,9 +412,9 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW, BOTH>& P, const Bufs& 
     // (slots stay undefined when not needed; probe_finish reads them only
     // under the same predicate)
     if ((gneed >> q) & 1u) {
-      P.s1[q] = T::load(B.tab, T::slot1(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+      P.s1[q] = T::load(B.tab, T::slot1(aux, K.a[q], K.b[q], K.c[q], PCLS[q] + coff, seed, slots) * T::SZ);
       if constexpr (BOTH)
-        P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+        P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q] + coff, seed, slots) * T::SZ);
     }
   }
 }
@@ -418,7 +422,7 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW, BOTH>& P, const Bufs& 
 template <bool NARROW, bool BOTH>
 __device__ __forceinline__ void probe_second(Probe<NARROW, BOTH>& P, const Bufs& B, uint32_t slots,
                                              uint32_t seed, const Aux& aux, const Hyp& h,
-                                             const Cand& c) {
+                                             const Cand& c, uint32_t coff = 0) {
   using T = Tab<NARROW>;
   // keys recomputed from (h, c), which stay live anyway
   const Keys K = make_keys(h, c, use_j8_of(h, c));
@@ -427,12 +431,12 @@ __device__ __forceinline__ void probe_second(Probe<NARROW, BOTH>& P, const Bufs&
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       if ((P.gneed >> q) & 1u) {
-        const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
+        const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q] + coff);
         if (T::hit(P.s1[q], key)) {
           hit1 |= 1u << q;
         } else if (T::flagged(P.s1[q])) {         // all second loads before any wait
           need2 |= 1u << q;
-          P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q], seed, slots) * T::SZ);
+          P.s2[q] = T::load(B.tab, T::slot2(aux, K.a[q], K.b[q], K.c[q], PCLS[q] + coff, seed, slots) * T::SZ);
         }
       }
     }
@@ -443,7 +447,7 @@ __device__ __forceinline__ void probe_second(Probe<NARROW, BOTH>& P, const Bufs&
 
 template <bool NARROW, bool COUNT, bool BOTH>
 __device__ __forceinline__ double probe_finish(const Probe<NARROW, BOTH>& P, const Hyp& h,
-                                               const Cand& c, Counts& cnt) {
+                                               const Cand& c, Counts& cnt, uint32_t coff = 0) {
   using T = Tab<NARROW>;
   const uint32_t jm = h.jmask, km = c.mask, im = h.imask;
   const uint32_t hit1 = P.hit1, need2 = P.need2;
@@ -456,7 +460,7 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW, BOTH>& P, con
     cf[q] = 0.0;
     if constexpr (BOTH) {                       // both slots loaded: branch-free selects
       if ((P.gneed >> q) & 1u) {
-        const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
+        const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q] + coff);
         // BOTH kernels probe the flag-free copy of the table (lt_model.d_plain)
         const bool m1 = T::hit_plain(P.s1[q], key);
         const bool m2 = T::hit_plain(P.s2[q], key);
@@ -470,7 +474,7 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW, BOTH>& P, con
       pr6[q] = true;
       cf[q] = P.s1[q].coef;
     } else if ((need2 >> q) & 1u) {
-      const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q]);
+      const typename T::Key key = T::key(K.a[q], K.b[q], K.c[q], PCLS[q] + coff);
       pr6[q] = T::hit(P.s2[q], key);
       cf[q] = P.s2[q].coef;
     } else if ((P.lpres >> q) & 1u) {          // resolved from LDS
@@ -501,11 +505,36 @@ __device__ __forceinline__ double probe_finish(const Probe<NARROW, BOTH>& P, con
 template <bool NARROW, bool COUNT>
 __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_t seed,
                                           const Hyp& h, const Cand& c, Counts& cnt,
-                                          const Aux& aux) {
+                                          const Aux& aux, uint32_t coff = 0) {
   Probe<NARROW> P;
-  probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c), aux);
-  probe_second<NARROW>(P, B, slots, seed, aux, h, c);
-  return probe_finish<NARROW, COUNT, false>(P, h, c, cnt);
+  probe_issue<NARROW>(P, B, slots, seed, h, c, probe_need(h, c), aux, coff);
+  probe_second<NARROW>(P, B, slots, seed, aux, h, c, coff);
+  return probe_finish<NARROW, COUNT, false>(P, h, c, cnt, coff);
+}
+
+// Every trigram term of an expansion (general kernels): tris[0] the first
+// scorer's (node records), tris[t] scorer t's (lattice_decode.h n_xtri: its
+// node masks and class 4/5/6 coefficients from the xtri arrays, its keys'
+// classes + LT_XTRI_CLASS_STRIDE * t).  Global node indices: gk of the
+// candidate, gj / gi of the hypothesis' last two words (has_i: wi exists).
+// Implicit Unknowns never occur with further scorers (lt_batch_create).
+template <bool NARROW, bool COUNT>
+__device__ __forceinline__ void trigram_terms(const DecodeParams& p, const Bufs& B, const Hyp& h, const Cand& c,
+                                              uint32_t gk, uint32_t gj, uint32_t gi, Counts& cnt, const Aux& aux,
+                                              double* tris) {
+  tris[0] = p.has_tri ? trigram<NARROW, COUNT>(B, p.slots, p.seed, h, c, cnt, aux) : 0.0;
+  for (int t = 1; t <= p.n_xtri; ++t) {
+    const int64_t o = (int64_t)(t - 1) * p.n_nodes;
+    Cand ct = c;
+    ct.mask = p.xmask[o + gk];
+    ct.f4 = p.xf4[o + gk];
+    ct.f5 = p.xf5[o + gk];
+    Hyp ht = h;
+    ht.jmask = p.xmask[o + gj];
+    ht.f6 = p.xf6[o + gj];
+    ht.imask = (h.imask & F_WI) ? (p.xmask[o + gi] | F_WI) : 0u;
+    tris[t] = trigram<NARROW, COUNT>(B, p.slots, p.seed, ht, ct, cnt, aux, (uint32_t)(XTRI_CLASS_STRIDE * t));
+  }
 }
 
 // inc = ((0 + pre...) + tri) + post...   (score_funcs.py:50-54).  With edge
@@ -514,6 +543,23 @@ __device__ __forceinline__ double trigram(const Bufs& B, uint32_t slots, uint32_
 // edge from wj (local node jl) to the candidate gn.  unk_d > 0: the candidate
 // is the implicit Unknown of that span length (its post terms from p.unk_post;
 // a batch with implicit Unknowns has no edge terms).
+// increment() of a composite with several trigram terms (general kernels):
+// term kind 0 takes the next of tris[] (constructor order)
+__device__ __forceinline__ double increment_x(const DecodeParams& p, const Cand& c, const double* tris,
+                                              uint32_t gn, uint32_t jl) {
+  double inc = c.pre;
+  int nd = 0, ne = 0, nt = 0;
+  for (int t = 0; t < p.n_terms; ++t) {
+    const uint32_t kind = (uint32_t)(p.term_kinds >> (2 * t)) & 3u;
+    double v;
+    if (kind == 0) v = tris[nt++];
+    else if (kind == 1) v = p.npost[(int64_t)(nd++) * p.n_nodes + gn];
+    else v = p.edge_val[(int64_t)(ne++) * p.n_edges + p.edge_base[gn] + jl];
+    inc += v;
+  }
+  return inc;
+}
+
 // GEN = false: the composite has no term after the trigram (p.n_post == 0,
 // p.n_edge == 0; launch_k picks it), so inc = pre + tri and the kernel keeps
 // none of the post / edge arrays or their loops live (round 6: the k=1
@@ -1458,6 +1504,7 @@ __device__ __forceinline__ Hyp read_entry(const Entry& e) {
   h.jword = e.jword; h.jmorph = e.jmorph; h.jtag = e.jtag; h.jmask = e.jmask;
   h.iword = e.iword; h.imorph = e.imorph; h.imask = e.imask; h.depth = e.depth;
   h.jnode = e.jnode;
+  h.inode = e.pad0;
   return h;
 }
 
@@ -2580,8 +2627,9 @@ __global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
   h.iword = ci.word; h.imorph = ci.morph; h.imask = i >= 0 ? (ci.mask | F_WI) : 0u;
   h.depth = 0;
   h.jnode = 0;
+  h.inode = 0;
   Counts cnt;
-  p.inc[w] = trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux);
+  p.inc[w] = trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux, p.coff);
 }
 
 // One lane per path: the exact-order sums.
@@ -2761,7 +2809,7 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
   const Bufs B = make_bufs(p);
   const Aux aux{nullptr, 0u, p.hk};             // class 3 from the table itself
   const int k = p.k, S = p.span_slots;
-  const bool wide = decode_is_wide(p.max_len, k);
+  const bool wide = decode_is_wide(p.max_len, k) || p.n_xtri > 0;
   const int n = p.sent_n[s];
   const uint32_t nbase = (uint32_t)p.node_off[s];
   const int32_t* ssp = p.span_start + p.span_off[s];
@@ -2802,7 +2850,12 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
           const Cand c = cand_at(B, p, nbase, nd, d);
           const bool skip = (h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax);   // beam.py:43-45
           double sc = 0.0;
-          if (!skip) {
+          if (!skip && p.n_xtri) {              // several trigram terms (score_funcs.py:50-54)
+            double tris[MAX_TRI];
+            trigram_terms<NARROW, false>(p, B, h, c, nbase + (uint32_t)node, nbase + h.jnode, nbase + h.inode, cnt,
+                                         aux, tris);
+            sc = h.score + increment_x(p, c, tris, nbase + (uint32_t)node, h.jnode);   // beam.py:115
+          } else if (!skip) {
             const double tri = p.has_tri ? trigram<NARROW, false>(B, p.slots, p.seed, h, c, cnt, aux) : 0.0;
             sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode, imp ? d : 0);   // beam.py:115
           }
@@ -2844,7 +2897,7 @@ __global__ void __launch_bounds__(64) lt_trace_k(DecodeParams p, TraceParams t) 
       ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
       ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
       ne.depth = h.depth + 1;
-      ne.jnode = (uint32_t)node; ne.pad0 = ne.pad1 = ne.pad2 = 0;
+      ne.jnode = (uint32_t)node; ne.pad0 = h.jnode; ne.pad1 = ne.pad2 = 0;   // pad0: wi's local node
       ent[(int64_t)e * k + kept] = ne;
       t.beam_gen[(po + e) * k + kept] = bg;
     }
@@ -2958,8 +3011,16 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
             const Cand c = cand_at(B, p, nbase, nd, d);
             if ((h.jmask & F_UNK) && (c.mask & F_UNK) && (d < dmax)) continue;    // beam.py:43-45
             if (COUNT) ++cn.exp;
-            const double tri = p.has_tri ? trigram<NARROW, COUNT>(B, p.slots, p.seed, h, c, cn, aux) : 0.0;
-            const double sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode, imp ? d : 0);   // beam.py:115
+            double sc;
+            if (p.n_xtri) {                     // several trigram terms (score_funcs.py:50-54)
+              double tris[MAX_TRI];
+              trigram_terms<NARROW, COUNT>(p, B, h, c, nbase + (uint32_t)node, nbase + h.jnode, nbase + h.inode, cn,
+                                           aux, tris);
+              sc = h.score + increment_x(p, c, tris, nbase + (uint32_t)node, h.jnode);   // beam.py:115
+            } else {
+              const double tri = p.has_tri ? trigram<NARROW, COUNT>(B, p.slots, p.seed, h, c, cn, aux) : 0.0;
+              sc = h.score + increment(p, c, tri, nbase + (uint32_t)node, h.jnode, imp ? d : 0);   // beam.py:115
+            }
             const WItem it{ord_key(sc), g, nd, (uint32_t)d, (uint32_t)r};
             if (hn < k) {
               H[hn] = it;
@@ -2988,7 +3049,7 @@ __global__ void __launch_bounds__(64) lt_beam_wide(DecodeParams p) {
         ne.jword = c.word; ne.jmorph = c.morph; ne.jtag = c.tag; ne.jmask = c.mask;
         ne.iword = h.jword; ne.imorph = h.jmorph; ne.imask = h.jmask | F_WI;
         ne.depth = h.depth + 1;
-        ne.jnode = it.node; ne.pad0 = ne.pad1 = ne.pad2 = 0;
+        ne.jnode = it.node; ne.pad0 = h.jnode; ne.pad1 = ne.pad2 = 0;     // pad0: wi's local node
         R[(int64_t)es * k + t] = ne;
         bp[(int64_t)e * bstride + t] = bpw_pack(it.node, it.d, it.r);
       }

@@ -62,12 +62,16 @@ struct lt_piece {
   int64_t* d_edge_base = nullptr;                // [n_nodes], rebased to the piece
   double* d_edge_val = nullptr;                  // [n_edge][n_edges]
   lt::F46* d_esc = nullptr;                      // [n_nodes] class-4/6 pairs of PX_ESC nodes (or none)
+  // further trigram scorers (lt_batch_desc.n_xtri): [n_xtri][n_nodes], rebased to the piece
+  uint32_t* d_xmask = nullptr;
+  double *d_xf4 = nullptr, *d_xf5 = nullptr, *d_xf6 = nullptr;
 };
 
 struct lt_batch {
   lt_ctx* ctx = nullptr;
   int32_t n_sent = 0, max_len = 8, n_post = 0, has_tri = 0, max_k = 1;
   int32_t n_edge = 0, n_terms = 0;    // edge terms (lt_batch_desc.n_edge)
+  int32_t n_xtri = 0;                  // further trigram terms (lt_batch_desc.n_xtri): general kernel
   uint64_t term_kinds = 0;
   int64_t n_nodes = 0, n_span = 0, total_chars = 0, bp_entries = 0;
   int inf_signs = 0;                  // +inf (1) / -inf (2) among the node score terms

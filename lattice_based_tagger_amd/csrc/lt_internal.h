@@ -47,6 +47,14 @@ struct DecodeParams {
   int64_t n_edges;
   const int64_t* edge_base;     // [n_nodes]: value of predecessor local node j at edge_base[gn] + j
   const double* edge_val;       // [n_edge][n_edges]
+  // further trigram terms (lt_batch_desc.n_xtri; general kernel only): scorer
+  // t = 1..n_xtri's node mask + flags and class 4/5/6 coefficients at
+  // [(t-1) * n_nodes + node], its keys' classes + LT_XTRI_CLASS_STRIDE * t
+  int32_t n_xtri;
+  const uint32_t* xmask;
+  const double* xf4;
+  const double* xf5;
+  const double* xf6;
   // k=1 lane schedule of the piece (launch_k1_sched): wave w's macro-steps are
   // sched[wave_off[w] * 64 ..] (64 entries each)
   const uint32_t* sched;
@@ -91,6 +99,7 @@ struct EvalParams {
   int32_t n_terms;
   const double* terms;
   int32_t trigram_pos;
+  uint32_t coff;                // key class offset of the trigram scorer (LT_XTRI_CLASS_STRIDE * scorer)
   double* inc;                  // [n_words] scratch
   double* out;                  // [n_paths]
 };

@@ -13,10 +13,14 @@
 //
 // Three small kernels on the decode stream build the slab on the device
 // (per-block length sums, one-block scan of the sums, then a pass that
-// copies the entries and gathers the codes with coalesced writes), and
-// lt_slab_to_host_k copies its used bytes -- read from the header on the
-// device, so the host never waits for the size -- into pinned host memory
-// with plain vector stores over PCIe.
+// copies the entries and gathers the codes with coalesced writes), and a DMA
+// (SDMA engine, hipMemcpyAsync) copies the slab's capacity into pinned host
+// memory.  Round 6: that copy was a kernel of 64 blocks storing the used
+// bytes over PCIe (lt_slab_to_host_k, the size read from the header on the
+// device); its blocks sat on CUs for the whole transfer and kept the
+// decode's LDS-filling blocks off them -- the k=1 decode of the next step ran
+// 0.56 -> 0.94 ms beside it.  The DMA moves the capacity (the worst case,
+// about the padded results' bytes), but takes no CU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -165,12 +169,15 @@ hipError_t launch_pack_results(const ResultsPackParams& p, hipStream_t st) {
 
 int64_t pack_blocks(int64_t n_entries) { return (n_entries + PB - 1) / PB; }
 
+#ifndef LT_SLAB_KERNEL_COPY
+#define LT_SLAB_KERNEL_COPY 0           // 1: the round-2..5 copy kernel (A/B builds)
+#endif
 hipError_t launch_slab_to_host(const void* slab, void* host, size_t capacity, hipStream_t st) {
+  if (!LT_SLAB_KERNEL_COPY) return capacity ? hipMemcpyAsync(host, slab, capacity, hipMemcpyDeviceToHost, st) : hipSuccess;
   const int64_t c16 = (int64_t)(capacity / 16);
   if (c16 == 0) return hipSuccess;
   const int64_t want = (c16 + 255) / 256;
-  // enough 16 B stores in flight for PCIe (~54 GB/s) from a few blocks, so
-  // that the copy finds CU slots while a decode occupies the GPU
+  // enough 16 B stores in flight for PCIe (~54 GB/s) from a few blocks
   const unsigned blocks = (unsigned)(want < 64 ? want : 64);
   hipLaunchKernelGGL(lt_slab_to_host_k, dim3(blocks), dim3(256), 0, st, static_cast<const int4*>(slab),
                      static_cast<int4*>(host), c16);

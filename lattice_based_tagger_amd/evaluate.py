@@ -38,7 +38,7 @@ class PathsDesc(C.Structure):
                 ('word', C.c_void_p), ('morph0', C.c_void_p), ('tag', C.c_void_p),
                 ('mask', C.c_void_p), ('f4', C.c_void_p), ('f5', C.c_void_p), ('f6', C.c_void_p),
                 ('prev1', C.c_void_p), ('prev2', C.c_void_p), ('n_terms', C.c_int32),
-                ('terms', C.c_void_p), ('trigram_pos', C.c_int32)]
+                ('terms', C.c_void_p), ('trigram_pos', C.c_int32), ('trigram_scorer', C.c_int32)]
 
 
 def _words_of(seq):
@@ -49,9 +49,37 @@ def evaluate_batch(sequences, score_functions, device=0):
     """``[score_functions.evaluate(seq) for seq in sequences]`` on the GPU.
 
     ``sequences``: ``Sequence`` objects (e.g. ``beam_search`` matures) or lists
-    of words ``[BOS, w1, ..., EOS]``.  Returns a list of Python floats."""
+    of words ``[BOS, w1, ..., EOS]``.  Returns a list of Python floats.
+
+    A composite with several trigram scorers is evaluated one scorer per
+    launch (each launch's total is that scorer's E_t exactly: 0 + E_t), and
+    the totals are summed here in constructor order, as
+    ``BeamScoreFunctions.evaluate`` does (`score_funcs.py:44-48`)."""
     funcs = list(score_functions.funcs)
     model = lowered_model(score_functions)
+    sequences = list(sequences)
+    if len(model.trigrams) > 1:
+        per = []
+        t = 0
+        for f in funcs:
+            if type(f).__name__ in (TRIGRAM_SCORER, PACKED_TRIGRAM_SCORER):
+                per.append(_evaluate_launch(sequences, model, [f], device, scorer=t))
+                t += 1
+            else:
+                per.append(_evaluate_launch(sequences, model, [f], device))
+        out = []
+        for p in range(len(sequences)):
+            total = 0
+            for v in per:
+                total += v[p]
+            out.append(float(total))
+        return out
+    return _evaluate_launch(sequences, model, funcs, device)
+
+
+def _evaluate_launch(sequences, model, funcs, device, scorer=0):
+    """One lt_evaluate launch: the scorers ``funcs`` (at most one trigram
+    scorer, the composite's ``scorer``-th) over ``sequences``."""
     trigram_pos = -1
     local = []
     for pos, f in enumerate(funcs):
@@ -69,7 +97,7 @@ def evaluate_batch(sequences, score_functions, device=0):
         base = len(cols['word'])
         replay = [base]                                       # Sequence([seq.sequences[0]])
         for idx, w in enumerate(words):
-            wid, mid, tid, m, c4, c5, c6 = node_record(model, w)
+            wid, mid, tid, m, c4, c5, c6 = node_record(model, w, scorer)
             cols['word'].append(wid)
             cols['morph'].append(mid)
             cols['tag'].append(tid)
@@ -112,7 +140,7 @@ def evaluate_batch(sequences, score_functions, device=0):
     desc = PathsDesc(n_paths, len(cols['word']), ptr(arrs['path_off']), ptr(arrs['word']),
                      ptr(arrs['morph0']), ptr(arrs['tag']), ptr(arrs['mask']), ptr(arrs['f4']),
                      ptr(arrs['f5']), ptr(arrs['f6']), ptr(arrs['prev1']), ptr(arrs['prev2']),
-                     len(local), ptr(arrs['terms']), trigram_pos)
+                     len(local), ptr(arrs['terms']), trigram_pos, scorer)
     out = np.zeros(n_paths, dtype=np.float64)
     dec = Decoder.get(device)
     dm = dec.device_model(model)

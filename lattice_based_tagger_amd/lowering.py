@@ -28,9 +28,17 @@ is then evaluated once per lattice node (like the three built-in node-local
 scorers) and summed in constructor order.  A plugin that declares it but reads
 ``seq`` gets ``None`` and fails loudly.
 
-Unsupported composites (a plugin of any other class, two trigram scorers,
-non-float64 or NaN coefficients, +inf and -inf terms together) raise: there
-is no CPU fallback decoder.
+Several trigram scorers (round 6): each ``SimpleTrigramFeatureScore`` of the
+composite is its own term, summed in its own numpy order and added in
+constructor order (`score_funcs.py:50-54`).  Their keys share one interned id
+space and one device table, the key class of scorer t carrying ``16 * t``
+(``XTRI_CLASS_STRIDE``); scorer t >= 1 gets its own node masks and class
+4-6 coefficients (``xtri_*`` batch arrays, lattice_decode.h ABI 6), and the
+batch decodes on the general kernel.
+
+Unsupported composites (a plugin of any other class, non-float64 or NaN
+coefficients, +inf and -inf terms together) raise: there is no CPU fallback
+decoder.
 """
 
 import numpy as np
@@ -83,6 +91,10 @@ def node_mask_from_vocab(vm_word, vm_morph, vm_tag):
 # kinds of the scorers after the leading node-local ones (lt_batch_desc.term_kinds)
 KIND_TRI, KIND_NODE, KIND_EDGE = 0, 1, 2
 MAX_TERMS = 32
+# several trigram scorers: scorer t's keys carry class + 16 * t (lattice_decode.h
+# LT_XTRI_CLASS_STRIDE); at most LT_MAX_TRI of them
+XTRI_CLASS_STRIDE = 16
+MAX_TRI = 8
 
 
 class EdgeSequence:
@@ -117,7 +129,11 @@ class LoweredModel:
            node_post row) or KIND_EDGE (an ``edge_local`` plugin: an edge_val
            row, one value per lattice edge)
     post_funcs, edge_funcs : the KIND_NODE / KIND_EDGE plugins of ``plan``
-    trigram : the SimpleTrigramFeatureScore or None
+    trigram : the first SimpleTrigramFeatureScore or None
+    trigrams : every trigram scorer, in constructor order (trigrams[0] is
+               ``trigram``); keys / coefs hold all of them, scorer t's classes
+               offset by 16 * t, vmasks[t] / locals[t] its pre-filter masks and
+               node-local classes
     vocab : dict value -> id (1-based) over every key component
     vmask : uint32[len(vocab)+1] key-slot bits per id
     keys : uint32[F, 4] (a, b, c, class) of the probed classes
@@ -133,12 +149,18 @@ class LoweredModel:
         self.pre_funcs, self.post_funcs, self.edge_funcs = [], [], []
         self.plan = []
         self.trigram = None
+        self.trigrams = []
         for f in funcs:
             name = type(f).__name__
             if name in (TRIGRAM_SCORER, PACKED_TRIGRAM_SCORER):
-                if self.trigram is not None:
-                    raise NotImplementedError('at most one SimpleTrigramFeatureScore is supported')
-                self.trigram = f
+                if self.trigrams and (name == PACKED_TRIGRAM_SCORER or
+                                      type(self.trigrams[0]).__name__ == PACKED_TRIGRAM_SCORER):
+                    raise NotImplementedError('a model pack scorer cannot be combined with another trigram scorer')
+                if len(self.trigrams) >= MAX_TRI:
+                    raise NotImplementedError('more than %d trigram scorers' % MAX_TRI)
+                if self.trigram is None:
+                    self.trigram = f
+                self.trigrams.append(f)
                 self.plan.append((KIND_TRI, f))
             elif name in NODE_LOCAL_SCORERS or getattr(f, 'node_local', False) is True:
                 if self.plan:
@@ -167,11 +189,12 @@ class LoweredModel:
         self.coefficients = None
         self.local = None           # packed models: {(cls, *comps): coef} of classes 4-6
         self.image = None           # packed models: prebuilt device image
+        self.vmasks, self.feature_dics, self.coefficient_arrays = [], [], []
         if self.trigram is not None:
             if type(self.trigram).__name__ == PACKED_TRIGRAM_SCORER:
                 self._lower_pack(self.trigram.pack)
             else:
-                self._lower_trigram(self.trigram)
+                self._lower_trigrams()
         self._device_models = {}
 
     @property
@@ -191,7 +214,35 @@ class LoweredModel:
     def has_trigram(self):
         return self.trigram is not None
 
-    def _lower_trigram(self, tri):
+    @property
+    def n_xtri(self):
+        """Trigram scorers past the first (lattice_decode.h n_xtri)."""
+        return max(len(self.trigrams) - 1, 0)
+
+    def _lower_trigrams(self):
+        vocab = self.vocab
+        # the tag set first: ids 1..13, distinct in their low four bits -- the
+        # slot inside a key's line group (lt_common.h, HASH_VERSION 5)
+        for t in TAG_IDS_FIRST:
+            vocab[t] = len(vocab) + 1
+        parts = [self._lower_trigram(tri, t) for t, tri in enumerate(self.trigrams)]
+        # one id space for every scorer: the masks sized to the final vocabulary
+        self.vmasks = []
+        for slot_pairs in (p[2] for p in parts):
+            vmask = np.zeros(len(vocab) + 1, dtype=np.uint32)
+            if slot_pairs:
+                sp = np.asarray(slot_pairs, dtype=np.int64)
+                np.bitwise_or.at(vmask, sp[:, 0], (np.uint32(1) << sp[:, 1].astype(np.uint32)))
+            self.vmasks.append(vmask)
+        self.vmask = self.vmasks[0]
+        self.keys = np.concatenate([p[0] for p in parts]).reshape(-1, 4)
+        self.coefs = np.concatenate([p[1] for p in parts])
+        self.feature_dic = self.feature_dics[0]
+        self.coefficients = self.coefficient_arrays[0]
+
+    def _lower_trigram(self, tri, t=0):
+        """Keys (class + 16 t), coefficients and the (id, slot bit) pairs of
+        the pre-filter masks of trigram scorer t."""
         enc = tri.encoder
         if enc is None:
             raise AttributeError("'NoneType' object has no attribute 'encode_word'")
@@ -207,13 +258,9 @@ class LoweredModel:
             raise NotImplementedError('+inf and -inf coefficients together: their sum is a NaN, whose '
                                       'order in Python\'s sort is not reproduced')
         dic = enc.feature_dic
-        self.feature_dic = dic
-        self.coefficients = coef
+        self.feature_dics.append(dic)
+        self.coefficient_arrays.append(coef)
         vocab = self.vocab
-        # the tag set first: ids 1..13, distinct in their low four bits -- the
-        # slot inside a key's line group (lt_common.h, HASH_VERSION 5)
-        for t in TAG_IDS_FIRST:
-            vocab[t] = len(vocab) + 1
         keys, coefs, slot_pairs = [], [], []
         cls_of = _ClassIndex.table
         n_coef = coef.shape[0]
@@ -240,19 +287,15 @@ class LoweredModel:
             i = int(idx)
             if not -n_coef <= i < n_coef:
                 raise IndexError('feature index %d out of range for %d coefficients' % (i, n_coef))
-            keys.append((ids[0], ids[1], ids[2], cls))
+            keys.append((ids[0], ids[1], ids[2], cls + XTRI_CLASS_STRIDE * t))
             coefs.append(coef[i])
-        vmask = np.zeros(len(vocab) + 1, dtype=np.uint32)
-        if slot_pairs:
-            sp = np.asarray(slot_pairs, dtype=np.int64)
-            np.bitwise_or.at(vmask, sp[:, 0], (np.uint32(1) << sp[:, 1].astype(np.uint32)))
-        self.vmask = vmask
-        self.keys = np.asarray(keys, dtype=np.uint32).reshape(-1, 4)
-        self.coefs = np.asarray(coefs, dtype=np.float64)
+        return (np.asarray(keys, dtype=np.uint32).reshape(-1, 4), np.asarray(coefs, dtype=np.float64),
+                slot_pairs)
 
     def _lower_pack(self, pack):
         """A model pack already holds the lowered tables and the device image."""
         self.vocab, self.vmask, self.keys, self.coefs, self.local = pack.lowered_parts()
+        self.vmasks = [self.vmask]
         self.image = pack.image
         self.coefficients = pack.array('coefficients')
 
@@ -272,16 +315,17 @@ class LoweredModel:
         seq = EdgeSequence(wj)
         return [f.score(seq, wk) for f in self.edge_funcs]
 
-    def node_local_features(self, w, is_unk):
-        """Coefficients (or None) of feature classes 4, 5 and 6 for node w."""
+    def node_local_features(self, w, is_unk, t=0):
+        """Coefficients (or None) of feature classes 4, 5 and 6 for node w
+        under trigram scorer t."""
         if self.local is not None:
             loc = self.local
             return (loc.get((4, w.len)), loc.get((5, w.word, w.tag0, w.is_l)),
                     loc.get((6, min(8, w.len))) if is_unk else None)
-        dic = self.feature_dic
+        dic = self.feature_dics[t] if t < len(self.feature_dics) else None
         if dic is None:
             return None, None, None
-        coef = self.coefficients
+        coef = self.coefficient_arrays[t]
         i4 = dic.get((4, w.len))
         i5 = dic.get((5, w.word, w.tag0, w.is_l))
         i6 = dic.get((6, min(8, w.len))) if is_unk else None

@@ -196,6 +196,8 @@ class NativePacker:
         c5c = np.asarray(list(c5.values()), dtype=np.float64)
         if getattr(model, 'edge_funcs', None):      # edge_local plugins: Python, per lattice edge
             raise Unsupported('edge_local scorers are evaluated per edge in Python')
+        if getattr(model, 'n_xtri', 0):             # several trigram scorers: per-scorer node arrays
+            raise Unsupported('several trigram scorers are packed by the Python packer')
         # node-local scorers in constructor order
         funcs = list(model.pre_funcs) + list(model.post_funcs)
         kinds, reg, ptag, pkey, pscorer, pval = [], [], [], [], [], []

@@ -27,6 +27,11 @@ layout described in DESIGN.md §Data layout:
   predecessor local node j, ``node_edge_base = base`` (``sent_edge_off``
   delimits each sentence's block).
 
+* several trigram scorers (``LoweredModel.trigrams``): scorer t >= 1's
+  pre-filter mask + flags and class 4-6 coefficients of every node in the
+  ``xtri_*`` arrays ([n_xtri][n_nodes], lattice_decode.h ABI 6); no implicit
+  Unknowns then.
+
 * implicit Unknowns (``implicit_unk``, lattice_decode.h ``n_unk``): the
   synthesised Unknown of a span is not stored as a node when its record
   equals the *canonical* record of its length d -- the record of an Unknown
@@ -92,9 +97,22 @@ class PackedBatch:
     UNK_FIELDS = ('unk_word', 'unk_morph0', 'unk_tag', 'unk_mask', 'unk_pre', 'unk_f4', 'unk_f5',
                   'unk_f6', 'unk_post')
 
+    XTRI_FIELDS = ('xtri_mask', 'xtri_f4', 'xtri_f5', 'xtri_f6')
+
     @property
     def n_unk(self):
         return int(getattr(self, 'unk_n', 0))
+
+    @property
+    def n_xtri(self):
+        return int(getattr(self, 'xtri_n', 0))
+
+    def _xtri_of(self, out, node_sel):
+        """The further trigram scorers' node arrays of a sub-batch."""
+        out['xtri_n'] = self.n_xtri
+        if self.n_xtri:
+            for f in self.XTRI_FIELDS:
+                out[f] = getattr(self, f)[:, node_sel]
 
     def _unk_of(self, out):
         """The implicit-Unknown records (batch-wide) into a sub-batch's fields."""
@@ -153,6 +171,7 @@ class PackedBatch:
             out[f] = getattr(self, f)[n0:n1]
         self._edges_of(out, np.arange(n0, n1), np.arange(s0, s1))
         self._unk_of(out)
+        self._xtri_of(out, slice(n0, n1))
         return PackedBatch(**out)
 
     # backpointer bytes of one launch: lt_batch_create takes sum_s (n_s + 1) * k
@@ -203,6 +222,7 @@ class PackedBatch:
             out[f] = getattr(self, f)[ni]
         self._edges_of(out, ni, order)
         self._unk_of(out)
+        self._xtri_of(out, ni)
         return PackedBatch(**out)
 
 
@@ -214,11 +234,12 @@ def _span_candidates(bindex_b, b, n, max_len):
     return groups
 
 
-def node_record(model, w):
+def node_record(model, w, t=0):
     """Device fields of lattice node ``w``: interned word / morph0 / tag ids,
     pre-filter mask + flags, and the coefficients of the node-local feature
-    classes 4, 5, 6 (None when absent)."""
-    vocab, vmask = model.vocab, model.vmask
+    classes 4, 5, 6 (None when absent) -- under trigram scorer t."""
+    vocab = model.vocab
+    vmask = model.vmasks[t] if t < len(model.vmasks) else model.vmask
     is_unk = w.tag0 == Unk
     wid = vocab.get(w.word, 0)
     mid = vocab.get(w.morph0, 0)
@@ -228,7 +249,7 @@ def node_record(model, w):
         m |= L.F_UNK
     if w.tag0 in CONTEXTUAL_TAGS:
         m |= L.F_CTX
-    c4, c5, c6 = model.node_local_features(w, is_unk)
+    c4, c5, c6 = model.node_local_features(w, is_unk, t)
     if c4 is not None:
         m |= L.F_HAS4
     if c5 is not None:
@@ -259,17 +280,22 @@ def implicit_unk_ok(model):
     no edge terms, and node-local terms only from the three built-in scorers
     (whose value for an Unknown depends on its length and on table entries
     for its surface -- which ``_same_record`` then sees)."""
-    if getattr(model, 'n_edge', 0):
+    if getattr(model, 'n_edge', 0) or getattr(model, 'n_xtri', 0):
         return False
     return all(type(f).__name__ in KNOWN_NODE_SCORERS for f in list(model.pre_funcs) + list(model.post_funcs))
 
 
 def _record(model, w):
-    """(wid, mid, tid, mask, pre, f4, f5, f6, post) of node w, as pack stores it."""
+    """(wid, mid, tid, mask, pre, f4, f5, f6, post, xtri) of node w, as pack
+    stores it; xtri: (mask, f4, f5, f6) under each further trigram scorer."""
     wid, mid, tid, m, c4, c5, c6 = node_record(model, w)
     p, q = model.node_terms(w)
+    x = []
+    for t in range(1, getattr(model, 'n_xtri', 0) + 1):
+        m_t, x4, x5, x6 = node_record(model, w, t)[3:]
+        x.append((m_t, 0.0 if x4 is None else x4, 0.0 if x5 is None else x5, 0.0 if x6 is None else x6))
     return (wid, mid, tid, m, float(p), 0.0 if c4 is None else c4, 0.0 if c5 is None else c5,
-            0.0 if c6 is None else c6, [float(v) for v in q])
+            0.0 if c6 is None else c6, [float(v) for v in q], x)
 
 
 def _bits(rec):
@@ -336,10 +362,15 @@ def pack(sentences, model, max_len=8, implicit_unk=True):
     words, morphs, tags, masks = [], [], [], []
     pre, f4, f5, f6 = [], [], [], []
     post = [[] for _ in range(n_post)]
+    n_x = getattr(model, 'n_xtri', 0)
+    xcols = [([], [], [], []) for _ in range(n_x)]
     node_objects = []
 
     def add_record(rec):
-        wid, mid, tid, m, p, c4, c5, c6, q = rec
+        wid, mid, tid, m, p, c4, c5, c6, q, x = rec
+        for cols, vals in zip(xcols, x):
+            for col, v in zip(cols, vals):
+                col.append(v)
         words.append(wid)
         morphs.append(mid)
         tags.append(tid)
@@ -400,8 +431,12 @@ def pack(sentences, model, max_len=8, implicit_unk=True):
         node_f5=f64(f5), node_f6=f64(f6),
         node_post=f64(post).reshape(n_post, -1) if n_post else np.zeros((0, len(words))),
         edge_terms=n_edge, term_kinds=int(model.term_kinds), n_terms=len(model.plan),
-        unk_n=S if implicit else 0,
+        unk_n=S if implicit else 0, xtri_n=n_x,
     )
+    if n_x:
+        batch.xtri_mask = u32([c[0] for c in xcols]).reshape(n_x, -1)
+        batch.xtri_f4, batch.xtri_f5, batch.xtri_f6 = (f64([c[j] for c in xcols]).reshape(n_x, -1)
+                                                        for j in (1, 2, 3))
     if implicit:
         col = lambda i: [r[i] for r in canon]      # noqa: E731
         batch.unk_word, batch.unk_morph0, batch.unk_tag = i32(col(0)), i32(col(1)), i32(col(2))

@@ -22,7 +22,8 @@ class _ModelDesc(C.Structure):
 
 
 class _BatchDesc(C.Structure):
-    # include/lattice_decode.h lt_batch_desc (ABI 5); edge terms unused here
+    # include/lattice_decode.h lt_batch_desc (ABI 6); edge terms and further
+    # trigram terms unused here (ref_beam.py restates those composites)
     _fields_ = [('n_sent', C.c_int32), ('max_len', C.c_int32), ('n_post', C.c_int32),
                 ('has_trigram', C.c_int32), ('n_nodes', C.c_int64), ('n_span', C.c_int64)] + [
         (f, C.c_void_p) for f in ('sent_n', 'sent_node_off', 'sent_span_off', 'span_start',
@@ -32,7 +33,8 @@ class _BatchDesc(C.Structure):
         ('n_edges', C.c_int64), ('sent_edge_off', C.c_void_p), ('node_edge_base', C.c_void_p),
         ('edge_val', C.c_void_p), ('n_unk', C.c_int32)] + [
         (f, C.c_void_p) for f in ('unk_word', 'unk_morph0', 'unk_tag', 'unk_mask', 'unk_pre',
-                                  'unk_f4', 'unk_f5', 'unk_f6', 'unk_post')]
+                                  'unk_f4', 'unk_f5', 'unk_f6', 'unk_post')] + [
+        ('n_xtri', C.c_int32)] + [(f, C.c_void_p) for f in ('xtri_mask', 'xtri_f4', 'xtri_f5', 'xtri_f6')]
 
 
 _lib = None
@@ -67,6 +69,9 @@ _UNK_DT = {'unk_word': np.int32, 'unk_morph0': np.int32, 'unk_tag': np.int32, 'u
 
 
 def decode(packed, keys, coefs, k, s0=0, s1=None, nthreads=1):
+    if int(getattr(packed, 'xtri_n', 0)):
+        raise NotImplementedError('lt_oracle.c restates one trigram term; oracle/ref_beam.py restates '
+                                  'composites with several')
     lib = load()
     arr = {f: np.ascontiguousarray(getattr(packed, f), dtype=dt) for f, dt in _DT.items()}
     n_post = int(packed.n_post)

@@ -183,7 +183,8 @@ def make_sentences(dic, n_sent, n_eojeol, seed):
 
 
 def main():
-    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'lookup', 'wide', 'plugins']
+    sets = sys.argv[1:] or ['base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'lookup', 'wide', 'plugins',
+                            'multitri']
 
     if 'base' in sets:
         d = BaseMorphemeDictionary()
@@ -257,6 +258,9 @@ def main():
                 cases.append(case(b, c, name, funcs, tag='scorers'))
         dump('scorers', models, cases)
 
+    if 'multitri' in sets:
+        dump_multitri()
+
     if 'edge' in sets:
         dump_edge()
 
@@ -271,6 +275,37 @@ def main():
 
     if 'plugins' in sets:
         dump_plugins()
+
+
+def dump_multitri():
+    """Composites with several SimpleTrigramFeatureScores (score_funcs.py:50-54
+    sums any scorers in order): two and three trigram terms over different
+    feature dictionaries, one scorer twice, node-local terms between them."""
+    raw = synth.make_lattices(24, seed=21, eojeols=6)
+    sm_a = synth.make_model(raw, seed=21, n_features=4000)
+    sm_b = synth.make_model(raw, seed=22, n_features=2500)
+    lats, dic_a, coef_a = synth.to_words(raw, sm_a, word_cls=Word)
+    _, dic_b, coef_b = synth.to_words(raw, sm_b, word_cls=Word)
+    tri_a = SimpleTrigramFeatureScore(SimpleTrigramEncoder(dic_a), coef_a)
+    tri_b = SimpleTrigramFeatureScore(SimpleTrigramEncoder(dic_b), coef_b)
+    rng = np.random.default_rng(23)
+    tri_c = SimpleTrigramFeatureScore(SimpleTrigramEncoder(dic_a), rng.normal(0, 0.5, len(dic_a)))
+    reg = RegularizationScore(unknown_penalty=-0.3, known_preference=0.15, syllable_penalty=-0.05)
+    mp = MorphemePreferenceScore({'Noun': {'x1': 0.75, 'x2': 1}, 'Verb': {'x3': -0.5}})
+    composites = {
+        'two_tri': BeamScoreFunctions(reg, tri_a, tri_b),
+        'tri_sandwich': BeamScoreFunctions(tri_b, mp, tri_a, reg),
+        'three_tri': BeamScoreFunctions(tri_c, reg, tri_b, tri_a),
+        'same_twice': BeamScoreFunctions(tri_a, tri_a),
+    }
+    models = {k: [spec_of(f) for f in v.funcs] for k, v in composites.items()}
+    cases = []
+    for name, funcs in composites.items():
+        for b, c in lats:
+            cases.append(case(b, c, name, funcs, tag='multitri'))
+    for b, c in lats[:4]:
+        cases.append(case(b, c, 'two_tri', composites['two_tri'], max_len=12, tag='multitri_wide'))
+    dump('multitri', models, cases)
 
 
 def dump_plugins():

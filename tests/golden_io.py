@@ -18,6 +18,9 @@ SETS = ('base', 'demo', 'synth', 'scorers', 'edge', 'dense', 'wide')
 # sets whose composites hold user plugins (tests/plugin_defs.py), which the C
 # restatement (oracle/lt_oracle.c) does not evaluate
 PLUGIN_SETS = ('plugins',)
+# composites with several SimpleTrigramFeatureScores (round 6): the general
+# kernel; the C restatement (one trigram term) does not take them
+MULTI_SETS = ('multitri',)
 EdgeTableScore = make_edge_table_class(BeamScoreFunction)
 
 

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi():
     lib = _capi.load()
-    assert lib.lt_abi_version() == _capi.ABI_VERSION == 5
+    assert lib.lt_abi_version() == _capi.ABI_VERSION == 6
     assert lib.lt_device_count() >= 0
 
 

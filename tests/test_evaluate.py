@@ -5,7 +5,7 @@ the reference returned (make_golden.py).  CPU: the restated scorers; GPU:
 
 import pytest
 
-from golden_io import PLUGIN_SETS, SETS, load
+from golden_io import MULTI_SETS, PLUGIN_SETS, SETS, load
 from lattice_based_tagger_amd import evaluate_batch
 from lattice_based_tagger_amd.word import Word, bos_word, eos_word
 
@@ -38,7 +38,7 @@ class _Seq:
         self.sequences = words
 
 
-@pytest.mark.parametrize('name', SETS + PLUGIN_SETS)
+@pytest.mark.parametrize('name', SETS + PLUGIN_SETS + MULTI_SETS)
 def test_cpu_evaluate_matches_reference(name):
     paths = _paths(name)
     assert paths
@@ -47,7 +47,7 @@ def test_cpu_evaluate_matches_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', SETS)
+@pytest.mark.parametrize('name', SETS + MULTI_SETS)
 def test_gpu_evaluate_batch_matches_reference(gpu_decoder, name):
     groups = {}
     for funcs, words, hexv in _paths(name):

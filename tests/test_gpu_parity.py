@@ -12,14 +12,14 @@
 import numpy as np
 import pytest
 
-from golden_io import SETS, beams_of, load, path_matches
+from golden_io import MULTI_SETS, SETS, beams_of, load, path_matches
 from lattice_based_tagger_amd import _capi, beam_search, beam_search_batch, synth
 from oracle import lt_oracle
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('name', SETS)
+@pytest.mark.parametrize('name', SETS + MULTI_SETS)
 def test_golden_vectors_on_gpu(gpu_decoder, name):
     cases = load(name)
     groups = {}

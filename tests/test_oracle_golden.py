@@ -3,11 +3,11 @@ pinned against the reference's own outputs (tests/golden)."""
 
 import pytest
 
-from golden_io import PLUGIN_SETS, SETS, load, path_matches
+from golden_io import MULTI_SETS, PLUGIN_SETS, SETS, load, path_matches
 from oracle import ref_beam
 
 
-@pytest.mark.parametrize('name', SETS + PLUGIN_SETS)
+@pytest.mark.parametrize('name', SETS + PLUGIN_SETS + MULTI_SETS)
 def test_ref_beam_matches_reference(name):
     n_checked = 0
     for case in load(name):

@@ -8,7 +8,7 @@ every mature."""
 import numpy as np
 import pytest
 
-from golden_io import SETS, load
+from golden_io import MULTI_SETS, SETS, load
 from lattice_based_tagger_amd import Word
 from lattice_based_tagger_amd.beam import lowered_model, path_score_type, typed_score
 from lattice_based_tagger_amd.word import bos_word
@@ -26,7 +26,7 @@ def _path(case, codes):
     return out
 
 
-@pytest.mark.parametrize('name', SETS)
+@pytest.mark.parametrize('name', SETS + MULTI_SETS)
 def test_path_score_type_matches_reference(name):
     seen = set()
     for case in load(name):
