@@ -784,11 +784,12 @@ static void arena_free(lt_arena& a) {
 }
 
 // Arenas up to this size are kept for reuse, at most SPARE_N per context
-// (Tagger.tag_batch keeps three chunk batches in flight, one more is queued)
+// (Tagger.tag_batch keeps up to four chunk batches in flight, one more is
+// queued)
 // and at most SPARE_BYTES (device + pinned host) in all: the largest batches
 // seen do not pin gigabytes for the context's lifetime.
 constexpr size_t SPARE_MAX = (size_t)1 << 30;
-constexpr size_t SPARE_N = 4;
+constexpr size_t SPARE_N = 6;
 constexpr size_t SPARE_BYTES = (size_t)3 << 30;
 
 static size_t arena_bytes(const lt_arena& a) { return a.d_bytes + a.h_bytes; }
@@ -1870,13 +1871,18 @@ lt_status lt_result_fetch_packed(lt_ctx* c, lt_batch* b) {
   if (b->last_k < 1) return fail(LT_EINVAL, "lt_result_fetch_packed: no decode launched");
   HIP_TRY(hipSetDevice(c->device));
   const int i = b->cur;
-  // everything on the copy stream, under the next decode: pack the slot
-  // (once per decode), copy the used bytes
+  // the pack (once per decode) on the decode stream, right behind the
+  // decode: its kernels take the CUs briefly between two decodes (round 6:
+  // on the copy stream, beside the next decode, they kept its LDS-filling
+  // blocks waiting -- k=1 0.56 -> 0.72 ms); the DMA of the slab on the copy
+  // stream, under the next decode; the slot's reader event after the DMA
   if (b->res[i].packed_launch != b->launch_serial) {
-    HIP_TRY(pack_last_results_on(b, lt_batch::RD_COPY, b->res[i].slab, c->cstream));
+    HIP_TRY(pack_last_results_on(b, lt_batch::RD_COPY, b->res[i].slab, c->stream));
     b->res[i].packed_launch = b->launch_serial;
   }
+  HIP_TRY(hipStreamWaitEvent(c->cstream, b->ev_rd[i][lt_batch::RD_COPY], 0));
   HIP_TRY(launch_slab_to_host(b->res[i].slab, b->h_slab, b->slab_cap, c->cstream));
+  HIP_TRY(slot_read(b, lt_batch::RD_COPY, c->cstream));
   return LT_OK;
 }
 

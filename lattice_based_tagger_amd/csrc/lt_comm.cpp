@@ -148,6 +148,7 @@ struct lt_comm {
   hipEvent_t done[2] = {nullptr, nullptr};
   hipEvent_t g0[2] = {nullptr, nullptr}, g1[2] = {nullptr, nullptr};
   hipEvent_t fetched[2] = {nullptr, nullptr};   // root: copy of receive slot i to the host queued
+  hipEvent_t packed[2] = {nullptr, nullptr};    // send slot i packed (on the decode stream)
   bool fetch_pending[2] = {false, false};
   // root: pinned mirror of one receive block (nranks slabs at stride cap)
   char* h_slabs = nullptr;
@@ -218,6 +219,7 @@ lt_status lt_comm_create(lt_ctx* ctx, int nranks, int rank, const uint8_t id[LT_
     e = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&c->g0[i]);
     if (e == hipSuccess) e = hipEventCreate(&c->g1[i]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->packed[i], hipEventDisableTiming);
   }
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->fetched[i], hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -238,7 +240,7 @@ lt_status lt_comm_destroy(lt_comm* c) {
   for (hipEvent_t ev : c->fetched)
     if (ev) (void)hipEventDestroy(ev);
   for (int i = 0; i < 2; ++i) {
-    hipEvent_t evs[] = {c->done[i], c->g0[i], c->g1[i]};
+    hipEvent_t evs[] = {c->done[i], c->g0[i], c->g1[i], c->packed[i]};
     for (hipEvent_t ev : evs)
       if (ev) (void)hipEventDestroy(ev);
   }
@@ -317,16 +319,23 @@ lt_status lt_gather_launch(lt_comm* c, lt_batch* b) {
   const int i = c->next;
   const bool at_root = c->rank == c->root;
   HIP_TRY(hipSetDevice(x->device));
-  // everything on the communicator stream (the decode stream goes on with
-  // the next decode): on the root, the host copy of receive slot i must be
-  // done with it; the decode's results are packed into send slot i (whose
-  // previous gather precedes on this stream), then gathered
+  // the decode's results are packed into send slot i on the decode stream,
+  // right behind the decode (round 6: packed on the communicator stream, the
+  // pack kernels' blocks took CUs beside the next decode, whose LDS-filling
+  // blocks then waited -- a k=1 decode 0.56 -> 0.72 ms with the packed-result
+  // copy on one GPU); slot i's previous gather must be done with it.  The
+  // gather itself runs on the communicator stream (the decode stream goes on
+  // with the next decode); on the root, the host copy of receive slot i must
+  // be done with it first
+  if (c->used[i]) HIP_TRY(hipStreamWaitEvent(x->stream, c->done[i], 0));
+  HIP_TRY(lt::pack_last_results_on(b, lt_batch::RD_GATHER, c->send[i], x->stream));
+  HIP_TRY(hipEventRecord(c->packed[i], x->stream));
   if (at_root && c->fetch_pending[i]) {
     HIP_TRY(hipStreamWaitEvent(c->stream, c->fetched[i], 0));
     c->fetch_pending[i] = false;
   }
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->packed[i], 0));
   HIP_TRY(hipEventRecord(c->g0[i], c->stream));
-  HIP_TRY(lt::pack_last_results_on(b, lt_batch::RD_GATHER, c->send[i], c->stream));
   // one gather of the padded slabs (the used part of each is what the root
   // copies to the host)
   NCCL_TRY(r.gather(c->send[i], at_root ? c->recv[i] : nullptr, c->cap, ncclUint8, c->root, c->comm,

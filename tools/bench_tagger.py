@@ -73,9 +73,10 @@ def main():
     if a.chunk:
         Tagger.CHUNK = a.chunk
     # warm-up, as a service does once at start: model lowering, device model,
-    # and the pipeline's batch arenas at chunk size (three chunks in flight;
-    # the context recycles them for every later call)
-    tagger.tag_batch(sents[:3 * Tagger.CHUNK], beam_size=a.k)
+    # and the pipeline's batch arenas at chunk size (up to four chunks in
+    # flight since round 6's decode stage; the context recycles them for every
+    # later call)
+    tagger.tag_batch(sents[:5 * Tagger.CHUNK], beam_size=a.k)
     model = lowered_model(funcs)
     npk = packer_for(model)
     best = {}
