@@ -24,6 +24,14 @@ tail -1 $O/pytest_gpu.log
 cd $R && TAG=$TAG bash tools/gpu_prof.sh || exit 1
 cp $R/gpurun_out/prof_$TAG/traffic.json $R/profiles/${TAG}_traffic.json
 cp $R/gpurun_out/prof_$TAG/traffic.json $O/traffic.json
+# round 6: the SQ counter set per k (VALU / LDS instructions, LDS bank
+# conflicts, VALU busy) -> the issue roofline bench.py reads
+# (profiles/**/sq_summary*.json, tied to this source by its hash)
+cd $R && OUT=evidence_$TAG/sq LIBS=base KS="${KS:-1 5 16}" timeout -k 10 900 bash tools/gpu_sq_ab.sh > $O/sq.log 2>&1 \
+  || { echo SQ_FAIL; tail -20 $O/sq.log; exit 1; }
+mkdir -p $R/profiles/$TAG
+python3 $R/tools/sq_summary.py $O/sq base $R/profiles/$TAG/sq_summary.json || exit 1
+cp $R/profiles/$TAG/sq_summary.json $O/sq_summary.json
 cd $R
 timeout -k 10 600 python3 -u bench.py > $O/bench_default.log 2>&1 || { echo BENCH_FAIL; tail -30 $O/bench_default.log; exit 1; }
 tail -1 $O/bench_default.log > $O/bench_default.jsonl
