@@ -989,6 +989,9 @@ __device__ __forceinline__ void k1_wave_sents(const DecodeParams& p, int slot0, 
   }
 }
 
+#ifndef K1_FILL_AUX
+#define K1_FILL_AUX 0                   // cache policy of the fill's row stores (2: nontemporal; A/B)
+#endif
 constexpr int K1_NCAP = 192;                    // end positions per sentence whose counts the schedule kernel keeps in LDS
 constexpr int K1_RT = 16;                       // schedule rows per LDS tile of the fill
 
@@ -1208,7 +1211,8 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
     const int nr = min(K1_RT, nrow - R0);
 #pragma unroll
     for (int r = 0; r < K1_RT; ++r)
-      if (r < nr) __builtin_amdgcn_raw_buffer_store_b32(tile[r][lane], out, (uint32_t)lane * 4u, (R0 + r) * 256, 0);
+      if (r < nr) __builtin_amdgcn_raw_buffer_store_b32(tile[r][lane], out, (uint32_t)lane * 4u, (R0 + r) * 256,
+                                                        K1_FILL_AUX);
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }

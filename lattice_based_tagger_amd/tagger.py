@@ -197,6 +197,9 @@ class Tagger:
 
     # sentences per pipeline chunk of tag_batch
     CHUNK = 4096
+    # pipeline stages of tag_batch: 4 (decode + path preparation on a worker)
+    # or 3 (the caller decodes and materialises; rounds 2-5); LT_TAGGER_STAGES
+    STAGES = int(__import__('os').environ.get('LT_TAGGER_STAGES', '4'))
 
     def tag_batch(self, sents, beam_size=5):
         """Best ``Sequence`` per sentence.  Raises IndexError like ``tag``
@@ -224,6 +227,38 @@ class Tagger:
         finally:
             if enabled:
                 gc.enable()
+
+    @staticmethod
+    def _pipeline3(chunks, lat0, front, upload, finish):
+        """The three-stage pipeline (builder, uploader, the caller decoding
+        and materialising)."""
+        from collections import deque
+        from concurrent.futures import ThreadPoolExecutor
+        out = []
+        with ThreadPoolExecutor(max_workers=1) as builder, ThreadPoolExecutor(max_workers=1) as uploader:
+            stages = deque()
+
+            def feed(i):
+                if i < len(chunks):
+                    stages.append(uploader.submit(upload, i, builder.submit(front, chunks[i],
+                                                                            lat0 if i == 0 else None)))
+            feed(0)
+            feed(1)
+            try:
+                for i in range(len(chunks)):
+                    lat, packed, views, dbs = stages.popleft().result()
+                    feed(i + 2)
+                    out += finish(i, lat, packed, views, dbs)
+            finally:
+                for f in stages:                   # an error: drop what is still in flight
+                    f.cancel()
+                    if not f.cancelled():
+                        try:
+                            for _, _, db in f.result()[3] or ():
+                                db.close()
+                        except BaseException:
+                            pass
+        return out
 
     def _tag_native(self, lex, sents, beam_size):
         from collections import deque
@@ -280,6 +315,8 @@ class Tagger:
             dec = decoder(0)
             dbs = dec.upload(model, packed, k) if dec is not None and packed is not None else None
             return finish(0, lat, packed, views, dbs)
+        if self.STAGES == 3:
+            return self._pipeline3(chunks, lat0, front, upload, finish)
 
         def decode(i, fut):                        # the decode stage (worker): device + path preparation
             lat, packed, views, dbs = fut.result()

@@ -37,13 +37,15 @@ def main():
         if not m:
             continue
         k = int(m.group(1))
+        # the decode kernel of beam k (lt_decode.hip kernel_name_for); the
+        # table also holds the counting launch's kernel (lt_beam_pk's COUNT
+        # variant for k = 2..8), which is not the decode
+        kernel = 'lt_viterbi_pk' if k <= 1 else 'lt_beam_hw' if k <= 8 else 'lt_beam_pk'
         ctr = {}
-        kernel = None
         for line in open(os.path.join(d, f)):
             t = line.split()
-            if len(t) < 4 or not t[0].startswith('lt_') or t[0].startswith(('lt_k1_sched', 'lt_strip')):
+            if len(t) < 4 or re.sub(r'<.*', '', t[0]) != kernel:
                 continue
-            kernel = re.sub(r'<.*', '', t[0])
             ctr[t[1]] = float(t[3].split('=')[1])
         if not ctr:
             continue
