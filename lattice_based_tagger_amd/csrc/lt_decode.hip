@@ -990,7 +990,11 @@ __device__ __forceinline__ void k1_wave_sents(const DecodeParams& p, int slot0, 
 }
 
 #ifndef K1_FILL_AUX
-#define K1_FILL_AUX 0                   // cache policy of the fill's row stores (2: nontemporal; A/B)
+// cache policy of the fill's row stores: nontemporal (the rows are read once,
+// by the decode; written through, they displaced table lines the decode right
+// after needed -- fresh-batch step 0.752-0.771 -> 0.698-0.736 ms,
+// profiles/r06/ab_fill_nt/)
+#define K1_FILL_AUX 2
 #endif
 constexpr int K1_NCAP = 192;                    // end positions per sentence whose counts the schedule kernel keeps in LDS
 constexpr int K1_RT = 16;                       // schedule rows per LDS tile of the fill
