@@ -600,7 +600,6 @@ def main():
         fresh = {'value': total_sent_of(a, d, strong) / fel, 'unit': 'sentences/s',
                  'ms_per_step': fel / a.steps * 1e3, 'prep_ms_last': db.prep_ms(),
                  'prep_bytes': db.prep_bytes(), 'host_sched_ms': host_sched_ms,
-                 'ms_per_step_with_host_sched': fel / a.steps * 1e3 + (host_sched_ms or 0.0),
                  'step': 'lane-schedule build (lt_k1_sched) + decode + result D2H of a batch not decoded '
                          'before, batch resident in HBM (H2D excluded, as the headline)'}
     total_sent = total_sent_of(a, d, strong)
