@@ -961,6 +961,22 @@ __device__ __forceinline__ unsigned long long pk_stamp() {
 #define PK_STAMP(i) do { } while (0)
 #endif
 
+// the k=1 kernel's result stores: written once, read by the D2H copy --
+// nontemporal with K1_OUT_NT (A/B), so that they do not displace table lines
+// cache policy of the decoders' HBM backpointer stores (written once, read
+// back once by the backtrace; 2: nontemporal, A/B)
+#ifndef BM_BP_AUX
+#define BM_BP_AUX 0
+#endif
+#ifndef K1_OUT_NT
+#define K1_OUT_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ void k1_out(T* a, T v) {
+  if constexpr (K1_OUT_NT != 0) __builtin_nontemporal_store(v, a);
+  else *a = v;
+}
+
 // per-sentence static record (LDS)
 struct alignas(16) SentRec {
   uint32_t n, bp_lo, bp_hi, nbase;
@@ -1420,7 +1436,7 @@ lt_viterbi_pk(DecodeParams p) {
       if (e < BPL) bpl[wv][msr][e] = bpv;
       else bpoff = (uint32_t)(((((int64_t)si.bp_hi << 32) | si.bp_lo) + (int64_t)e * bstride) * 4);   // past the window
     }
-    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, bpoff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, bpoff, 0, BM_BP_AUX);
     __builtin_amdgcn_wave_barrier();
     PK_STAMP(7);                                 // [7] argmax (LDS atomics), ring + backpointer write
 #ifdef PK_PHASES
@@ -1435,12 +1451,12 @@ lt_viterbi_pk(DecodeParams p) {
   const int64_t cumn = own ? p.cum_n[sid] : 0;   // its first path-code slot
   if (own) {
     const VEntry& f = R[lane][nw % RING];
-    p.out_count[sid] = 1;
-    p.out_score[sid] = f.score + 0.0;
+    k1_out(&p.out_count[sid], 1);
+    k1_out(&p.out_score[sid], f.score + 0.0);
     // (depth <= n on a consistent beam: the unsigned clamp keeps a corrupted
     // entry from sending the stores below out of the sentence's code rows)
     pdepth = (int)min(f.depth, (uint32_t)nw);
-    p.out_len[sid] = (int32_t)pdepth;
+    k1_out(&p.out_len[sid], (int32_t)pdepth);
     int32_t* codes = p.out_codes + cumn;
     const uint32_t* bpg = p.bp + p.bp_off[sid];
     int pos = nw;
@@ -1453,13 +1469,13 @@ lt_viterbi_pk(DecodeParams p) {
     int step = pdepth - 1;
     for (; step >= 0 && pos >= BPL; --step) {
       const uint32_t v = bpg[(int64_t)pos * bstride];
-      codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
+      k1_out(&codes[step], path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN));
       pos -= (int)bp_d(v);
     }
     const uint32_t* const bw = bpl[wv][lane];
     for (; step >= 0 && pos > 0; --step) {
       const uint32_t v = bw[pos];
-      codes[step] = path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN);
+      k1_out(&codes[step], path_code(bp_node(v), pos, (int)bp_d(v), MAX_SPAN));
       pos -= (int)bp_d(v);
     }
   }
@@ -1471,7 +1487,7 @@ lt_viterbi_pk(DecodeParams p) {
     if (nw_w <= d_w) continue;                   // (uniform)
     const int64_t cb = ((int64_t)__builtin_amdgcn_readlane((int)(cumn >> 32), w) << 32) |
                        (uint32_t)__builtin_amdgcn_readlane((int)cumn, w);
-    for (int j = d_w + lane; j < nw_w; j += 64) p.out_codes[cb + j] = -1;
+    for (int j = d_w + lane; j < nw_w; j += 64) k1_out(&p.out_codes[cb + j], -1);
   }
 
   if (COUNT) {
@@ -2029,7 +2045,7 @@ lt_beam_pk(DecodeParams p) {
     }
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][wl] = ne;
-    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + wl) * 4u : OOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + wl) * 4u : OOB, 0, BM_BP_AUX);
     }
     if (lane == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
@@ -2513,7 +2529,7 @@ lt_beam_hw(DecodeParams p) {
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][hl] = ne;
     __builtin_amdgcn_raw_buffer_store_b32(
-        bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, 0);
+        bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, BM_BP_AUX);
     if (live && hl == 0) cnt9[em9] = nrun;
     __builtin_amdgcn_wave_barrier();
     PK_STAMP(4);

@@ -1,8 +1,11 @@
-# round 6 call e: Tagger.tag_batch with the four-stage pipeline against the
-# three-stage one (LT_TAGGER_STAGES), interleaved, five timed calls each
+# round 6 call e: the fresh-batch step with nontemporal schedule-row stores
+# in the fill (K1_FILL_AUX=2) against the current build, then
+# Tagger.tag_batch with the four-stage pipeline against the three-stage one
+# (LT_TAGGER_STAGES), interleaved, five timed calls each
 set -o pipefail
 mkdir -p gpurun_out/r6e
 export PYTHONUNBUFFERED=1
+LIBS="base fillnt" KS="1" ROUNDS=3 STEPS=20 timeout -k 10 600 bash tools/gpu_ab.sh > gpurun_out/r6e/ab.log 2>&1 && cat gpurun_out/r6e/ab.log &&
 for RD in 1 2; do
 for ST in 3 4; do
 for K in 1 5; do
