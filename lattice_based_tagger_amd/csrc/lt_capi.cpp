@@ -978,8 +978,20 @@ static hipError_t prep_fill(lt_batch* b, hipStream_t st) {
     e = launch_k1_sched_fill(p, b->pieces[q].d_wave_off, b->pieces[q].d_sched, st, q == 0 ? b->prep_ev0 : nullptr,
                              q + 1 == P ? b->prep_ev1 : nullptr);
   }
-  if (e == hipSuccess) b->prep_done = true;
+  if (e == hipSuccess) {
+    b->prep_done = true;
+    b->prep_fused = false;
+  }
   return e;
+}
+
+// LT_K1_FUSED_FILL (default 1): a fresh beam-1 schedule filled inside the decode
+static bool fused_fill_on() {
+  static const bool on = [] {
+    const char* v = std::getenv("LT_K1_FUSED_FILL");
+    return !(v && v[0] == '0');
+  }();
+  return on;
 }
 
 // The k=1 lane schedule of a batch created for larger beams, at its first
@@ -1188,7 +1200,8 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
           const int64_t steps = k1_schedule(
               cnt, nw, [&](int i, int e) { return k1_candidates(ssw[i], e, d->max_len); },
               [&](int64_t t, int i, int e, int off, int) {
-                plw[i][e - 1] = (uint32_t)t | ((uint32_t)off << K1_TBITS);   // (t < 2^K1_TBITS: checked below)
+                // (t < 2^K1_TBITS: checked below)
+                plw[i][e - 1] = k1_place_word(t, off, k1_dead_mask(ssw[i], e, d->max_len));
               });
           wo[(size_t)w + 1] = steps;
           int64_t m = longest.load();
@@ -1485,7 +1498,7 @@ lt_status lt_batch_prepare_k1(lt_batch* b) {
 lt_status lt_batch_prep_ms(lt_batch* b, float* ms) {
   if (!b || !ms) return fail(LT_EINVAL, "lt_batch_prep_ms: NULL argument");
   *ms = 0.0f;
-  if (!b->prep_ev0 || !b->prep_ev1) return LT_OK;
+  if (!b->prep_ev0 || !b->prep_ev1 || b->prep_fused) return LT_OK;
   HIP_TRY(hipEventElapsedTime(ms, b->prep_ev0, b->prep_ev1));
   return LT_OK;
 }
@@ -1577,6 +1590,7 @@ static void piece_params(const lt_batch* b, size_t q, int k, DecodeParams& p) {
   p.sched = b->has_sched ? pc.d_sched : nullptr;
   p.wave_off = b->has_sched ? pc.d_wave_off : nullptr;
   p.k1_place = b->has_sched ? pc.d_place : nullptr;
+  p.k1_fill = nullptr;                // (lt_decode_launch: a fresh schedule filled by the decode)
   p.n_edges = pc.n_edges;
   p.edge_base = pc.d_edge_base;
   p.edge_val = pc.d_edge_val;
@@ -1652,9 +1666,13 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   // the k=1 lane schedule, if the batch has not got it yet: queued in front
   // of the decode on its stream (lt_batch_create builds it for max_k = 1; a
   // batch for larger beams gets it here, at its first beam-1 decode)
+  bool fuse = false;
   if (!wide && beam_template_for(k) == 1) {
     if ((st = lazy_sched(c, b)) != LT_OK) return st;
-    HIP_TRY(prep_fill(b, c->stream));
+    // a schedule not filled yet is filled by the decode itself (p.k1_fill);
+    // LT_K1_FUSED_FILL=0: by the standalone fill kernel in front of it
+    fuse = b->has_sched && !b->prep_done && fused_fill_on();
+    if (!fuse) HIP_TRY(prep_fill(b, c->stream));
   }
   if ((st = next_slot(c, b)) != LT_OK) return st;
   const int r = (int)(c->n_launch % lt_ctx::KRING);
@@ -1662,6 +1680,7 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
   const int32_t wide_threads = p.wide_threads;
   for (size_t q = 0; q < P; ++q) {           // timing: start of the first piece .. end of the last
     piece_params(b, q, k, p);
+    p.k1_fill = fuse ? b->pieces[q].d_sched : nullptr;
     hipEvent_t e0 = q == 0 ? c->kev0[r] : nullptr, e1 = q + 1 == P ? c->kev1[r] : nullptr;
     if (wide) {
       p.wide_threads = std::max(1, std::min(wide_threads, p.n_sent));
@@ -1669,6 +1688,10 @@ lt_status lt_decode_launch(lt_ctx* c, const lt_model* m, lt_batch* b, int k) {
     } else {
       HIP_TRY(launch_decode(p, c->stream, false, e0, e1));
     }
+  }
+  if (fuse) {
+    b->prep_done = true;
+    b->prep_fused = true;
   }
   b->last_end = c->kev1[r];          // other streams wait for this decode here
   b->launch_serial = c->n_serial++;

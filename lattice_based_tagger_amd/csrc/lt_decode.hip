@@ -1014,6 +1014,7 @@ __device__ __forceinline__ void k1_wave_sents(const DecodeParams& p, int slot0, 
 #endif
 constexpr int K1_NCAP = 192;                    // end positions per sentence whose counts the schedule kernel keeps in LDS
 constexpr int K1_RT = 16;                       // schedule rows per LDS tile of the fill
+constexpr int K1_RT_FUSED = 12;                 // ... of the fill inside the beam-1 decode (its ring)
 
 // The schedule of a wave on the device, k1_schedule's rule with a lane per
 // sentence (lane w < W: sentence w's positions left, next end position, its
@@ -1099,7 +1100,7 @@ __device__ __forceinline__ int64_t k1_lane_schedule(const DecodeParams& p, const
       }
     }
     const bool mine = lane < W && ((take >> lane) & 1u);   // (a shift by 32 or more is not a zero)
-    if (mine) p.k1_place[cn + pos - 1] = (uint32_t)t | ((uint32_t)off << K1_TBITS);
+    if (mine) p.k1_place[cn + pos - 1] = k1_place_word(t, off, k1_dead_mask(p.span_start + so, pos, p.max_len));
     t += steps;
     if (mine) {
       ++pos;
@@ -1132,15 +1133,15 @@ __global__ void __launch_bounds__(64) lt_k1_sched_count(DecodeParams p, int64_t*
 // position's span starts loaded together) -- and copied out by coalesced
 // 256 B stores.  A sentence's positions are placed in increasing macro-steps,
 // so a cursor per sentence (its first position not yet complete) bounds the
-// positions a tile can hold: at most one per macro-step, K1_RT.
-template <int W>
-__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
-  __shared__ uint32_t tile[K1_RT][64];
-  __shared__ int curs[W];
-  const int wave = blockIdx.x;
-  const int lane = (int)threadIdx.x;
+// positions a tile can hold: at most one per macro-step, RT.  One wave (lane
+// = threadIdx.x & 63) fills wave schedule `wave`; tile: RT x 64 words of LDS,
+// curs: W words (the standalone fill lt_k1_sched, or the beam-1 decode of a
+// batch without its schedule, p.k1_fill).
+template <int W, int RT>
+__device__ __forceinline__ void k1_fill_wave(const DecodeParams& p, int wave, const int64_t* wave_off,
+                                             uint32_t* sched, uint32_t (*tile)[64], int* curs) {
+  const int lane = (int)(threadIdx.x & 63);
   const int slot0 = wave * W;
-  if (slot0 >= p.n_sent) return;
   int nS[W];
   uint32_t nbS[W];
   int64_t soS[W], cnS[W];
@@ -1159,13 +1160,16 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
   for (int w = 0; w < W; ++w)
     if (g == w) { ng = nS[w]; nbg = nbS[w]; sog = soS[w]; cng = cnS[w]; }
   const uint32_t wb = (uint32_t)g << 26;
-  static_assert(K1_RT == 16, "two positions per lane per tile");
-  for (int R0 = 0; R0 < nrow; R0 += K1_RT) {
+  static_assert(RT <= 16, "a tile's positions of a sentence: at most RT, lanes cover 16");
+  for (int R0 = 0; R0 < nrow; R0 += RT) {
 #pragma unroll
-    for (int r = 0; r < K1_RT; ++r) tile[r][lane] = K1_IDLE;
+    for (int r = 0; r < RT; ++r) tile[r][lane] = K1_IDLE;
     const int cur = g < W ? curs[g] : 1;
     // positions cur + j8 and cur + 8 + j8: placements and span starts together
+    // ss: the position's span starts; dm: its dead implicit Unknowns
+    // (k1_dead_mask, from the placement word)
     int ss[2][MAX_SPAN + 1], t0[2], q0[2];
+    uint32_t dm[2];
     bool in[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1176,8 +1180,9 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
 #pragma unroll
       for (int jj = 0; jj <= MAX_SPAN; ++jj) ss[h][jj] = in[h] ? src[jj] : 0;
       t0[h] = (int)(v & ((1u << K1_TBITS) - 1u));
-      in[h] = in[h] && t0[h] < R0 + K1_RT;
-      q0[h] = (int)(v >> K1_TBITS);
+      in[h] = in[h] && t0[h] < R0 + RT;
+      q0[h] = (int)((v >> K1_TBITS) & 63u);
+      dm[h] = v >> K1_DBITS;
     }
     int done = 0;                                // positions of sentence g completed in this tile
 #pragma unroll
@@ -1193,8 +1198,10 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
 #pragma unroll
         for (int jj = 0; jj < MAX_SPAN; ++jj) {
           const int a = ss[h][jj];
-          const bool unk = a == ss[h][jj + 1] && MAX_SPAN - jj <= dmax;
-          cnt[jj] = unk ? 1 : ss[h][jj + 1] - a;
+          const int d = MAX_SPAN - jj;
+          const bool unk = a == ss[h][jj + 1] && d <= dmax;
+          const bool dead = d < MAX_SPAN && ((dm[h] >> (d - 1)) & 1u);   // (k1_unk_dead)
+          cnt[jj] = dead ? 0 : unk ? 1 : ss[h][jj + 1] - a;
           // entry i: node nbg + a + i, or the slot's implicit Unknown (d - 1 = 7 - jj)
           e0v[jj] = (unk ? (K1_UNK | (uint32_t)(MAX_SPAN - 1 - jj)) : nbg + (uint32_t)a) | wb;
           run += cnt[jj];
@@ -1215,27 +1222,35 @@ __global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t*
 #pragma unroll 1
             for (int i = 0; i < cnt[jj]; ++i, ++q) {
               const int row = t0[h] + (q >> 6) - R0;
-              if (row >= 0 && row < K1_RT) tile[row][q & 63] = (e0v[jj] + (uint32_t)i) | (q < 64 ? K1_FIRST : 0u);
+              if (row >= 0 && row < RT) tile[row][q & 63] = (e0v[jj] + (uint32_t)i) | (q < 64 ? K1_FIRST : 0u);
             }
           }
         }
         last = t0[h] + ((q - 1) >> 6);
       }
-      const bool complete = in[h] && last < R0 + K1_RT;
+      const bool complete = in[h] && last < R0 + RT;
       const unsigned long long cm = __builtin_amdgcn_ballot_w64(complete);
       done += __builtin_popcount((uint32_t)(cm >> (g * 8)) & 0xFFu);
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     if (j8 == 0 && g < W) curs[g] = cur + done;
-    const int nr = min(K1_RT, nrow - R0);
+    const int nr = min(RT, nrow - R0);
 #pragma unroll
-    for (int r = 0; r < K1_RT; ++r)
+    for (int r = 0; r < RT; ++r)
       if (r < nr) __builtin_amdgcn_raw_buffer_store_b32(tile[r][lane], out, (uint32_t)lane * 4u, (R0 + r) * 256,
                                                         K1_FILL_AUX);
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
+}
+
+template <int W>
+__global__ void __launch_bounds__(64) lt_k1_sched(DecodeParams p, const int64_t* wave_off, uint32_t* sched) {
+  __shared__ uint32_t tile[K1_RT][64];
+  __shared__ int curs[W];
+  if ((int)blockIdx.x * W >= p.n_sent) return;
+  k1_fill_wave<W, K1_RT>(p, (int)blockIdx.x, wave_off, sched, tile, curs);
 }
 
 template <int W, bool NARROW, bool COUNT, bool GEN = true>
@@ -1247,8 +1262,8 @@ lt_viterbi_pk(DecodeParams p) {
   __shared__ uint32_t bpl[P_WPB][W][BPL];
   __shared__ uint4 stg[P_WPB][REC_CHUNKS * 64];
   __shared__ SentRec srec[P_WPB][W];
-  __shared__ unsigned long long amax[P_WPB][2][W];
-  __shared__ uint32_t amin[P_WPB][2][W];
+  __shared__ unsigned long long amax[P_WPB][W];  // the sentence's argmax at its current end position
+  __shared__ uint32_t amin[P_WPB][W];
   __shared__ uint32_t sep[P_WPB][W];            // sentence w's current end position e | (e % RING) << 24
   __shared__ double d3l[D3_DIM * D3_DIM];
   __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records (as staged ones)
@@ -1269,6 +1284,19 @@ lt_viterbi_pk(DecodeParams p) {
   const int wave = blockIdx.x * P_WPB + wv;
   const int slot0 = wave * W;
   if (slot0 >= p.n_sent) return;                // whole wave
+  if (p.k1_fill) {
+    // a batch's first beam-1 decode (fresh schedule): the wave fills its own
+    // rows first (the standalone fill's work, k1_fill_wave), over LDS the
+    // decode initialises only after it -- the wave's ring as the row tile,
+    // its sep words as the cursors -- so the fill's load latency overlaps the
+    // other waves' decoding instead of running as a kernel of its own
+    static_assert(sizeof(ring[0]) >= K1_RT_FUSED * 64 * 4, "the fused fill's tile fits the wave's ring");
+    k1_fill_wave<W, K1_RT_FUSED>(p, wave, p.wave_off, p.k1_fill, reinterpret_cast<uint32_t (*)[64]>(&ring[wv][0][0]),
+                                 reinterpret_cast<int*>(&sep[wv][0]));
+    __builtin_amdgcn_s_waitcnt(0);               // the rows are stored before the first schedule load
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
   const Bufs B = make_bufs(p);
   const uint32_t slots = p.slots, seed = p.seed;
   const int has_tri = p.has_tri;
@@ -1302,8 +1330,8 @@ lt_viterbi_pk(DecodeParams p) {
     R[lane][0] = v_bos(load_cand(B, nbase));  // beam[0] = [BOS] (beam.py:21-23)
   }
   if (lane < W) {
-    amax[wv][0][lane] = 0ull; amax[wv][1][lane] = 0ull;
-    amin[wv][0][lane] = INV; amin[wv][1][lane] = INV;
+    amax[wv][lane] = 0ull;
+    amin[wv][lane] = INV;
     sep[wv][lane] = 0u;
   }
   // this wave's macro-steps in the lane schedule
@@ -1334,7 +1362,9 @@ lt_viterbi_pk(DecodeParams p) {
     const int msr = (int)((ent >> 26) & 7u);     // (0 for an idle lane)
     // the lane's sentence's end position: it moves to the next one at the
     // first macro-step of that position (every lane of the segment writes the
-    // same value; a wave's LDS operations complete in order)
+    // same value; a wave's LDS operations complete in order), which also
+    // clears the sentence's argmax words for it -- long before this step's
+    // argmax, and after every LDS access of the previous position's steps
     const bool first = (ent & K1_FIRST) != 0;
     const uint32_t sp0 = sep[wv][msr];
     int e = (int)(sp0 & 0xFFFFFFu), em9 = (int)(sp0 >> 24);
@@ -1342,10 +1372,10 @@ lt_viterbi_pk(DecodeParams p) {
       ++e;
       em9 = em9 == RING - 1 ? 0 : em9 + 1;
       sep[wv][msr] = (uint32_t)e | ((uint32_t)em9 << 24);
+      amax[wv][msr] = 0ull;
+      amin[wv][msr] = INV;
     }
-    const uint32_t spo = lane < W ? sep[wv][lane] : 0u;   // (owner lanes: their sentence's, updated)
     const int dmax = min(e, p.max_len);
-    const int cb = e & 1;
     // this lane's candidate: its staged record, or the implicit Unknown's
     const Cand cur = cand_lds32(imp ? ucan + 2u * (ent & 7u) : wst + 2 * lane, 1, pxl, B, imp ? INV : gn0);
     const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
@@ -1415,18 +1445,13 @@ lt_viterbi_pk(DecodeParams p) {
 #else
     const unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
 #endif
-    const unsigned long long mprev = (key && !first) ? amax[wv][cb][msr] : 0ull;
-    if (key) __hip_atomic_fetch_max(&amax[wv][cb][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const unsigned long long mk = key ? amax[wv][cb][msr] : 0ull;
+    const unsigned long long mprev = (key && !first) ? amax[wv][msr] : 0ull;
+    if (key) __hip_atomic_fetch_max(&amax[wv][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned long long mk = key ? amax[wv][msr] : 0ull;
     const bool top = key && key == mk;
-    if (top && mk != mprev) amin[wv][cb][msr] = INV;
-    if (top) __hip_atomic_fetch_min(&amin[wv][cb][msr], gk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t mgw = top ? amin[wv][cb][msr] : INV;
-    if (lane < W) {                              // reset the other parity for the sentence's next position
-      const int cbo = (int)(spo & 1u) ^ 1;
-      amax[wv][cbo][lane] = 0ull;
-      amin[wv][cbo][lane] = INV;
-    }
+    if (top && mk != mprev) amin[wv][msr] = INV;
+    if (top) __hip_atomic_fetch_min(&amin[wv][msr], gk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t mgw = top ? amin[wv][msr] : INV;
     uint32_t bpv = 0u, bpoff = OOB;
     if (top && mgw == gk) {                      // the (step's) winner writes beam[e]
       const SentRec si = srec[wv][msr];
@@ -1509,6 +1534,31 @@ lt_viterbi_pk(DecodeParams p) {
     atomicAdd(p.counters + 14, 1ull);
   }
 #endif
+}
+
+// The beam kernels' per-position word (their LDS ring cnt9): beam[e]'s size
+// in the low 16 bits, the number of its hypotheses whose last word is not
+// Unknown in the high 16.  An implicit Unknown of span (b, e) with b > b_min
+// is skipped after every hypothesis whose last word is Unknown (num_unk
+// counts the Unknowns at the tail: beam.py:43-45, Sequence.add :112-113), so
+// its span slot expands only the others: the slot's expansions enumerate
+// them alone, in rank order (the ring's live-rank list, LR[b][q] = the rank
+// of the q-th), which keeps the generation order of the expansions scored.
+// (A position without explicit nodes has none: the k=1 schedule's static
+// rule, lt_internal.h k1_unk_dead.)
+constexpr int CNT_BEAM = 0xFFFF;
+__device__ __forceinline__ int cnt_entry(int beam, int live) { return beam | (live << 16); }
+// hypotheses of span slot d (<= dmax) that expand: beam[e - d]'s size, or its
+// non-Unknown hypotheses for an empty slot's implicit Unknown past b_min
+__device__ __forceinline__ int cnt_live(int cv, bool empty, int d, int dmax) {
+  return (empty && d < dmax) ? (cv >> 16) : (cv & CNT_BEAM);
+}
+// lt_beam_pk (one sentence per wave, 64-lane rounds): such a slot expands all
+// of beam[e - d] unless none of it survives -- the per-expansion skip takes
+// the rest (a live-rank lookup in its expansion decode cost more than the
+// expansions it saved: k=16 10.55 -> 10.99 ms)
+__device__ __forceinline__ int cnt_any(int cv, bool empty, int d, int dmax) {
+  return (empty && d < dmax && (cv >> 16) == 0) ? 0 : (cv & CNT_BEAM);
 }
 
 // ===========================================================================
@@ -1741,7 +1791,7 @@ lt_beam_pk(DecodeParams p) {
 
   if (lane == 0) {                              // beam[0] = [BOS] (beam.py:21-23)
     R[0][0] = v_bos(load_cand(B, nbase));
-    cnt9[0] = 1;
+    cnt9[0] = cnt_entry(1, 1);
   }
   // The next position's first 64 records (lane t holds 16 B chunks t,
   // 64 + t, 128 + t of the block: consecutive lanes read consecutive bytes)
@@ -1792,8 +1842,11 @@ lt_beam_pk(DecodeParams p) {
 #pragma unroll
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
-      const int c = (d <= dmax) ? cnt9[(e - d) % RING] : 0;
-      // (an empty in-range slot holds its implicit Unknown)
+      const int cv = (d <= dmax) ? cnt9[(e - d) % RING] : 0;
+      // (an empty in-range slot holds its implicit Unknown, which needs no
+      // expansion when every hypothesis of beam[e - d] ends in Unknown:
+      // cnt_entry; the others are skipped per expansion)
+      const int c = cnt_any(cv, ss[j + 1] == ss[j], d, dmax);
       pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)max(ss[j + 1] - ss[j], 1));   // (c <= 256, m < 2^21)
     }
     const int M = pre[MAX_SPAN];
@@ -2019,6 +2072,7 @@ lt_beam_pk(DecodeParams p) {
     // block (a position with more than STAGE candidates) takes a separate,
     // uniform path with global loads, so the common path has no load to wait
     // for (and does not wait for the prefetch above).
+    int nlive = 0;                              // beam[e]'s hypotheses not ending in Unknown
     for (int w0 = 0; w0 < (BIG ? nrun : 1); w0 += 64) {   // one pass unless the beam exceeds 64
     const int wl = w0 + lane;                   // winner (rank) of this lane
     VEntry ne;
@@ -2045,9 +2099,10 @@ lt_beam_pk(DecodeParams p) {
     }
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][wl] = ne;
+    nlive += __builtin_popcountll(__builtin_amdgcn_ballot_w64(writer && !(ne.meta & F_UNK)));
     __builtin_amdgcn_raw_buffer_store_b32(bpv, bpr, writer ? (uint32_t)(e * bstride + wl) * 4u : OOB, 0, BM_BP_AUX);
     }
-    if (lane == 0) cnt9[em9] = nrun;
+    if (lane == 0) cnt9[em9] = cnt_entry(nrun, nlive);
     __builtin_amdgcn_wave_barrier();
     PK_STAMP(4);
 #ifdef PK_PHASES
@@ -2061,7 +2116,7 @@ lt_beam_pk(DecodeParams p) {
   // matures = beam[n] + EOS (beam.py:59-61); backtrace per mature rank
   __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): the backpointer stores are done
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const int nm = cnt9[n % RING];
+  const int nm = cnt9[n % RING] & CNT_BEAM;
   if (lane == 0) p.out_count[s] = nm;
   if constexpr (!BIG) {
     // (one mature per lane) the final entries, then the backpointer rows
@@ -2186,6 +2241,7 @@ lt_beam_hw(DecodeParams p) {
   static_assert(KT <= G && G >= MAX_SPAN + 1, "one writer lane per rank in a group; span starts fit a group");
   __shared__ VEntry ring[WPB][S][RING][KT];
   __shared__ int32_t cntl[WPB][S][RING];
+  __shared__ uint8_t lrkl[WPB][S][RING][KT];    // live-rank lists (cnt_entry)
   __shared__ uint4 stg[WPB][S * CPG];           // group h's record r: chunks CPG h + 2r, +1
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][S][LN];
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][S][LN];
@@ -2239,6 +2295,7 @@ lt_beam_hw(DecodeParams p) {
   }
   const rsrc_t bpr = make_rsrc_own(p.bp, (uint64_t)p.bp_bytes);
   VEntry (*const R)[KT] = ring[wv][hf];
+  uint8_t (*const LR)[KT] = lrkl[wv][hf];
   int32_t* const cnt9 = cntl[wv][hf];
   unsigned long long* const LK = lkey[wv][hf];
   uint32_t* const LG = lgen[wv][hf];
@@ -2249,7 +2306,8 @@ lt_beam_hw(DecodeParams p) {
 
   if (hv && hl == 0) {                          // beam[0] = [BOS] (beam.py:21-23)
     R[0][0] = v_bos(load_cand(B, nbase));
-    cnt9[0] = 1;
+    LR[0][0] = 0;
+    cnt9[0] = cnt_entry(1, 1);
   }
   if (HW_SPRE && hl == 0) spre[wv][hf][0] = 0;
   // next position's first STAGE records of every group (chunk c = 64 pl +
@@ -2323,9 +2381,12 @@ lt_beam_hw(DecodeParams p) {
       int term = 0;
       if (hl < MAX_SPAN) {
         const int d = MAX_SPAN - hl;
-        const int c = (live && d <= dmax) ? cnt9[ring_back(em9, d)] : 0;
-        // (an empty in-range slot holds its implicit Unknown)
-        term = (int)__umul24((uint32_t)c, (uint32_t)max(sst[wv][hf][hl + 1] - pfs, 1));   // (c <= 256, m < 2^21)
+        const int cv = (live && d <= dmax) ? cnt9[ring_back(em9, d)] : 0;
+        const int m = sst[wv][hf][hl + 1] - pfs;
+        // (an empty in-range slot holds its implicit Unknown, which needs no
+        // expansion when it is statically dead: cnt_dead)
+        const int c = cnt_live(cv, m == 0, d, dmax);
+        term = (int)__umul24((uint32_t)c, (uint32_t)max(m, 1));   // (c <= 256, m < 2^21)
       }
       term += __builtin_amdgcn_update_dpp(0, term, 0x111, 0xF, 0xF, true);      // row_shr:1
       term += __builtin_amdgcn_update_dpp(0, term, 0x112, 0xF, 0xF, true);      // row_shr:2
@@ -2343,7 +2404,8 @@ lt_beam_hw(DecodeParams p) {
 #pragma unroll
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
-      const int c = (live && d <= dmax) ? cnt9[(e - d) % RING] : 0;
+      const int cv = (live && d <= dmax) ? cnt9[(e - d) % RING] : 0;
+      const int c = cnt_live(cv, ss[j + 1] == ss[j], d, dmax);
       pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)max(ss[j + 1] - ss[j], 1));   // (c <= 256, m < 2^21)
     }
 #endif
@@ -2406,7 +2468,8 @@ lt_beam_hw(DecodeParams p) {
                             (imp || !act) ? INV : nbase + (uint32_t)node);
         beam_far(c, far, B, nbase + (uint32_t)node);
         const int hb = act ? ring_back(em9, d) : 0;
-        const int hr = act ? r : 0;
+        // (an implicit Unknown past b_min: the r-th hypothesis not ending in Unknown)
+        const int hr = !act ? 0 : (imp && d < dmax) ? (int)LR[hb][r] : r;
         const VEntry h0 = R[hb][hr];
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
         const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
@@ -2528,9 +2591,13 @@ lt_beam_hw(DecodeParams p) {
     }
     __builtin_amdgcn_wave_barrier();
     if (writer) R[em9][hl] = ne;
+    // the live-rank list of beam[e] (cnt_entry)
+    const bool xw = writer && !(ne.meta & F_UNK);
+    const uint32_t xb = (uint32_t)((__builtin_amdgcn_ballot_w64(xw) & hmask) >> (G * hf));
+    if (xw) LR[em9][__builtin_popcount(xb & ((1u << hl) - 1u))] = (uint8_t)hl;
     __builtin_amdgcn_raw_buffer_store_b32(
         bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, BM_BP_AUX);
-    if (live && hl == 0) cnt9[em9] = nrun;
+    if (live && hl == 0) cnt9[em9] = cnt_entry(nrun, __builtin_popcount(xb));
     __builtin_amdgcn_wave_barrier();
     PK_STAMP(4);
 #ifdef PK_PHASES
@@ -2548,7 +2615,7 @@ lt_beam_hw(DecodeParams p) {
   // ring (stage_bp_rows) when they fit
   constexpr int RW = (int)(RING * KT * sizeof(VEntry) / 4);
   constexpr int CAP = RW < BP_STAGE_PER_LANE * G ? RW : BP_STAGE_PER_LANE * G;
-  const int nm = hv ? cnt9[n % RING] : 0;
+  const int nm = hv ? cnt9[n % RING] & CNT_BEAM : 0;
   double fs = 0.0;
   int fd = 0;
   if (hv && hl < k && hl < nm) {

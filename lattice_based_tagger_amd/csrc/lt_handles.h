@@ -88,7 +88,9 @@ struct lt_batch {
   // batch has them (max_len <= 8; at create for max_k = 1, else at the first
   // beam-1 decode -- lazy_sched: then in buffers of their own, not the
   // arena); prep_done = the fill kernels are queued
-  bool has_sched = false, prep_done = false, lazy_sched = false;
+  // prep_fused = the last fill ran inside the beam-1 decode (p.k1_fill; no
+  // prep events of its own)
+  bool has_sched = false, prep_done = false, lazy_sched = false, prep_fused = false;
   double host_sched_ms = 0.0;          // lt_batch_create's host schedule pass (wall time)
   hipEvent_t prep_ev0 = nullptr, prep_ev1 = nullptr;   // around the last fill
   // device inputs, per launch piece (lt_batch_create: node records and

@@ -60,7 +60,8 @@ struct DecodeParams {
   const uint32_t* sched;
   const int64_t* wave_off;
   uint32_t* k1_place;           // [piece chars] placement of (sentence s, end position e) at cum_n[s] + e - 1
-                                // (first macro-step | first lane << K1_TBITS; k1_schedule)
+                                // (k1_place_word: first macro-step, first lane, dead Unknowns; k1_schedule)
+  uint32_t* k1_fill;            // non-NULL: the beam-1 decode fills its waves' rows of sched (== this) first
   // scratch + results
   uint32_t* bp;
   int64_t bp_bytes;             // bytes of bp (< 2^31: 32-bit buffer offsets)
@@ -219,17 +220,51 @@ inline int k1_waves(int n_sent) { return (n_sent + K1_W - 1) / K1_W; }
 // sentence's next end position (the lane's sentence moves to it)
 constexpr uint32_t K1_NODE = 0x03FFFFFFu, K1_IDLE = K1_NODE, K1_UNK = 0x40000000u, K1_FIRST = 0x80000000u;
 // a wave's macro-steps stay below 2^K1_TBITS (lt_batch_create checks): the
-// fill packs a position's first macro-step and first lane into one word
-constexpr int K1_TBITS = 20;
+// fill packs a position's placement into one word -- first macro-step, first
+// lane << K1_TBITS, and the position's dead implicit Unknowns (k1_dead_mask)
+// << K1_DBITS
+constexpr int K1_TBITS = 19, K1_DBITS = 25;
+// A statically dead implicit Unknown.  The reference skips an Unknown
+// candidate of span (b, e) after a hypothesis whose last word is Unknown
+// (num_unk counts the Unknowns at the tail, Sequence.add beam.py:112-113)
+// unless b = b_min (beam.py:43-45).  Every hypothesis of beam[b] ends in a
+// candidate of end position b; when position b holds no explicit node, all of
+// them are implicit Unknowns, so every such hypothesis ends in an Unknown and
+// the candidate is skipped after each of them -- it needs no lane.  Position
+// b's explicit nodes are span_start[(b-1)*8 .. b*8); `ss` is the sentence's
+// span table, d the span length, dmax = min(e, max_len) (d < dmax <=> b >
+// b_min).  A conservative rule: an explicit node at b tagged Unknown keeps
+// the candidate (the kernel skips it at run time then).
+__host__ __device__ inline bool k1_unk_dead(const int32_t* ss, int e, int d, int dmax) {
+  const int b = e - d;
+  return d < dmax && ss[b * MAX_SPAN] == ss[(b - 1) * MAX_SPAN];
+}
+// the dead implicit Unknowns of end position e: bit d - 1 for span length d
+// (1..7; d = dmax is never dead)
+__host__ __device__ inline uint32_t k1_dead_mask(const int32_t* ss, int e, int max_len) {
+  const int dmax = e < max_len ? e : max_len;
+  uint32_t m = 0;
+  for (int d = 1; d < dmax; ++d) {
+    const int j = MAX_SPAN - d;
+    const bool empty = ss[(e - 1) * MAX_SPAN + j + 1] == ss[(e - 1) * MAX_SPAN + j];
+    m |= (empty && k1_unk_dead(ss, e, d, dmax)) ? 1u << (d - 1) : 0u;
+  }
+  return m;
+}
+// a placement word (K1_TBITS / K1_DBITS)
+__host__ __device__ inline uint32_t k1_place_word(int64_t t, int off, uint32_t dead) {
+  return (uint32_t)t | ((uint32_t)off << K1_TBITS) | (dead << K1_DBITS);
+}
 // candidates of a sentence at end position e (1 <= e <= n) from its span
 // table `ss` (8 slots per position): every slot's nodes, and one implicit
-// Unknown for an empty slot within max_len
+// Unknown for an empty slot within max_len that is not statically dead
 __host__ __device__ inline int k1_candidates(const int32_t* ss, int e, int max_len) {
   const int dmax = e < max_len ? e : max_len;
   int x = 0;
   for (int j = 0; j < MAX_SPAN; ++j) {
     const int c = ss[(e - 1) * MAX_SPAN + j + 1] - ss[(e - 1) * MAX_SPAN + j];
-    x += (c == 0 && MAX_SPAN - j <= dmax) ? 1 : c;
+    const int d = MAX_SPAN - j;
+    x += c != 0 ? c : (d <= dmax && !k1_unk_dead(ss, e, d, dmax)) ? 1 : 0;
   }
   return x;
 }

@@ -217,6 +217,39 @@ def test_k1_schedule_long_and_dense(gpu_decoder, case):
     assert np.array_equal(codes, o[3])
 
 
+@pytest.mark.parametrize('case', ['bench', 'long', 'dense'])
+def test_k1_fill_inside_decode(gpu_decoder, case):
+    """A batch whose beam-1 schedule is not filled yet (lt_batch_reset_prep:
+    the next decode rebuilds it; likewise a beam-5 batch's first beam-1 decode)
+    has it filled by the decode kernel itself (DecodeParams.k1_fill,
+    LT_K1_FUSED_FILL): each wave fills its own rows in its ring's LDS before
+    decoding.  Byte-equal to the C restatement, and to the decode of the
+    schedule the standalone fill built (at lt_batch_create), twice over."""
+    if case == 'bench':
+        packed, keys, coefs = _synthetic(4096, seed=6161, n_features=200_000)
+    elif case == 'long':
+        packed, keys, coefs = _synthetic(400, seed=6262, n_features=100_000, eojeols=90)
+    else:
+        packed, keys, coefs = _synthetic(300, seed=6363, n_features=100_000, eojeols=6,
+                                         extra_lambda=45.0, dup_rate=0.4)
+    dm = _capi.DeviceModel(gpu_decoder.ctx, keys, coefs)
+    db = _capi.DeviceBatch(gpu_decoder.ctx, packed, max_k=1)
+    try:
+        first = db.decode(dm, 1)                 # schedule filled at lt_batch_create
+        fused = []
+        for _ in range(2):
+            db.reset_prep()
+            fused.append(db.decode(dm, 1))
+    finally:
+        db.close()
+        dm.close()
+    o = lt_oracle.decode(packed, keys, coefs, 1, nthreads=16)
+    for count, length, score, codes in [first] + fused:
+        assert np.array_equal(count, o[0]) and np.array_equal(length, o[1])
+        assert np.array_equal(score.view(np.uint64), o[2].view(np.uint64))
+        assert np.array_equal(codes, o[3])
+
+
 def test_full_size_properties(gpu_decoder):
     """64K sentences, k=16: deterministic, sorted, and every path is a chain of
     spans from 0 to n made of the sentence's own nodes."""
