@@ -909,6 +909,14 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #ifndef HW_SPRE
 #define HW_SPRE 1
 #endif
+#ifndef HW_LIVE
+// lt_beam_hw: 1 = an implicit Unknown slot past b_min expands only the
+// hypotheses not ending in Unknown (live-rank lists, cnt_live); 0 = the slot
+// expands all of beam[b] unless none survives (cnt_any), the per-expansion
+// skip taking the rest.  A/B (profiles/r06/ab_hw_live/): 0 is faster, k=5
+// 3.82 -> 3.75 ms, k=2 1.90 -> 1.88, k=8 4.69 -> 4.60
+#define HW_LIVE 0
+#endif
 #ifndef HW_STAGE
 #define HW_STAGE 32                     // lt_beam_hw: records staged per wave and position
 #endif
@@ -2241,7 +2249,7 @@ lt_beam_hw(DecodeParams p) {
   static_assert(KT <= G && G >= MAX_SPAN + 1, "one writer lane per rank in a group; span starts fit a group");
   __shared__ VEntry ring[WPB][S][RING][KT];
   __shared__ int32_t cntl[WPB][S][RING];
-  __shared__ uint8_t lrkl[WPB][S][RING][KT];    // live-rank lists (cnt_entry)
+  __shared__ uint8_t lrkl[WPB][S][RING][HW_LIVE ? KT : 1];   // live-rank lists (cnt_entry; HW_LIVE)
   __shared__ uint4 stg[WPB][S * CPG];           // group h's record r: chunks CPG h + 2r, +1
   __shared__ __attribute__((aligned(16))) unsigned long long lkey[WPB][S][LN];
   __shared__ __attribute__((aligned(16))) uint32_t lgen[WPB][S][LN];
@@ -2295,7 +2303,7 @@ lt_beam_hw(DecodeParams p) {
   }
   const rsrc_t bpr = make_rsrc_own(p.bp, (uint64_t)p.bp_bytes);
   VEntry (*const R)[KT] = ring[wv][hf];
-  uint8_t (*const LR)[KT] = lrkl[wv][hf];
+  uint8_t (*const LR)[HW_LIVE ? KT : 1] = lrkl[wv][hf];
   int32_t* const cnt9 = cntl[wv][hf];
   unsigned long long* const LK = lkey[wv][hf];
   uint32_t* const LG = lgen[wv][hf];
@@ -2306,7 +2314,7 @@ lt_beam_hw(DecodeParams p) {
 
   if (hv && hl == 0) {                          // beam[0] = [BOS] (beam.py:21-23)
     R[0][0] = v_bos(load_cand(B, nbase));
-    LR[0][0] = 0;
+    if (HW_LIVE) LR[0][0] = 0;
     cnt9[0] = cnt_entry(1, 1);
   }
   if (HW_SPRE && hl == 0) spre[wv][hf][0] = 0;
@@ -2385,7 +2393,7 @@ lt_beam_hw(DecodeParams p) {
         const int m = sst[wv][hf][hl + 1] - pfs;
         // (an empty in-range slot holds its implicit Unknown, which needs no
         // expansion when it is statically dead: cnt_dead)
-        const int c = cnt_live(cv, m == 0, d, dmax);
+        const int c = HW_LIVE ? cnt_live(cv, m == 0, d, dmax) : cnt_any(cv, m == 0, d, dmax);
         term = (int)__umul24((uint32_t)c, (uint32_t)max(m, 1));   // (c <= 256, m < 2^21)
       }
       term += __builtin_amdgcn_update_dpp(0, term, 0x111, 0xF, 0xF, true);      // row_shr:1
@@ -2405,7 +2413,7 @@ lt_beam_hw(DecodeParams p) {
     for (int j = 0; j < MAX_SPAN; ++j) {
       const int d = MAX_SPAN - j;
       const int cv = (live && d <= dmax) ? cnt9[(e - d) % RING] : 0;
-      const int c = cnt_live(cv, ss[j + 1] == ss[j], d, dmax);
+      const int c = HW_LIVE ? cnt_live(cv, ss[j + 1] == ss[j], d, dmax) : cnt_any(cv, ss[j + 1] == ss[j], d, dmax);
       pre[j + 1] = pre[j] + (int)__umul24((uint32_t)c, (uint32_t)max(ss[j + 1] - ss[j], 1));   // (c <= 256, m < 2^21)
     }
 #endif
@@ -2469,7 +2477,7 @@ lt_beam_hw(DecodeParams p) {
         beam_far(c, far, B, nbase + (uint32_t)node);
         const int hb = act ? ring_back(em9, d) : 0;
         // (an implicit Unknown past b_min: the r-th hypothesis not ending in Unknown)
-        const int hr = !act ? 0 : (imp && d < dmax) ? (int)LR[hb][r] : r;
+        const int hr = !act ? 0 : (HW_LIVE && imp && d < dmax) ? (int)LR[hb][r] : r;
         const VEntry h0 = R[hb][hr];
         const bool skip = !act || ((h0.meta & F_UNK) && (c.mask & F_UNK) && (d < dmax));   // beam.py:43-45
         const uint32_t need = (!skip && has_tri) ? (c.mask & h0.meta & DQ_ALL) : 0u;
@@ -2594,7 +2602,7 @@ lt_beam_hw(DecodeParams p) {
     // the live-rank list of beam[e] (cnt_entry)
     const bool xw = writer && !(ne.meta & F_UNK);
     const uint32_t xb = (uint32_t)((__builtin_amdgcn_ballot_w64(xw) & hmask) >> (G * hf));
-    if (xw) LR[em9][__builtin_popcount(xb & ((1u << hl) - 1u))] = (uint8_t)hl;
+    if (HW_LIVE && xw) LR[em9][__builtin_popcount(xb & ((1u << hl) - 1u))] = (uint8_t)hl;
     __builtin_amdgcn_raw_buffer_store_b32(
         bpv, bpr, writer ? (uint32_t)((bpo + (int64_t)e * bstride + hl) * 4) : OOB, 0, BM_BP_AUX);
     if (live && hl == 0) cnt9[em9] = cnt_entry(nrun, __builtin_popcount(xb));
