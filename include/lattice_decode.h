@@ -223,18 +223,23 @@ typedef struct {
  * are computed here on the host (4 bytes per character, uploaded with the
  * batch), its memory is part of the batch's allocation, and its rows are
  * built on the device by a kernel on the upload stream (after
- * lt_batch_reset_prep: queued on the decode stream in front of the next
- * decode).  Neither blocks nor allocates.  A batch created for larger beams
- * gets none here (no host work, no arena bytes); its first beam-1 decode
- * builds one: steps and placements computed on the device, one host
- * synchronisation, buffers of its own (freed with the batch). */
+ * lt_batch_reset_prep: by the next beam-1 decode kernel itself, each of its
+ * waves filling its own rows before decoding; environment LT_K1_FUSED_FILL=0:
+ * by the fill kernel queued in front of it).  Neither blocks nor allocates.
+ * A batch created for larger beams gets none here (no host work, no arena
+ * bytes); its first beam-1 decode builds one: steps and placements computed
+ * on the device, one host synchronisation, buffers of its own (freed with
+ * the batch), the rows filled by that decode.  Candidates that the reference
+ * skips for sure take no lane: the implicit Unknown of a span (b, e) past
+ * b_min when end position b holds no explicit node (beam.py:43-45). */
 lt_status lt_batch_create(lt_ctx* ctx, const lt_batch_desc* desc, int max_k, lt_batch** out);
 lt_status lt_batch_destroy(lt_batch* batch);
 /* Benchmark hook: forget the device preparation, so that the next beam-1
  * decode rebuilds it on the decode stream (a "fresh batch" step). */
 lt_status lt_batch_reset_prep(lt_batch* batch);
 /* Device time (ms, HIP events) of the last device preparation of the batch;
- * valid once that work is complete (after lt_sync).  0 when none ran. */
+ * valid once that work is complete (after lt_sync).  0 when none ran as a
+ * kernel of its own (also when the decode filled the schedule). */
 lt_status lt_batch_prep_ms(lt_batch* batch, float* ms);
 /* Bytes of the batch's device preparation (the lane schedules and their wave
  * offsets) -- what a beam-1 decode reads of them.  Not counted: the
@@ -250,7 +255,8 @@ double lt_batch_host_sched_ms(const lt_batch* batch);
  * now, instead of at its first beam-1 decode: allocates, synchronises the
  * context stream once, and queues the schedule fill on it.  A pipeline calls
  * this off its launch path, so that no lt_decode_launch blocks.  No-op for a
- * batch that has one (or for max_len > LT_MAX_SPAN, decoded without). */
+ * batch that has one (or for max_len > LT_MAX_SPAN, decoded without).  Here
+ * the rows are filled by the standalone kernel. */
 lt_status lt_batch_prepare_k1(lt_batch* batch);
 /* Total path-code slots of the results for beam k: k * sum_s n_s. */
 int64_t lt_batch_code_slots(const lt_batch* batch, int k);

@@ -1,0 +1,7 @@
+# GPU suite + A/B of lt_beam_pk's single-round ranking by list position (base) against the generation compare (pkold)
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu --maxfail 6 -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+LIBS="pkold base" KS="16 12 32" ROUNDS=2 bash tools/gpu_ab.sh
