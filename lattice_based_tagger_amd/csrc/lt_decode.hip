@@ -658,15 +658,20 @@ struct V1Probe {
   uint32_t gneed, need2, pres;
 };
 
+// d3tab: the kernel's own LDS copy of the dense class-3 table (used when
+// aux.d3 is set) -- passed as the array itself, so that the compiler sees
+// that its reads cannot touch the record staging area (an LDS address from
+// a register would carry a wait for the record DMA in flight, K1_EARLY_DMA)
 template <bool NARROW>
 __device__ __forceinline__ void v1_issue(V1Probe<NARROW>& P, const Bufs& B, uint32_t slots, uint32_t seed,
-                                         const VEntry& h, const Cand& c, uint32_t need, const Aux& aux) {
+                                         const VEntry& h, const Cand& c, uint32_t need, const Aux& aux,
+                                         const double* d3tab) {
   using T = Tab<NARROW>;
   const V1Keys K = v1_keys(h, c);
   uint32_t gneed = need, pres = 0;
   P.cf[3] = -0.0;
   if (aux.d3 && ((need >> 3) & 1u)) {        // class 3 from the dense LDS table
-    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3mul)];
+    const double v = d3tab[d3_lds(h.jtag, c.tag, aux.d3mul)];
     const bool present = __builtin_bit_cast(uint64_t, v) != D3_ABSENT;
     P.cf[3] = present ? v : -0.0;
     pres = present ? 8u : 0u;
@@ -909,6 +914,12 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #ifndef HW_SPRE
 #define HW_SPRE 1
 #endif
+#ifndef PK_RANK_U
+#define PK_RANK_U 1                     // lt_beam_pk single-round ranking by list position (list_rank_u)
+#endif
+#ifndef HW_RANK_U
+#define HW_RANK_U 0                     // lt_beam_hw single-entry ranking by list_rank_u (A/B: k=5 3.75 -> 3.78 ms, k=2 1.87 -> 1.92, k=3 2.53 -> 2.49; off)
+#endif
 #ifndef HW_LIVE
 // lt_beam_hw: 1 = an implicit Unknown slot past b_min expands only the
 // hypotheses not ending in Unknown (live-rank lists, cnt_live); 0 = the slot
@@ -984,6 +995,36 @@ __device__ __forceinline__ void k1_out(T* a, T v) {
   if constexpr (K1_OUT_NT != 0) __builtin_nontemporal_store(v, a);
   else *a = v;
 }
+
+// Non-returning LDS atomics as inline asm.  The compiler puts a vmcnt(0) in
+// front of every LDS atomic while a buffer->LDS DMA may be in flight (it does
+// not for plain LDS reads and writes of other arrays): at k=1 that made the
+// per-sentence argmax wait for the next macro-step's record DMA every step.
+// (LDS operations of a wave complete in order, so a later read sees the
+// update; the compiler's lgkmcnt waits for its own reads stay correct, since
+// they count only operations younger than the read it waits for.)
+__device__ __forceinline__ uint32_t lds_addr(const void* a) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)a;
+}
+__device__ __forceinline__ __attribute__((unused)) void lds_max_u64(unsigned long long* a, unsigned long long v) {
+  asm volatile("ds_max_u64 %0, %1" ::"v"(lds_addr(a)), "v"(v) : "memory");
+}
+__device__ __forceinline__ __attribute__((unused)) void lds_min_u32(uint32_t* a, uint32_t v) {
+  asm volatile("ds_min_u32 %0, %1" ::"v"(lds_addr(a)), "v"(v) : "memory");
+}
+#ifndef K1_ASM_ATOMIC
+#define K1_ASM_ATOMIC 1                 // k=1 argmax atomics as inline asm (no DMA wait in front of them)
+#endif
+#ifndef K1_EARLY_DMA
+// k=1: 1 = the next macro-step's records DMA'd right after this step's
+// candidate record is read from the staging area (schedule entries loaded two
+// steps ahead), in flight with the primary probes.  Measured slower (0.539 vs
+// 0.526 ms, profiles/r06/ab_k1_dma/): VMEM completes in order, so the
+// primary-slot wait then also waits for the record DMA's longer HBM latency;
+// after the hit checks (0), the DMA overlaps the checks, the secondaries, the
+// sum and -- with K1_ASM_ATOMIC -- the argmax.
+#define K1_EARLY_DMA 0
+#endif
 
 // per-sentence static record (LDS)
 struct alignas(16) SentRec {
@@ -1351,6 +1392,9 @@ lt_viterbi_pk(DecodeParams p) {
     return ((ent & K1_NODE) == K1_NODE || (ent & K1_UNK)) ? INV : (ent & K1_NODE);
   };
   uint32_t ent = nsteps > 0 ? sch[0] : K1_IDLE;   // (a wave of empty sentences has no step)
+#if K1_EARLY_DMA
+  uint32_t ent1 = nsteps > 1 ? sch[64] : K1_IDLE;   // the next step's (its records go out early in this one)
+#endif
   dma_packed(B, node_of(ent), wst, lane);
   __builtin_amdgcn_raw_buffer_store_b32(0u, bpr, OOB, 0, 0);      // the invariant's first store
   __builtin_amdgcn_wave_barrier();
@@ -1362,8 +1406,13 @@ lt_viterbi_pk(DecodeParams p) {
     // backpointer store)
     __builtin_amdgcn_s_waitcnt(0x0F71);
     PK_STAMP(1);                                 // [1] wait for the staged records
+#if K1_EARLY_DMA
+    // the schedule entry two macro-steps ahead: arrives under this step's probes
+    const uint32_t ent2 = t + 2 < nsteps ? sch[(int64_t)(t + 2) * 64] : K1_IDLE;
+#else
     // the next macro-step's schedule entry: arrives under this step's probes
     const uint32_t ent1 = t + 1 < nsteps ? sch[(int64_t)(t + 1) * 64] : K1_IDLE;
+#endif
     const uint32_t gn0 = node_of(ent);
     const bool imp = (ent & K1_UNK) != 0;        // an implicit Unknown (its record from ucan)
     const bool act = gn0 != INV || imp;
@@ -1386,6 +1435,17 @@ lt_viterbi_pk(DecodeParams p) {
     const int dmax = min(e, p.max_len);
     // this lane's candidate: its staged record, or the implicit Unknown's
     const Cand cur = cand_lds32(imp ? ucan + 2u * (ent & 7u) : wst + 2 * lane, 1, pxl, B, imp ? INV : gn0);
+#if K1_EARLY_DMA
+    // the staging area is read: the next macro-step's records go out now, in
+    // flight with this step's ring reads and primary probes (no later LDS
+    // access of the step touches the staging area, so the compiler adds no
+    // wait for the DMA before them; the argmax atomics are asm, K1_ASM_ATOMIC)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
+    dma_packed(B, node_of(ent1), wst, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+#endif
     const int d0 = (int)((cur.mask & D_MASK) >> D_SHIFT) + 1;
     int bm0 = em9 - d0;
     bm0 += bm0 < 0 ? RING : 0;
@@ -1394,7 +1454,7 @@ lt_viterbi_pk(DecodeParams p) {
 
     V1Probe<NARROW> P;
     const uint32_t need = (!skip0 && has_tri) ? (cur.mask & h0.meta & DQ_ALL) : 0u;
-    v1_issue<NARROW>(P, B, slots, seed, h0, cur, need, aux);
+    v1_issue<NARROW>(P, B, slots, seed, h0, cur, need, aux, d3l);
 #ifdef PK_PHASES
     PK_STAMP(2);                                 // [2] records/ring reads, primary issue
     __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1406,12 +1466,14 @@ lt_viterbi_pk(DecodeParams p) {
     // issued after a buffer->LDS DMA waits for it (vmcnt).
     const VEntry h1 = R[msr][act ? bm0 : 0];
     v1_check<NARROW>(P, B, slots, seed, h1, cur, aux);
+#if !K1_EARLY_DMA
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
     dma_packed(B, node_of(ent1), wst, lane);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    v1_issue2<NARROW>(P, B, slots, seed, h1, cur, aux);   // secondaries: their wait covers the DMA too
+#endif
+    v1_issue2<NARROW>(P, B, slots, seed, h1, cur, aux);   // secondaries (K1_EARLY_DMA: the DMA is older)
 #ifdef PK_PHASES
     PK_STAMP(4);                                 // [4] hit checks, record DMA issue, secondary issue
     __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0)
@@ -1454,11 +1516,19 @@ lt_viterbi_pk(DecodeParams p) {
     const unsigned long long key = !skip0 ? ord_key(best_s) : 0ull;
 #endif
     const unsigned long long mprev = (key && !first) ? amax[wv][msr] : 0ull;
+#if K1_ASM_ATOMIC
+    if (key) lds_max_u64(&amax[wv][msr], key);
+#else
     if (key) __hip_atomic_fetch_max(&amax[wv][msr], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     const unsigned long long mk = key ? amax[wv][msr] : 0ull;
     const bool top = key && key == mk;
     if (top && mk != mprev) amin[wv][msr] = INV;
+#if K1_ASM_ATOMIC
+    if (top) lds_min_u32(&amin[wv][msr], gk);
+#else
     if (top) __hip_atomic_fetch_min(&amin[wv][msr], gk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     const uint32_t mgw = top ? amin[wv][msr] : INV;
     uint32_t bpv = 0u, bpoff = OOB;
     if (top && mgw == gk) {                      // the (step's) winner writes beam[e]
@@ -1476,6 +1546,9 @@ lt_viterbi_pk(DecodeParams p) {
     ++nsteps_done;
 #endif
     ent = ent1;
+#if K1_EARLY_DMA
+    ent1 = ent2;
+#endif
   }
 
   // matures = beam[n] + EOS (beam.py:59-61); backtrace, one owner lane per sentence
@@ -1638,6 +1711,35 @@ __device__ __forceinline__ int list_rank(const unsigned long long* LK, int q0, i
     const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
 #pragma unroll
     for (int u = 0; u < 4; ++u) rank += (kq[u] > ck || (kq[u] == ck && q + u < ci)) ? 1 : 0;
+  }
+  return rank;
+}
+
+// list_rank over wave-uniform bounds for lanes in groups of G (lt_beam_hw):
+// the lane's entry sits at list position base + (lane % G), so entry q ties
+// before it iff lane % G > q - base -- a lane mask made in scalar registers
+// per entry (inverse ballot) instead of a per-lane compare, and a scalar loop
+template <int G>
+__device__ __forceinline__ int list_rank_u(const unsigned long long* LK, int q0, int q1, unsigned long long ck,
+                                           int base) {
+  q0 = __builtin_amdgcn_readfirstlane(q0);
+  q1 = __builtin_amdgcn_readfirstlane(q1);
+  base = __builtin_amdgcn_readfirstlane(base);
+  constexpr unsigned long long REP = G == 64 ? 1ull : G == 32 ? 0x0000000100000001ull : 0x0001000100010001ull;
+  static_assert(G == 16 || G == 32 || G == 64, "lane groups of 16, 32 or 64");
+  int rank = 0;
+  for (int q = q0; q < q1; q += 4) {
+    const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
+    const ulonglong2 kb = *reinterpret_cast<const ulonglong2*>(&LK[q + 2]);
+    const unsigned long long kq[4] = {ka.x, ka.y, kb.x, kb.y};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int x = q + u - base;                // (uniform)
+      const unsigned long long gm = G == 64 ? ~0ull : (1ull << G) - 1ull;
+      const unsigned long long m = x < 0 ? gm : x >= G - 1 ? 0ull : ((gm << (x + 1)) & gm);
+      const bool before = __builtin_amdgcn_inverse_ballot_w64(m * REP);
+      rank += (kq[u] > ck || (kq[u] == ck && before)) ? 1 : 0;
+    }
   }
   return rank;
 }
@@ -1979,8 +2081,13 @@ lt_beam_pk(DecodeParams p) {
         if (t < R0) valid += __builtin_popcountll(__ballot(myk[t] != 0ull));
       if (R0 == 1 && nrun == 0) {
         // one entry per lane: rank against the 64 entries of the list
-        int rank = 0;
         const int qe = KTP + ((min(64, M - base) + 3) & ~3);   // entries past M are 0
+#if PK_RANK_U
+        // (the list holds the round's entries in generation order, lane l's at
+        // KTP + l: ties broken by list position, masks in scalar registers)
+        const int rank = list_rank_u<64>(LK, KTP, qe, myk[0], KTP);
+#else
+        int rank = 0;
 #pragma unroll 2
         for (int q = KTP; q < qe; q += 4) {
           const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&LK[q]);
@@ -1991,6 +2098,7 @@ lt_beam_pk(DecodeParams p) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) rank += (kq[u] > myk[0] || (kq[u] == myk[0] && gq[u] < myg[0])) ? 1 : 0;
         }
+#endif
         if (myk[0] != 0ull && rank < k) { tkey[wv][rank] = myk[0]; tgen[wv][rank] = myg[0]; }
       } else {
         // several entries per lane: prune with tau = the k-th largest of the
@@ -2513,7 +2621,14 @@ lt_beam_hw(DecodeParams p) {
         // slots of round 0 (slots past M hold 0 keys)
         const int qe = KTP + ((min(G, max(M - base, 0)) + 3) & ~3);
         const int qmax = gmax(qe);
+#if HW_RANK_U
+        {
+          const int r = list_rank_u<G>(LK, KTP, qmax, myk[0], KTP);
+          if (myk[0] != 0ull && r < k) { TK[r] = myk[0]; TG[r] = myg[0]; }
+        }
+#else
         rank_into(LK, KTP, qmax, myk[0], myg[0], KTP + hl, k, TK, TG);
+#endif
       } else {
         // threshold pruning (lt_beam_pk), per half: tau = the k-th largest of
         // the half's lane maxima
