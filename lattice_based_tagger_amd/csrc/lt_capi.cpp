@@ -1197,11 +1197,19 @@ lt_status lt_batch_create(lt_ctx* c, const lt_batch_desc* d, int max_k, lt_batch
             nw[cnt] = d->sent_n[s];
             plw[cnt] = place[q].data() + pcum[q][(size_t)sl];
           }
+          // run_at reaches every (sentence, position) once, before its
+          // placement: it leaves the position's dead mask in the placement
+          // word, which emit completes
           const int64_t steps = k1_schedule(
-              cnt, nw, [&](int i, int e) { return k1_candidates(ssw[i], e, d->max_len); },
+              cnt, nw,
+              [&](int i, int e) {
+                uint32_t dead = 0;
+                const int x = k1_candidates_dead(ssw[i], e, d->max_len, &dead);
+                plw[i][e - 1] = k1_place_word(0, 0, dead);
+                return x;
+              },
               [&](int64_t t, int i, int e, int off, int) {
-                // (t < 2^K1_TBITS: checked below)
-                plw[i][e - 1] = k1_place_word(t, off, k1_dead_mask(ssw[i], e, d->max_len));
+                plw[i][e - 1] |= k1_place_word(t, off, 0u);   // (t < 2^K1_TBITS: checked below)
               });
           wo[(size_t)w + 1] = steps;
           int64_t m = longest.load();

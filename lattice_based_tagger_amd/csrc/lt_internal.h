@@ -255,6 +255,27 @@ __host__ __device__ inline uint32_t k1_dead_mask(const int32_t* ss, int e, int m
 __host__ __device__ inline uint32_t k1_place_word(int64_t t, int off, uint32_t dead) {
   return (uint32_t)t | ((uint32_t)off << K1_TBITS) | (dead << K1_DBITS);
 }
+// k1_candidates and k1_dead_mask of one end position in one pass (the host
+// schedule: the count when a sentence reaches the position, the mask kept
+// for its placement word)
+__host__ __device__ inline int k1_candidates_dead(const int32_t* ss, int e, int max_len, uint32_t* dead) {
+  const int dmax = e < max_len ? e : max_len;
+  const int32_t* r = ss + (e - 1) * MAX_SPAN;
+  int x = 0;
+  uint32_t m = 0;
+  for (int j = 0; j < MAX_SPAN; ++j) {
+    const int c = r[j + 1] - r[j];
+    const int d = MAX_SPAN - j;
+    if (c != 0) {
+      x += c;
+    } else if (d <= dmax) {
+      if (d < dmax && k1_unk_dead(ss, e, d, dmax)) m |= 1u << (d - 1);
+      else x += 1;
+    }
+  }
+  *dead = m;
+  return x;
+}
 // candidates of a sentence at end position e (1 <= e <= n) from its span
 // table `ss` (8 slots per position): every slot's nodes, and one implicit
 // Unknown for an empty slot within max_len that is not statically dead
