@@ -917,6 +917,9 @@ __device__ __forceinline__ void v_count(Counts& cnt, const VEntry& h, const Cand
 #ifndef PK_RANK_U
 #define PK_RANK_U 1                     // lt_beam_pk single-round ranking by list position (list_rank_u)
 #endif
+#ifndef HW_D3_MAXKT
+#define HW_D3_MAXKT 4                   // lt_beam_hw: the dense class-3 table in LDS up to this KT
+#endif
 #ifndef HW_RANK_U
 #define HW_RANK_U 0                     // lt_beam_hw single-entry ranking by list_rank_u (A/B: k=5 3.75 -> 3.78 ms, k=2 1.87 -> 1.92, k=3 2.53 -> 2.49; off)
 #endif
@@ -955,6 +958,22 @@ __device__ __forceinline__ void dma_packed(const Bufs& B, uint32_t gn, uint4* wa
 #pragma unroll
   for (int pl = 0; pl < 2; ++pl) {
     const uint32_t o = nj[pl] != INV ? nj[pl] * (uint32_t)sizeof(NodeRec) + (uint32_t)(lane & 1) * 16u : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wave_planes + pl * 64), 16, o, 0, 0, PK_DMA_AUX);
+  }
+}
+
+// K1_DMA_DIRECT: DMA instruction pl has lane t fetch part pl of its own
+// record (chunks node*32 + 16 pl), so lane t's record lands at chunks t and
+// 64 + t: the staged-record reads are 16 B apart per lane (no bank
+// conflict) and no permute is needed; each instruction touches twice the
+// lines of the packed stream (dma_packed), the pair of them the same lines.
+#ifndef K1_DMA_DIRECT
+#define K1_DMA_DIRECT 0
+#endif
+__device__ __forceinline__ void dma_direct(const Bufs& B, uint32_t gn, uint4* wave_planes) {
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl) {
+    const uint32_t o = gn != INV ? gn * (uint32_t)sizeof(NodeRec) + (uint32_t)pl * 16u : OOB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(B.node, (lds_void*)(wave_planes + pl * 64), 16, o, 0, 0, PK_DMA_AUX);
   }
 }
@@ -1395,7 +1414,11 @@ lt_viterbi_pk(DecodeParams p) {
 #if K1_EARLY_DMA
   uint32_t ent1 = nsteps > 1 ? sch[64] : K1_IDLE;   // the next step's (its records go out early in this one)
 #endif
+#if K1_DMA_DIRECT
+  dma_direct(B, node_of(ent), wst);
+#else
   dma_packed(B, node_of(ent), wst, lane);
+#endif
   __builtin_amdgcn_raw_buffer_store_b32(0u, bpr, OOB, 0, 0);      // the invariant's first store
   __builtin_amdgcn_wave_barrier();
 
@@ -1434,7 +1457,11 @@ lt_viterbi_pk(DecodeParams p) {
     }
     const int dmax = min(e, p.max_len);
     // this lane's candidate: its staged record, or the implicit Unknown's
+#if K1_DMA_DIRECT
+    const Cand cur = cand_lds32(imp ? ucan + 2u * (ent & 7u) : wst + lane, imp ? 1 : 64, pxl, B, imp ? INV : gn0);
+#else
     const Cand cur = cand_lds32(imp ? ucan + 2u * (ent & 7u) : wst + 2 * lane, 1, pxl, B, imp ? INV : gn0);
+#endif
 #if K1_EARLY_DMA
     // the staging area is read: the next macro-step's records go out now, in
     // flight with this step's ring reads and primary probes (no later LDS
@@ -1442,7 +1469,11 @@ lt_viterbi_pk(DecodeParams p) {
     // wait for the DMA before them; the argmax atomics are asm, K1_ASM_ATOMIC)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
+#if K1_DMA_DIRECT
+    dma_direct(B, node_of(ent1), wst);
+#else
     dma_packed(B, node_of(ent1), wst, lane);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
 #endif
@@ -1469,7 +1500,11 @@ lt_viterbi_pk(DecodeParams p) {
 #if !K1_EARLY_DMA
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): cur is out of the staging area
+#if K1_DMA_DIRECT
+    dma_direct(B, node_of(ent1), wst);
+#else
     dma_packed(B, node_of(ent1), wst, lane);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
 #endif
@@ -2365,7 +2400,7 @@ lt_beam_hw(DecodeParams p) {
   __shared__ uint32_t tgen[WPB][S][KT];
   __shared__ __attribute__((aligned(16))) int sst[WPB][S][12];   // each group's span starts of the position
   __shared__ __attribute__((aligned(16))) int spre[WPB][S][HW_SPRE ? 12 : 1];   // and expansion prefixes
-  constexpr bool USE_D3 = KT <= 4;
+  constexpr bool USE_D3 = KT <= HW_D3_MAXKT;
   __shared__ uint4 ucan[REC_CHUNKS * MAX_SPAN]; // the implicit Unknowns' records
   // the batch's class-4/6 pair table (read per expansion: LDS, not the caches)
   __shared__ F46 pxl[MAX_PAIRS];
