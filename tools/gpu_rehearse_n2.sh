@@ -1,7 +1,9 @@
 # Two ranks on the one-GPU box (both on GPU 0): exercises the N>1 bench path
-# (gloo barriers, max-over-ranks timing, the strong split of one batch and
-# rank 0's check, the gather setup and its every-rank-or-none fallback --
-# RCCL refuses two ranks on one GPU).  ARGS: extra bench.py arguments.
+# (the host group's barriers, max-over-ranks timing, the strong split of one
+# batch and rank 0's check).  RCCL refuses two ranks on one GPU, so with the
+# default RCCL gather every rank reports the failed setup and exits 3 (by
+# design: no silent fallback); ARGS="--gather 0" times the ranks each copying
+# their own results.  ARGS: extra bench.py arguments.
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
