@@ -186,6 +186,7 @@ struct lt_model {
   int narrow = 0;          // 16 B SlotN (all ids < 2^20) or 32 B SlotW
   double* d_d3 = nullptr;    // dense class-3 table or NULL
   uint32_t d3mul = 0;
+  uint32_t d3off = 0;        // its bit window (d3_window; set when d_d3 is)
 };
 
 namespace {
@@ -392,6 +393,18 @@ static void build_dense3(const std::vector<KeyRec>& keys, uint32_t& mul, std::ve
   std::sort(vals.begin(), vals.end());
   vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
   if (vals.size() > (size_t)D3_DIM) return;
+  // bit windows first (d3_window), then odd multipliers
+  for (int off = 0; off <= 32 - D3_BITS && !mul; ++off) {
+    const uint32_t cand = 1u << (32 - D3_BITS - off);
+    uint64_t used = 0;
+    bool inj = true;
+    for (uint32_t v : vals) {
+      const uint64_t bit = 1ull << d3_index(v, cand);
+      if (used & bit) { inj = false; break; }
+      used |= bit;
+    }
+    if (inj) mul = cand;
+  }
   uint32_t m = 0x9E3779B1u;
   for (int trial = 0; trial < 20000 && !mul; ++trial, m = m * 0x2C1B3C6Du + 0x297A2D39u) {
     const uint32_t cand = m | 1u;
@@ -549,8 +562,11 @@ static lt_status model_upload(lt_ctx* c, const lt_model_image* v, lt_model** out
     e = hipMemcpyAsync(m->d_table, v->table, (size_t)v->table_bytes, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMalloc(&m->d_plain, (size_t)v->table_bytes);
   if (e == hipSuccess) e = launch_strip_flags(m->d_plain, m->d_table, v->table_bytes, m->narrow != 0, c->stream);
-  if (e == hipSuccess && v->d3mul) {
+  // (an image whose multiplier is not a bit window -- a pack from an older
+  // build -- decodes without the dense table: class 3 from the hashed table)
+  if (e == hipSuccess && v->d3mul && d3_window(v->d3mul) >= 0) {
     m->d3mul = v->d3mul;
+    m->d3off = (uint32_t)d3_window(v->d3mul);
     e = dalloc_copy(&m->d_d3, v->d3, (size_t)D3_DIM * D3_DIM, c->stream);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1560,7 +1576,7 @@ static lt_status fill_params(lt_ctx* c, const lt_model* m, lt_batch* b, int k, D
   p.seed = m->seed;
   p.hk = narrow_hash(m->seed);
   p.d3 = m->d_d3;
-  p.d3mul = m->d3mul;
+  p.d3off = m->d3off;
   p.narrow = m->narrow;
   p.has_tri = b->has_tri;
   p.max_len = b->max_len;
@@ -1781,7 +1797,7 @@ lt_status lt_evaluate(lt_ctx* c, const lt_model* m, const lt_paths_desc* d, doub
     p.narrow = m->narrow;
     p.has_tri = d->trigram_pos >= 0 ? 1 : 0;
     p.d3 = m->d_d3;
-    p.d3mul = m->d3mul;
+    p.d3off = m->d3off;
     p.n_paths = d->n_paths;
     p.n_words = d->n_words;
     p.words = d_words;

@@ -258,6 +258,16 @@ constexpr int D3_BITS = 5;
 constexpr int D3_DIM = 1 << D3_BITS;
 constexpr uint64_t D3_ABSENT = 0x7FF5A5A55A5A0001ull;     // a NaN payload
 LT_HD uint32_t d3_index(uint32_t v, uint32_t mul) { return (v * mul) >> (32 - D3_BITS); }
+// A multiplier 2^(27 - off) makes d3_index the bit window v[off, off + 5):
+// the library tries those first (the interned tags are a short run of ids,
+// so a window separates them), and the kernels take the window as one
+// bit-field extract instead of a 32-bit multiply.  Its offset, or -1 for any
+// other multiplier (the kernels then probe class 3 in the hashed table).
+LT_HD int d3_window(uint32_t mul) {
+  for (int off = 0; off <= 32 - D3_BITS; ++off)
+    if (mul == (1u << (32 - D3_BITS - off))) return off;
+  return -1;
+}
 
 // Device node record (AoS, 32 B = 2 x 16 B loads), built by the library from
 // the SoA arrays of lt_batch_desc.  The node's class-4 and class-6

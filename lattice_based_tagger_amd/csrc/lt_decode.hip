@@ -211,7 +211,7 @@ __device__ __forceinline__ double numpy_sum9(const double (&v)[9], const bool (&
 // LDS-resident parts of the model a block stages at its start.
 struct Aux {
   const double* d3;       // dense class-3 table (D3_DIM^2) or nullptr
-  uint32_t d3mul;
+  uint32_t d3off;
   NarrowHash hk;          // narrow table slot hash
 };
 
@@ -361,9 +361,11 @@ __device__ __forceinline__ uint32_t probe_need(const Hyp& h, const Cand& c) {
 #ifndef LT_D3_SWIZZLE
 #define LT_D3_SWIZZLE 1                 // 0: the unswizzled layout (A/B builds)
 #endif
-__device__ __forceinline__ uint32_t d3_lds(uint32_t jtag, uint32_t ktag, uint32_t mul) {
-  const uint32_t r = d3_index(jtag, mul);
-  return (r << D3_BITS) | (d3_index(ktag, mul) ^ (LT_D3_SWIZZLE ? r : 0u));
+// (off: the table's bit window, d3_window -- d3_index of its multiplier as
+// one bit-field extract)
+__device__ __forceinline__ uint32_t d3_lds(uint32_t jtag, uint32_t ktag, uint32_t off) {
+  const uint32_t r = __builtin_amdgcn_ubfe(jtag, off, D3_BITS);
+  return (r << D3_BITS) | (__builtin_amdgcn_ubfe(ktag, off, D3_BITS) ^ (LT_D3_SWIZZLE ? r : 0u));
 }
 // copy the host-layout table src (row-major) into the swizzled LDS layout
 __device__ __forceinline__ void d3_stage(const double* __restrict__ src, double* dst) {
@@ -381,7 +383,7 @@ __device__ __forceinline__ Aux stage_aux(const DecodeParams& p, double* d3l) {
   if (p.d3) d3_stage(p.d3, d3l);
   if (p.d3) __syncthreads();
   a.d3 = p.d3 ? d3l : nullptr;
-  a.d3mul = p.d3mul;
+  a.d3off = p.d3off;
   a.hk = p.hk;
   return a;
 }
@@ -398,7 +400,7 @@ __device__ __forceinline__ void probe_issue(Probe<NARROW, BOTH>& P, const Bufs& 
   uint32_t gneed = need, lpres = 0;
   // class 3 from the dense LDS table (the first scorer's class-3 keys only)
   if (aux.d3 && coff == 0 && ((need >> 3) & 1u)) {
-    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3mul)];
+    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3off)];
     P.s1[3].coef = v;
     gneed &= ~8u;
     lpres |= (__builtin_bit_cast(uint64_t, v) != D3_ABSENT) ? 8u : 0u;
@@ -671,7 +673,7 @@ __device__ __forceinline__ void v1_issue(V1Probe<NARROW>& P, const Bufs& B, uint
   uint32_t gneed = need, pres = 0;
   P.cf[3] = -0.0;
   if (aux.d3 && ((need >> 3) & 1u)) {        // class 3 from the dense LDS table
-    const double v = d3tab[d3_lds(h.jtag, c.tag, aux.d3mul)];
+    const double v = d3tab[d3_lds(h.jtag, c.tag, aux.d3off)];
     const bool present = __builtin_bit_cast(uint64_t, v) != D3_ABSENT;
     P.cf[3] = present ? v : -0.0;
     pres = present ? 8u : 0u;
@@ -786,7 +788,7 @@ __device__ __forceinline__ void bm_issue(BMProbe<NARROW>& P, const Bufs& B, uint
   P.cf3 = -0.0;
   P.pres3 = 0;
   if (aux.d3 && ((need >> 3) & 1u)) {
-    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3mul)];
+    const double v = aux.d3[d3_lds(h.jtag, c.tag, aux.d3off)];
     const bool present = __builtin_bit_cast(uint64_t, v) != D3_ABSENT;
     P.cf3 = present ? v : -0.0;
     P.pres3 = present ? 8u : 0u;
@@ -2851,7 +2853,7 @@ static int beam_group_lanes(int k) { return k <= 3 ? 16 : 32; }
 template <bool NARROW>
 __global__ void __launch_bounds__(256) lt_eval_words_k(EvalParams p) {
   __shared__ double d3l[D3_DIM * D3_DIM];
-  Aux aux{nullptr, p.d3mul, p.hk};
+  Aux aux{nullptr, p.d3off, p.hk};
   if (p.d3) {
     d3_stage(p.d3, d3l);
     __syncthreads();

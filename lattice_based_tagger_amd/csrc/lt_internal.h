@@ -13,7 +13,7 @@ struct DecodeParams {
   uint32_t seed;
   NarrowHash hk;                // narrow tables: slot hash constants (from seed)
   const double* d3;             // dense class-3 table (D3_DIM^2) or NULL
-  uint32_t d3mul;
+  uint32_t d3off;               // the dense class-3 table's bit window (lt_common.h d3_window)
   int32_t narrow;               // 1: SlotN, 0: SlotW
   int32_t has_tri;
   // batch (device pointers)
@@ -88,7 +88,7 @@ struct EvalParams {
   int32_t narrow;
   int32_t has_tri;
   const double* d3;
-  uint32_t d3mul;
+  uint32_t d3off;               // the dense class-3 table's bit window (lt_common.h d3_window)
   int32_t n_paths;
   int64_t n_words;
   const NodeRec* words;         // AoS word records

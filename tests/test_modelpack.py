@@ -105,3 +105,26 @@ def test_packed_model_decodes_golden_vectors(gpu_decoder, tmp_path, name):
                     assert path_matches(c, codes, m.sequences[1:-1])
                     checked += 1
     assert checked > 0 or name == 'base'
+
+
+@pytest.mark.parametrize('name', ['demo', 'base', 'scorers', 'dense'])
+def test_dense_class3_table_uses_a_bit_window(name):
+    """The dense class-3 table's index (lt_common.h d3_index) is a bit window
+    v[off, off + 5) of the interned tag id when one separates the model's
+    class-3 tag values (d3_window: the kernels then take it as one bit-field
+    extract): true for the reference's tag set, interned first."""
+    from lattice_based_tagger_amd import synth
+    for case in _models(name)[:3]:
+        lm = LoweredModel(case.funcs)
+        if not lm.has_trigram:
+            continue
+        mul = _capi.ModelImage(lm.keys, lm.coefs).arrays()['d3mul']
+        if mul:
+            assert mul & (mul - 1) == 0 and mul <= 1 << 27, (case.tag, hex(mul))
+    raw = synth.make_lattices(256, seed=3)
+    lay = synth.layout(raw)
+    cols = synth.node_columns(raw, lay)
+    sm = synth.make_model(raw, lay, cols, seed=3, n_features=20_000)
+    _, keys, coefs = synth.pack_fast(raw, sm, lay, cols)
+    mul = _capi.ModelImage(keys, coefs).arrays()['d3mul']
+    assert mul and mul & (mul - 1) == 0
