@@ -1494,9 +1494,10 @@ lt_viterbi_pk(DecodeParams p) {
     PK_STAMP(3);                                 // [3] wait for the primary slots
 #endif
     // primary slots back: hits; the next macro-step's records DMA'd, then the
-    // secondary loads of misses at flagged slots (one wait covers both).  The
-    // DMA comes after every LDS read of this step's scoring: an LDS read
-    // issued after a buffer->LDS DMA waits for it (vmcnt).
+    // secondary loads of misses at flagged slots (their wait covers the DMA
+    // too: VMEM completes in order).  Issued here, after the primary-slot
+    // wait, the DMA's HBM latency overlaps the checks, the secondaries, the
+    // sum and the argmax (K1_EARLY_DMA, K1_ASM_ATOMIC).
     const VEntry h1 = R[msr][act ? bm0 : 0];
     v1_check<NARROW>(P, B, slots, seed, h1, cur, aux);
 #if !K1_EARLY_DMA
@@ -1658,23 +1659,23 @@ lt_viterbi_pk(DecodeParams p) {
 // in the low 16 bits, the number of its hypotheses whose last word is not
 // Unknown in the high 16.  An implicit Unknown of span (b, e) with b > b_min
 // is skipped after every hypothesis whose last word is Unknown (num_unk
-// counts the Unknowns at the tail: beam.py:43-45, Sequence.add :112-113), so
-// its span slot expands only the others: the slot's expansions enumerate
-// them alone, in rank order (the ring's live-rank list, LR[b][q] = the rank
-// of the q-th), which keeps the generation order of the expansions scored.
+// counts the Unknowns at the tail: beam.py:43-45, Sequence.add :112-113).
 // (A position without explicit nodes has none: the k=1 schedule's static
 // rule, lt_internal.h k1_unk_dead.)
 constexpr int CNT_BEAM = 0xFFFF;
 __device__ __forceinline__ int cnt_entry(int beam, int live) { return beam | (live << 16); }
-// hypotheses of span slot d (<= dmax) that expand: beam[e - d]'s size, or its
-// non-Unknown hypotheses for an empty slot's implicit Unknown past b_min
+// HW_LIVE=1 (lt_beam_hw, measured slower): such a slot expands only the
+// hypotheses not ending in Unknown, enumerated in rank order through the
+// ring's live-rank list (LR[b][q] = the rank of the q-th), which keeps the
+// generation order of the expansions scored
 __device__ __forceinline__ int cnt_live(int cv, bool empty, int d, int dmax) {
   return (empty && d < dmax) ? (cv >> 16) : (cv & CNT_BEAM);
 }
-// lt_beam_pk (one sentence per wave, 64-lane rounds): such a slot expands all
-// of beam[e - d] unless none of it survives -- the per-expansion skip takes
-// the rest (a live-rank lookup in its expansion decode cost more than the
-// expansions it saved: k=16 10.55 -> 10.99 ms)
+// The shipped rule of both beam kernels: such a slot expands all of
+// beam[e - d] unless none of it survives -- the per-expansion skip takes the
+// rest (the live-rank lookup in the expansion decode cost more than the
+// expansions it saved: lt_beam_pk k=16 10.55 -> 10.99 ms, lt_beam_hw k=5
+// 3.75 -> 3.82 ms)
 __device__ __forceinline__ int cnt_any(int cv, bool empty, int d, int dmax) {
   return (empty && d < dmax && (cv >> 16) == 0) ? 0 : (cv & CNT_BEAM);
 }
