@@ -1,11 +1,11 @@
 # SQ counter set at the final source (the issue roofline's same_build), then the default bench line
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/evidence_r06c
+O=$R/gpurun_out/evidence_r06d
 mkdir -p $O
 cd $R
 export PYTHONUNBUFFERED=1
-OUT=evidence_r06c/sq LIBS=base KS="1 5 16" timeout -k 10 900 bash tools/gpu_sq_ab.sh > $O/sq.log 2>&1 || { echo SQ_FAIL; tail -20 $O/sq.log; exit 1; }
+OUT=evidence_r06d/sq LIBS=base KS="1 5 16" timeout -k 10 900 bash tools/gpu_sq_ab.sh > $O/sq.log 2>&1 || { echo SQ_FAIL; tail -20 $O/sq.log; exit 1; }
 mkdir -p $R/profiles/r06
 python3 $R/tools/sq_summary.py $O/sq base $R/profiles/r06/sq_summary.json || exit 1
 cp $R/profiles/r06/sq_summary.json $O/sq_summary.json
