@@ -177,31 +177,26 @@ struct Span {
   uint32_t off = 0, len = 0;
 };
 
-inline uint64_t seq_hash(const uint32_t* s, uint32_t n) {
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xC2B2AE3D27D4EB4Full);
+// Sequence hash in three parts, so that a common prefix is hashed once: the
+// state after a prefix (hs_feed from HS_INIT) continues with any suffix, and
+// the length is folded in at the end (the lemmatizer hashes the stem w[:i] +
+// each rule's stem, and each rule's eomi + the rest of the word).
+constexpr uint64_t HS_INIT = 0x9E3779B97F4A7C15ull;
+inline uint64_t hs_feed(uint64_t h, const uint32_t* s, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) {
     h ^= s[i];
     h *= 0xff51afd7ed558ccdull;
     h ^= h >> 29;
   }
+  return h;
+}
+inline uint64_t hs_final(uint64_t h, uint32_t n) {
+  h ^= (uint64_t)n * 0xC2B2AE3D27D4EB4Full;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 31;
   return h ^ (h >> 32);
 }
-
-// seq_hash of the concatenation a[0 .. na) + b[0 .. nb), without building it
-inline uint64_t seq_hash2(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb) {
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)(na + nb) * 0xC2B2AE3D27D4EB4Full);
-  for (uint32_t i = 0; i < na; ++i) {
-    h ^= a[i];
-    h *= 0xff51afd7ed558ccdull;
-    h ^= h >> 29;
-  }
-  for (uint32_t i = 0; i < nb; ++i) {
-    h ^= b[i];
-    h *= 0xff51afd7ed558ccdull;
-    h ^= h >> 29;
-  }
-  return h ^ (h >> 32);
-}
+inline uint64_t seq_hash(const uint32_t* s, uint32_t n) { return hs_final(hs_feed(HS_INIT, s, n), n); }
 
 class Table {
  public:
@@ -242,9 +237,9 @@ class Table {
       if (tag_of(v) == tag(h) && same(idx_of(v), s, n)) return &infos[idx_of(v)];
     return nullptr;
   }
-  // find() of the concatenation a + b
-  const Info* find2(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb) const {
-    const uint64_t h = seq_hash2(a, na, b, nb);
+  // find() of the concatenation a + b; ha = hs_feed(HS_INIT, a, na)
+  const Info* find2(uint64_t ha, const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb) const {
+    const uint64_t h = hs_final(hs_feed(ha, b, nb), na + nb);
     size_t i = (size_t)h & mask_;
     for (uint64_t v; (v = slots_[i]) != 0; i = (i + 1) & mask_) {
       if (tag_of(v) != tag(h)) continue;
@@ -287,6 +282,7 @@ class Table {
 
 struct RulePair {
   Span stem, eomi;            // in Table::pool
+  uint64_t eomi_hs = 0;       // hs_feed(HS_INIT, eomi): the prefix state of eomi + rest
 };
 
 struct Standalone {
@@ -387,14 +383,15 @@ struct Worker {
   }
 
   // consider() of stem s1 + s2, eomi e1 + e2: the two lookups run on the
-  // pieces; the candidate is copied only when both succeed
-  void consider_parts(const uint32_t* s1, uint32_t n1, const uint32_t* s2, uint32_t n2,
-                      const uint32_t* e1, uint32_t m1, const uint32_t* e2, uint32_t m2,
+  // pieces (s1h, e1h: the hash prefix states of s1, e1); the candidate is
+  // copied only when both succeed
+  void consider_parts(uint64_t s1h, const uint32_t* s1, uint32_t n1, const uint32_t* s2, uint32_t n2,
+                      uint64_t e1h, const uint32_t* e1, uint32_t m1, const uint32_t* e2, uint32_t m2,
                       uint32_t w_off, uint32_t m, int32_t len, int32_t b, int32_t e, bool is_l,
                       std::vector<WordRec>& out) {
-    const Info* ei = lx.table.find2(e1, m1, e2, m2);
+    const Info* ei = lx.table.find2(e1h, e1, m1, e2, m2);
     if (!ei || !(ei->flags & F_EOMI)) return;
-    const Info* si = lx.table.find2(s1, n1, s2, n2);
+    const Info* si = lx.table.find2(s1h, s1, n1, s2, n2);
     if (!si || !(si->flags & (F_ADJ | F_VERB))) return;
     set_cand(s1, n1, s2, n2, e1, m1, e2, m2);
     consider(w_off, m, len, b, e, is_l, out);
@@ -427,7 +424,8 @@ struct Worker {
     const uint32_t* w = text + w_off;
     const std::vector<RulePair>& R = lx.rules;
     const uint32_t* P = lx.table.pool.data();
-    for (uint32_t i = 0; i < m; ++i) {
+    uint64_t wh = HS_INIT;                       // hs_feed(HS_INIT, w, i): the stem prefix w[:i]
+    for (uint32_t i = 0; i < m; wh = hs_feed(wh, w + i, 1), ++i) {
       // (l, r) = (word[:i+1], word[i+1:]), while i < max_i
       if (i + 1 < m) consider_text(w_off, i + 1, m - i - 1, w_off, m, len, b, e, is_l, out);
       // 1 syllable conjugation: the pairs of rules[c], |rules[c]| times over
@@ -437,8 +435,8 @@ struct Worker {
         const size_t first = out.size();
         for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
           const RulePair& rp = R[(size_t)q];
-          consider_parts(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, w + i + 1,
-                         m - i - 1, w_off, m, len, b, e, is_l, out);
+          consider_parts(wh, w, i, P + rp.stem.off, rp.stem.len, rp.eomi_hs, P + rp.eomi.off, rp.eomi.len,
+                         w + i + 1, m - i - 1, w_off, m, len, b, e, is_l, out);
         }
         const size_t pass = out.size() - first;
         if (pass) out.reserve(out.size() + pass * (size_t)(ci->rule_n - 1));
@@ -461,8 +459,8 @@ struct Worker {
         if (!ci) continue;
         for (int32_t q = ci->rule_lo; q < ci->rule_lo + ci->rule_n; ++q) {
           const RulePair& rp = R[(size_t)q];
-          consider_parts(w, i, P + rp.stem.off, rp.stem.len, P + rp.eomi.off, rp.eomi.len, rest, nrest,
-                         w_off, m, len, b, e, is_l, out);
+          consider_parts(wh, w, i, P + rp.stem.off, rp.stem.len, rp.eomi_hs, P + rp.eomi.off, rp.eomi.len, rest,
+                         nrest, w_off, m, len, b, e, is_l, out);
         }
       }
     }
@@ -801,6 +799,7 @@ lt_status lt_lexicon_create(const lt_lexicon_desc* d, lt_lexicon** out) {
       if (!decode(d->rule_eomi, q)) return lt::set_error(LT_EINVAL, "lt_lexicon_create: bad UTF-8");
       rp.eomi = Span{(uint32_t)tab.pool.size(), (uint32_t)cp.size()};
       tab.pool.insert(tab.pool.end(), cp.begin(), cp.end());
+      rp.eomi_hs = hs_feed(HS_INIT, cp.data(), (uint32_t)cp.size());
       lx->rules.push_back(rp);
     }
     if (!decode(d->rule_surface, r)) return lt::set_error(LT_EINVAL, "lt_lexicon_create: bad UTF-8");
