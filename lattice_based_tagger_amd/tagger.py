@@ -16,6 +16,7 @@ Decoding runs on the device.
 
 import gc
 import sys
+import time
 
 from .beam import beam_search_batch
 from .tagset import Adjective, Adverb, Determiner, Exclamation, Noun, Number, Verb
@@ -134,6 +135,7 @@ class Tagger:
         self._lexicon_given = lexicon is not None     # used as given, never rebuilt
         self._eojeol_lookup = None
         self.lookup_threads = lookup_threads
+        self.last_stats = None                     # tag_batch's stage times of its last pipelined call
         if custom_lookup is not None:
             if not callable(custom_lookup):
                 raise TypeError('custom_lookup must be a callable (eojeol, offset) -> [Word]')
@@ -276,7 +278,9 @@ class Tagger:
                     raise IndexError('list index out of range')        # beam.py:32 on bindex == []
             return lat
 
+        t_call = time.perf_counter()
         lat0 = lookup(chunks[0])                   # (the reference raises before scoring)
+        lat0_s = time.perf_counter() - t_call
         model = lowered_model(self.score_funcs)
         npk = packer_for(model)
         decs = None
@@ -327,13 +331,24 @@ class Tagger:
                                                                 decoder=decoder(i))
 
         out = []
+        # where the caller's time goes (last_stats): blocked on the decode
+        # stage, building Sequences; the builder's own lookup + pack time
+        st = {'chunks': len(chunks), 'lat0_s': lat0_s, 'wait_s': 0.0, 'objects_s': 0.0, 'front_s': 0.0,
+              'first_chunk_s': 0.0}
+        self.last_stats = st
+
+        def front_timed(chunk, lat=None):
+            t = time.perf_counter()
+            r = front(chunk, lat)
+            st['front_s'] += time.perf_counter() - t
+            return r
         with ThreadPoolExecutor(max_workers=1) as builder, ThreadPoolExecutor(max_workers=1) as uploader, \
                 ThreadPoolExecutor(max_workers=1) as decoding:
             stages = deque()
 
             def feed(i):
                 if i < len(chunks):
-                    up = uploader.submit(upload, i, builder.submit(front, chunks[i], lat0 if i == 0 else None))
+                    up = uploader.submit(upload, i, builder.submit(front_timed, chunks[i], lat0 if i == 0 else None))
                     stages.append((up, decoding.submit(decode, i, up)))
             feed(0)
             feed(1)
@@ -341,12 +356,18 @@ class Tagger:
             try:
                 for i in range(len(chunks)):
                     _, dfut = stages.popleft()
+                    t = time.perf_counter()
                     _, lat, packed, views, dbs, prep = dfut.result()
+                    t1 = time.perf_counter()
+                    st['wait_s'] += t1 - t
+                    if i == 0:
+                        st['first_chunk_s'] = t1 - t_call
                     feed(i + 3)
                     if prep is None:
                         out += finish(i, lat, packed, views, dbs)
                     else:
                         out += [m[0] for m in materialise_prepared(prep)]
+                    st['objects_s'] += time.perf_counter() - t1
             finally:
                 for up, dfut in stages:            # an error: drop what is still in flight
                     dfut.cancel()

@@ -81,6 +81,8 @@ def main():
     # later call)
     tagger.tag_batch(sents[:5 * Tagger.CHUNK], beam_size=a.k)
 
+    call_stats = []
+
     def api_calls():
         times = []
         out = None
@@ -90,6 +92,9 @@ def main():
             t0 = time.perf_counter()
             out = tagger.tag_batch(sents, beam_size=a.k)
             times.append(time.perf_counter() - t0)
+            st = dict(tagger.last_stats or {})
+            st['call_s'] = times[-1]
+            call_stats.append({key: round(v, 4) if isinstance(v, float) else v for key, v in st.items()})
         return times, out
     if a.api_first:
         api_times, out = api_calls()
@@ -146,6 +151,7 @@ def main():
             'phase_s': best, 'sentences_per_s': {p: len(sents) / v for p, v in best.items()},
             'tag_batch_api_sentences_per_s': len(sents) / api,
             'tag_batch_api_runs_sentences_per_s': [len(sents) / t for t in api_times],
+            'tag_batch_api_call_stats': call_stats,
             'lookup_threads': a.threads or os.cpu_count(), 'nproc': os.cpu_count(), 'api_first': a.api_first}
     print(json.dumps(line))
 
