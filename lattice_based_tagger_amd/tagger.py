@@ -222,10 +222,14 @@ class Tagger:
             matures = beam_search_batch(lattices, self.score_funcs, beam_size=beam_size,
                                         device=self.device)
             return [m[0] for m in matures]
+        self.last_stats = None
         enabled = gc.isenabled()
         gc.disable()
         try:
-            return self._tag_native(lex, sents, beam_size)
+            out = self._tag_native(lex, sents, beam_size)
+            if self.last_stats is not None and 't_end' in self.last_stats:
+                self.last_stats['teardown_s'] = time.perf_counter() - self.last_stats.pop('t_end')
+            return out
         finally:
             if enabled:
                 gc.enable()
@@ -384,4 +388,14 @@ class Tagger:
                             dfut.result()
                         except BaseException:
                             pass
+                st['loop_s'] = time.perf_counter() - t_call
+        t = time.perf_counter()
+        st['inside_s'] = t - t_call
+        # the last chunk's lattice, pack and prepared paths (its decode
+        # future holds them) and chunk 0's lattice, released here and timed:
+        # after a phase that freed gigabytes this release took 0.17-0.23 s
+        # (profiles/r06/tagger_calls/)
+        lat = packed = views = dbs = prep = dfut = lat0 = None
+        st['t_end'] = time.perf_counter()
+        st['release_s'] = st['t_end'] - t
         return out

@@ -92,8 +92,12 @@ def main():
             t0 = time.perf_counter()
             out = tagger.tag_batch(sents, beam_size=a.k)
             times.append(time.perf_counter() - t0)
+            t1 = time.perf_counter()
+            gc.collect()                          # (untimed: what the call left for the collector)
+            gc_s = time.perf_counter() - t1
             st = dict(tagger.last_stats or {})
             st['call_s'] = times[-1]
+            st['gc_after_s'] = gc_s
             call_stats.append({key: round(v, 4) if isinstance(v, float) else v for key, v in st.items()})
         return times, out
     if a.api_first:
@@ -110,7 +114,9 @@ def main():
         packed, views = npk.pack_lattices(lat, max_len=8)        # (as Tagger.tag_batch packs)
         t['pack'] = time.perf_counter() - t0
         t0 = time.perf_counter()
-        dec = Decoder.get(0)
+        # (a context of its own, so that this 64K-sentence batch's arena
+        # stays out of the pool of the context the tag_batch calls use)
+        dec = Decoder.get(0, 1)
         dm = dec.device_model(model)
         dbs = [_capi.DeviceBatch(dec.ctx, packed, max_k=a.k)]
         t['batch_create_h2d'] = time.perf_counter() - t0
@@ -126,7 +132,7 @@ def main():
         t['decode_d2h'] = time.perf_counter() - t0
         t['kernel_only'] = kern
         t0 = time.perf_counter()
-        matures = decode_batch(packed, views, lat.chars, model, a.k, 0, best_only=True)
+        matures = decode_batch(packed, views, lat.chars, model, a.k, 0, best_only=True, decoder=dec)
         t['decode_and_materialise_best'] = time.perf_counter() - t0
         t['total'] = t['lookup'] + t['pack'] + t['decode_and_materialise_best']
         if not best or t['total'] < best['total']:
